@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""bench.py — frames/s and Mrays/s of the MI355X ray tracer (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--kernel auto]
+
+A step is one frame of the reference's GPU render loop (src/main.cpp:325-370):
+per-frame camera + light upload (SSBO 2/1), the render dispatch, completion,
+and for N > 1 the RCCL fan-in of every rank's rows to rank 0 (one process per
+GPU, launched by torch.distributed.run). Default workload: config 3, the car
+scene (4,022 triangles + 100 spheres, reference BVH with the 2-triangle road),
+1920x1080, maxBounces 3, barycentric, no Fresnel. All N ranks render one frame
+together (interleaved 8-row stripes), so the total work per step is fixed:
+scaling "strong".
+
+value = Mrays/s = (closest-hit + shadow rays of the frame, counted on the
+reference walk by the counting kernel) x frames / s, summed over the job.
+Rank 0 prints one JSON line with the roofline of the render kernel and the CPU
+baseline (the oracle, OpenMP on host cores, on a bounded row sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
+import rtamd  # noqa: E402
+import tiling  # noqa: E402
+
+METRIC = "Mrays/sec + FPS @1920x1080, car scene (4122 shapes), 1/2/4/8 GPUs"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+# config -> (scene generator config, width, height, maxBounces, description)
+WORKLOADS = {
+    2: (2, 800, 600, 1, "monkey stand-in (1,240 shapes), 800x600, primary + shadow"),
+    3: (3, 1920, 1080, 3, "car stand-in (4,022 triangles + 100 spheres), 1920x1080, reflection depth 3"),
+    4: (3, 3840, 2160, 3, "car stand-in, 3840x2160"),
+    5: (5, 1920, 1080, 3, "100k random triangles, deep BVH, 1920x1080"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=3, choices=sorted(WORKLOADS))
+    ap.add_argument("--variant", type=int, default=0, help="car road: 0 = 2-triangle quad, 1 = 222 strips")
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet"])
+    ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    return ap.parse_args()
+
+
+def cpu_baseline(fs, W, H, mb, seconds, threads):
+    """The oracle (oracle/rt_oracle.c, the GLSL restated, OpenMP) on a band of
+    rows through the middle of the same frame; the band grows until the
+    measurement takes roughly `seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg only)
+    p = oracle.params(W, H, mb)
+    rows = 8
+    while True:
+        y0 = max(0, H // 2 - rows // 2)
+        t0 = time.perf_counter()
+        _, st = oracle.render(fs, W, H, p, y0=y0, out_rows=rows, stats=True, threads=threads)
+        dt = time.perf_counter() - t0
+        if dt >= seconds * 0.5 or rows >= H:
+            break
+        rows = min(H, max(rows * 2, int(rows * seconds / max(dt, 1e-3) * 0.9)))
+    rays = st["closest_rays"] + st["shadow_rays"]
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (GLSL restated, OpenMP) rows [{y0},{y0 + rows}) of the same {W}x{H} frame: "
+                      f"{rows * W} pixels, {rays} rays in {dt:.2f} s",
+            "ms_per_frame_equiv": dt * 1e3 * H / rows,
+            "cpu": platform.processor() or platform.machine()}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    # One non-default stream shared by torch (RCCL waits on it) and the renderer.
+    torch.cuda.set_stream(torch.cuda.Stream())
+
+    cfg, W, H, mb, desc = WORKLOADS[a.config]
+    fs = rtamd.generate(cfg, a.variant, W, H)
+    sc_stats = rtamd.Scene().generate(cfg, a.variant, W / H).bvh_stats()
+
+    ctx = rtamd.ComputeShader(torch.cuda.current_device())
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True, False, False)
+    ctx.set_kernel({"auto": 0, "lane": 1, "packet": 2}[a.kernel])
+
+    plan = tiling.StripePlan(H, world, a.stripe)
+    rows = plan.rows(rank)
+    buf = torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev)
+
+    # Work of this rank's rows on the reference walk (counting kernel, untimed).
+    st = ctx.collect_stats(W, H, plan.y0(rank), a.stripe, world, rows)
+    mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, rows * W), st["hits"]],
+                        dtype=torch.float64, device=dev)
+    total = mine.clone()
+    if world > 1:
+        dist.all_reduce(total)
+    rays_frame = float(total[0] + total[1])
+    b_alg_rank = float(mine[2])
+
+    cam, light = fs.camera, fs.light
+
+    def frame():
+        ctx.set_camera(cam)   # SSBO 2 (src/main.cpp:328-330)
+        ctx.set_light(light)  # SSBO 1 (:332-334)
+        ctx.dispatch_rows(W, H, plan.y0(rank), a.stripe, world, rows, buf.data_ptr(), W * 16)
+        if world > 1:
+            tiling.gather_to_root(buf, plan)
+
+    for _ in range(a.warmup):
+        frame()
+    torch.cuda.synchronize()
+    ctx.kernel_times()  # drop warm-up dispatches
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        frame()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el[0])
+
+    kt = ctx.kernel_times()
+    k_ms = float(np.mean(kt)) if len(kt) else float("nan")
+    k_med = float(np.median(kt)) if len(kt) else float("nan")
+
+    if rank == 0:
+        fps = a.steps / elapsed
+        achieved = b_alg_rank / (k_ms * 1e-3) / 1e9
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                traffic = json.load(f).get(f"config{a.config}_n{world}_{a.kernel}")
+        out = {
+            "metric": METRIC,
+            "value": rays_frame * fps / 1e6,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": elapsed / a.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural stand-in meshes, fixed seed; the reference's .obj assets are absent)",
+            "config": {"workload": f"config {a.config}: {desc}" + (" (222-strip road)" if a.variant else ""),
+                       "width": W, "height": H, "maxBounces": mb, "useBVH": 1, "useFresnel": 0,
+                       "triangle_test": "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
+                       "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel,
+                       "parallelism": f"row-stripes{a.stripe}x{world}" + ("+rccl-gather" if world > 1 else "")},
+            "fps": fps,
+            "mrays_primary_per_s": W * H * fps / 1e6,
+            "rays_per_frame": rays_frame,
+            "kernel_ms_mean": k_ms,
+            "kernel_ms_median": k_med,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": b_alg_rank,
+                "kernel": "k_packet" if a.kernel in ("auto", "packet") else "k_lane",
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu:
+            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(fs, W, H, mb, a.cpu_seconds, thr)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,143 @@
+/*
+ * rt_api.h — C ABI of the MI355X renderer (librtamd.so).
+ *
+ * This is the drop-in for the reference's GPU operator boundary: the GL compute
+ * program, its SSBO bindings, its uniforms and glDispatchCompute. Each entry
+ * point names the reference call it replaces. Plain pointers and sizes only;
+ * every function returns an int status (RT_OK = 0, negative on error) and never
+ * throws across the boundary (the reference prints shader errors and carries
+ * on, src/computeShader.hpp:64-79; here the caller gets a code).
+ *
+ * Threading: one rt_ctx per device. A context is not thread-safe; different
+ * contexts may be driven from different threads. All work of a context is
+ * ordered on one HIP stream (its own, or the caller's via rt_set_stream).
+ */
+#ifndef RT_API_H
+#define RT_API_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "rt_flat.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct rt_ctx; /* opaque: one per device */
+
+enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID = -1,   /* bad argument (null pointer, negative size, bad rows)   */
+    RT_ERR_DEVICE = -2,    /* a HIP runtime call failed                              */
+    RT_ERR_NO_MEMORY = -3, /* device allocation failed                               */
+    RT_ERR_NO_SCENE = -4,  /* dispatch before rt_upload_scene / camera / light       */
+    RT_ERR_BVH = -5,       /* node/index arrays are out of range or too deep         */
+    RT_ERR_NO_DEVICE = -6  /* no HIP device with that ordinal                        */
+};
+
+/* Uniforms of gpu_shader.comp:126-130, set by src/main.cpp:357-361.
+ * Applied AT the next dispatch (the reference sets them after the dispatch, so
+ * its frame k uses frame k-1's values and frame 0 uses zeros). */
+typedef struct rt_params {
+    float resX, resY;        /* screenRes; pixel NDC and background use these        */
+    int maxBounces;          /* closest-hit bounces per pixel, >= 0                  */
+    int useBVH;              /* 1: BVH traversal branch, 0: brute-force branch       */
+    int useFresnel;          /* Fresnel-weighted reflections                         */
+    int useMollerTrumbore;   /* triangle test: 1 Moller-Trumbore, 0 barycentric      */
+} rt_params;
+
+/* Traversal kernel variants (all produce the same image). */
+enum rt_kernel {
+    RT_KERNEL_AUTO = 0,      /* pick the fastest for the uploaded scene               */
+    RT_KERNEL_LANE = 1,      /* one ray per lane, per-lane LDS stack (reference walk) */
+    RT_KERNEL_PACKET = 2     /* wave64 packet walk, wave-uniform stack + active mask  */
+};
+
+/* Work counted on the reference's own traversal (gpu_shader.comp:380-430 and
+ * :523-580) — what the reference shader would load. Filled by
+ * rt_collect_stats; used for Mrays/s and the algorithmic-bytes roofline. */
+typedef struct rt_stats {
+    uint64_t pixels;              /* pixels shaded                                  */
+    uint64_t closest_rays;        /* closest-hit traversals (primary + reflection)  */
+    uint64_t shadow_rays;         /* shadow traversals                              */
+    uint64_t node_visits;         /* FlatNode records popped and box-tested         */
+    uint64_t bvh_tests[4];        /* leaf primitive tests by type (BVH branch)      */
+    uint64_t brute_tests[4];      /* primitive tests by type (brute-force branch)   */
+    uint64_t closest_updates;     /* closest-hit record updates (material fetches)  */
+    uint64_t hits;                /* bounces that hit a shape                       */
+} rt_stats;
+
+/* ComputeShader("gpu_shader.comp") + the RGBA32F image (src/computeShader.hpp:30-83,
+ * src/main.cpp:182-195). Selects HIP device `device`. */
+int rt_create(struct rt_ctx** out, int device);
+int rt_destroy(struct rt_ctx* ctx);
+
+/* Order all work of the context on a caller stream (hipStream_t; NULL = own stream). */
+int rt_set_stream(struct rt_ctx* ctx, void* hip_stream);
+
+/* SSBO 3 (shapes), 4 (nodes), 5 (bvhIndices) (src/main.cpp:256-275). The root
+ * is node N-1 as in gpu_shader.comp:386. Copies to HBM and re-lays the records
+ * out for the kernels; the caller keeps ownership. N == 0 is allowed (the BVH
+ * branch then sees no shape). Returns RT_ERR_BVH for child/index out of range. */
+int rt_upload_scene(struct rt_ctx* ctx, const FlatShape* shapes, int num_shapes,
+                    const FlatNode* nodes, int num_nodes, const int* indices, int num_indices);
+
+/* Partial re-upload of shapes [first, first+count) (src/main.cpp:981-992, updateScene). */
+int rt_update_shapes(struct rt_ctx* ctx, int first, int count, const FlatShape* shapes);
+
+/* Re-upload of all nodes with the same topology (src/main.cpp:340-345, updateBVH). */
+int rt_update_nodes(struct rt_ctx* ctx, const FlatNode* nodes, int num_nodes);
+
+/* SSBO 2 and 1 (src/main.cpp:328-334). */
+int rt_set_camera(struct rt_ctx* ctx, const FlatCamera* camera);
+int rt_set_light(struct rt_ctx* ctx, const FlatLight* light);
+
+/* The five uniforms (src/main.cpp:357-361). */
+int rt_set_params(struct rt_ctx* ctx, const rt_params* params);
+
+/* Kernel variant; RT_KERNEL_AUTO by default. */
+int rt_set_kernel(struct rt_ctx* ctx, int kernel);
+
+/* glDispatchCompute(W,H,1) + glMemoryBarrier (src/main.cpp:352-354) into the
+ * context's own W x H RGBA32F surface, rows [y0, y1). Stream-ordered, async. */
+int rt_dispatch(struct rt_ctx* ctx, int width, int height, int y0, int y1);
+
+/* Same into a caller-owned device surface (for tiling and RCCL gathers).
+ * Row-stripe mapping: output row r (0-based, r < out_rows) holds image row
+ *   y = y0 + (r / stripe) * stripe * step + (r % stripe)
+ * so step = 1 renders the contiguous band [y0, y0+out_rows) and step = P with
+ * y0 = k*stripe renders the k-th of P interleaved stripe sets. Rows with
+ * y >= height are left untouched. `pitch` is in bytes (>= 16*width). */
+int rt_dispatch_rows(struct rt_ctx* ctx, int width, int height, int y0, int stripe,
+                     int step, int out_rows, float* dst, size_t pitch);
+
+/* glMemoryBarrier + wait: blocks until the context's stream is drained. */
+int rt_sync(struct rt_ctx* ctx);
+
+/* Read the context surface back to host memory (rows [0,height), `pitch` bytes). */
+int rt_read_image(struct rt_ctx* ctx, float* host_dst, size_t pitch);
+
+/* Device pointer and pitch of the context surface (zero-copy hand-off). */
+int rt_device_image(struct rt_ctx* ctx, void** ptr, size_t* pitch);
+
+/* Runs the counting variant of the reference traversal over the same rows as
+ * rt_dispatch_rows and returns the totals (synchronous; not for timed loops). */
+int rt_collect_stats(struct rt_ctx* ctx, int width, int height, int y0, int stripe,
+                     int step, int out_rows, rt_stats* out);
+
+/* Device time of the last render kernel in ms (HIP events on the context stream). */
+int rt_last_kernel_ms(struct rt_ctx* ctx, float* ms);
+
+/* Device times (ms) of the render dispatches issued since the previous call
+ * (up to 1024 are kept), written to ms[0..min(n,cap)). Returns n >= 0 and
+ * restarts the record. Waits for those dispatches to finish. */
+int rt_kernel_times(struct rt_ctx* ctx, float* ms, int cap);
+
+/* Human-readable status string. */
+const char* rt_status_string(int status);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_API_H */

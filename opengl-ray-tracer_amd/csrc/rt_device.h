@@ -1,0 +1,238 @@
+// rt_device.h — device-side scene layout and the per-ray primitives shared by
+// every render kernel. Included by rt_kernels.hip only.
+//
+// All arithmetic follows the reference shader (src/shaders/gpu_shader.comp)
+// with glm's operation order (dot = (x+y)+z, normalize = v*(1/sqrt(v.v)),
+// reflect = I - N*dot(N,I)*2, mix = x+a*(y-x)); the file is compiled with
+// -ffp-contract=off and IEEE div/sqrt so a pixel's discrete decisions (hit or
+// miss, shadowed or lit, which shape is closest) are those of the CPU oracle.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rtd {
+
+// ---------------------------------------------------------------------------
+// HBM layout (built on device by the pack kernels from the uploaded FlatShape
+// / FlatNode records; see DESIGN.md "Data layout in HBM").
+//
+// Shape record: 80 B = 5 x float4, one per shape, stored twice: in shape order
+// (brute-force branch) and in leaf order, i.e. geo_leaf[j] is the shape
+// bvhIndices[j], so a leaf scan is a contiguous stream and the index
+// indirection of gpu_shader.comp:404 is paid once at upload.
+//   w0 = type (int bits), w1 = shape index (int bits), f[0..17] = payload:
+//   sphere   : f0-2 centre, f3 radius
+//   plane    : f0-2 normal, f3 D
+//   wall     : f0-2 normal, f3 D, f4-6 start, f7 width, f8 height,
+//              f9-11 u axis, f12-14 v axis (gpu_shader.comp:305-307, precomputed)
+//   triangle : f0-2 normal, f3 D, f4-6 P1, f7-9 E1=P2-P1, f10-12 E2=P3-P1,
+//              f13 d00, f14 d01, f15 d11, f16 denom (gpu_shader.comp:218-229)
+// Material: 32 B = 2 x float4 per shape index: color.xyz, fresnel |
+//   ambient, diffuse, specular, float(shininess).
+// Node: 32 B = 2 x float4: bmin.xyz, a | bmax.xyz, b (int bits);
+//   inner: a = left, b = right; leaf: a = -(start+1), b = numShapes.
+struct GeoRec {
+    int type, idx;
+    float f[18];
+};
+static_assert(sizeof(GeoRec) == 80, "GeoRec is 5 float4");
+
+struct V {
+    float x, y, z;
+};
+__device__ __forceinline__ V mk(float x, float y, float z) { return V{x, y, z}; }
+__device__ __forceinline__ V operator+(V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V operator-(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V operator-(V a) { return V{-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ V operator*(V a, float s) { return V{a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ V operator*(float s, V a) { return V{s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ V mulv(V a, V b) { return V{a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V divs(V a, float s) { return V{a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ V cross(V a, V b) {
+    return V{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
+}
+__device__ __forceinline__ float len(V a) { return __builtin_sqrtf(dot(a, a)); }
+__device__ __forceinline__ V normalize(V a) { return a * (1.0f / __builtin_sqrtf(dot(a, a))); }
+__device__ __forceinline__ float dist(V a, V b) { return len(b - a); }
+__device__ __forceinline__ V reflect(V i, V n) { return i - (n * dot(n, i)) * 2.0f; }
+__device__ __forceinline__ V mix(V x, V y, float a) { return x + a * (y - x); }
+__device__ __forceinline__ float gmax(float a, float b) { return (a < b) ? b : a; }  // GLSL/glm max
+__device__ __forceinline__ float gmin(float a, float b) { return (b < a) ? b : a; }  // GLSL/glm min
+
+enum { NONE = 0, INNER = 1, OUTER = 2 };
+
+struct Ray {
+    V o, d;
+};
+
+// Everything a render kernel needs, passed by value.
+struct KParams {
+    const float4* __restrict__ geo_leaf;  // I records
+    const float4* __restrict__ geo_lin;   // S records
+    const float4* __restrict__ mat;       // S materials
+    const float4* __restrict__ nodes;     // N nodes
+    int S, N, I;
+    int max_stack;                        // reference walk's stack need (host-computed)
+    V cam_pos, cam_front, cam_right, cam_up;
+    float plane_w, plane_h;               // imagePlaneWidth/Height (gpu_shader.comp:156-157)
+    V light_pos, light_color;
+    float resX, resY;
+    int maxBounces, useBVH, useFresnel, useMT;
+    int width, height, y0, stripe, step, out_rows;
+    char* __restrict__ dst;
+    size_t pitch;
+    unsigned long long* __restrict__ stats;  // rt_stats layout, STATS kernels only
+};
+
+// Row mapping of rt_dispatch_rows (include/rt_api.h).
+__device__ __forceinline__ int image_row(const KParams& kp, int r) {
+    return kp.y0 + (r / kp.stripe) * kp.stripe * kp.step + (r % kp.stripe);
+}
+
+// getRay (gpu_shader.comp:155-168); imagePlaneHeight/Width come from the host
+// (same tanf as the oracle) since they are per-frame constants.
+__device__ __forceinline__ Ray get_ray(const KParams& kp, float ndcX, float ndcY) {
+    V p = ((kp.cam_pos + kp.cam_front) + (ndcX * kp.plane_w / 2.0f) * kp.cam_right) +
+          (ndcY * kp.plane_h / 2.0f) * kp.cam_up;
+    return Ray{kp.cam_pos, normalize(p - kp.cam_pos)};
+}
+
+// Result of one primitive test. Only INNER hits matter to every caller.
+struct Hit {
+    int type;
+    V p;
+};
+
+// get_intersection (gpu_shader.comp:242-328) on a packed record.
+//   sphere :246-271, plane :272-286, wall :287-316,
+//   triangle barycentric :196-240 / Moller-Trumbore :170-195.
+__device__ __forceinline__ Hit intersect(const GeoRec& g, const Ray& r, int use_mt) {
+    Hit h{NONE, V{0.f, 0.f, 0.f}};
+    const float* f = g.f;
+    if (g.type == 0) {
+        V c = mk(f[0], f[1], f[2]);
+        V oc = r.o - c;
+        float aa = dot(r.d, r.d);
+        float bb = 2.0f * dot(r.d, oc);
+        float cc = dot(oc, oc) - f[3] * f[3];
+        float D = bb * bb - 4.0f * aa * cc;
+        if (D > 0.0f) {
+            float sD = __builtin_sqrtf(D);
+            float t1 = (-bb - sD) / (2.0f * aa);
+            if (t1 > 0.0f) {
+                h.type = INNER;
+                h.p = r.o + t1 * r.d;
+            }
+            // t2 > 0 is OUTER (:263-268): never used, not computed.
+        }
+        return h;
+    }
+    if (g.type < 1 || g.type > 3) return h;
+    if (g.type == 3 && use_mt) {
+        V p1 = mk(f[4], f[5], f[6]), e1 = mk(f[7], f[8], f[9]), e2 = mk(f[10], f[11], f[12]);
+        V hh = cross(r.d, e2);
+        float a = dot(e1, hh);
+        if (__builtin_fabsf(a) < 1e-5f) return h;
+        float fi = 1.0f / a;
+        V s = r.o - p1;
+        float u = fi * dot(s, hh);
+        if (u < 0.0f || u > 1.0f) return h;
+        V q = cross(s, e1);
+        float v = fi * dot(r.d, q);
+        if (v < 0.0f || u + v > 1.0f) return h;
+        float t = fi * dot(e2, q);
+        if (t > 0.0f) {
+            h.type = INNER;
+            h.p = r.o + t * r.d;
+        }
+        return h;
+    }
+    // plane test shared by plane, wall and barycentric triangle
+    V n = mk(f[0], f[1], f[2]);
+    float np = dot(n, r.d);
+    if (np == 0.0f) return h;
+    float t = -(f[3] + dot(n, r.o)) / np;
+    if (!(t > 0.0f) || !(np > 0.0f)) return h;  // t<=0: NONE; np<=0: OUTER
+    V p = r.o + t * r.d;
+    if (g.type == 2) {
+        V lp = p - mk(f[4], f[5], f[6]);
+        float up = dot(lp, mk(f[9], f[10], f[11]));
+        float vp = dot(lp, mk(f[12], f[13], f[14]));
+        if (up < 0.0f || up > f[7] || vp < 0.0f || vp > f[8]) return h;
+    } else if (g.type == 3) {
+        V tp = p - mk(f[4], f[5], f[6]);
+        float d20 = dot(tp, mk(f[7], f[8], f[9]));
+        float d21 = dot(tp, mk(f[10], f[11], f[12]));
+        float v = (f[15] * d20 - f[14] * d21) / f[16];
+        float w = (f[13] * d21 - f[14] * d20) / f[16];
+        float u = 1.0f - v - w;
+        if (u < 0.0f || v < 0.0f || w < 0.0f) return h;
+    }
+    h.type = INNER;
+    h.p = p;
+    return h;
+}
+
+// getNormalFromShape (gpu_shader.comp:64-71).
+__device__ __forceinline__ V shape_normal(const GeoRec& g, V p) {
+    if (g.type == 0) return normalize(p - mk(g.f[0], g.f[1], g.f[2]));
+    return mk(g.f[0], g.f[1], g.f[2]);
+}
+
+struct Mat {
+    V color;
+    float fresnel, ambient, diffuse, specular, shininess;
+};
+
+__device__ __forceinline__ Mat load_mat(const float4* __restrict__ mat, int idx) {
+    float4 a = mat[2 * idx], b = mat[2 * idx + 1];
+    return Mat{mk(a.x, a.y, a.z), a.w, b.x, b.y, b.z, b.w};
+}
+
+// phong (gpu_shader.comp:331-361).
+__device__ __forceinline__ V phong(V p, V n, V view, V lpos, V lcol, const Mat& m) {
+    float dl = dist(lpos, p);
+    V lc = divs(lcol, dl);
+    V amb = m.ambient * lc;
+    V ldir = normalize(lpos - p);
+    float diff = gmax(dot(n, ldir), 0.0f);
+    V dif = (m.diffuse * diff) * lc;
+    V spc = mk(0.f, 0.f, 0.f);
+    if (diff > 0.0f) {
+        V rd = reflect(-ldir, n);
+        float sp = powf(gmax(dot(view, rd), 0.0f), m.shininess);
+        spc = (m.specular * sp) * lc;
+    }
+    return mulv((amb + dif) + spc, m.color);
+}
+
+// rayIntersectsAABB (gpu_shader.comp:364-377); inv computed once per ray.
+__device__ __forceinline__ bool ray_aabb(V o, V inv, V bmin, V bmax) {
+    V t0 = mulv(bmin - o, inv), t1 = mulv(bmax - o, inv);
+    float lx = gmin(t0.x, t1.x), ly = gmin(t0.y, t1.y), lz = gmin(t0.z, t1.z);
+    float hx = gmax(t0.x, t1.x), hy = gmax(t0.y, t1.y), hz = gmax(t0.z, t1.z);
+    float tmin = gmax(gmax(lx, ly), lz);
+    float tmax = gmin(gmin(hx, hy), hz);
+    return tmax >= tmin && tmax > 0.0f;
+}
+
+__device__ __forceinline__ V inv_dir(V d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+
+__device__ __forceinline__ GeoRec load_rec(const float4* __restrict__ base, int j) {
+    GeoRec g;
+    float4* dst = reinterpret_cast<float4*>(&g);
+    const float4* src = base + 5 * static_cast<size_t>(j);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) dst[k] = src[k];
+    return g;
+}
+
+// Writes the pixel for output row r, column x.
+__device__ __forceinline__ void store_px(const KParams& kp, int r, int x, float4 v) {
+    float4* row = reinterpret_cast<float4*>(kp.dst + static_cast<size_t>(r) * kp.pitch);
+    row[x] = v;
+}
+
+}  // namespace rtd

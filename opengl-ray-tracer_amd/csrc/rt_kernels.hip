@@ -1,0 +1,984 @@
+// rt_kernels.hip — the MI355X (gfx950) render kernels and the C ABI of
+// include/rt_api.h (librtamd.so).
+//
+// Kernels
+//   k_pack_shapes / k_pack_nodes : AoS FlatShape/FlatNode (the reference's SSBO
+//       records) -> the HBM layout of rt_device.h (run once per upload).
+//   k_lane<STATS>   : one ray per lane walking the reference's own traversal
+//       (stack in LDS, right child first, closest-hit shadow rays). It is the
+//       literal restatement of gpu_shader.comp and, with STATS, counts the work
+//       that shader performs (node loads, primitive tests, material fetches).
+//   k_packet        : the production kernel. A wave64 renders an 8x8 pixel tile
+//       as one packet: the tree walk order of gpu_shader.comp:384-426 does not
+//       depend on the ray, so the wave walks it once with a 64-bit active mask
+//       per stack entry (the stack lives in the wave's VGPR lanes: entry j in
+//       lane j, readlane/writelane), node and shape records are wave-uniform
+//       scalar loads, and each lane keeps exactly the state, order and
+//       tie-breaking of its own reference walk. Shadow rays stop per lane at the
+//       first occluder closer than the light (equivalent to the reference's
+//       closest-hit test).
+//
+// Launch geometry: 256-thread blocks = 4 waves side by side = 32 x 8 pixels;
+// grid = ceil(W/32) x ceil(rows/8). Every kernel is compiled with
+// -ffp-contract=off (Makefile) so its float sequence is the oracle's.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "rt_device.h"
+
+using namespace rtd;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kTileW = 32;  // pixels per block row (4 waves x 8)
+constexpr int kTileH = 8;
+constexpr int kMaxStack = 64;  // gpu_shader.comp:384
+constexpr int kRing = 1024;    // dispatch timings kept between rt_kernel_times calls
+
+// Stats slots, in rt_stats field order.
+enum {
+    ST_PIXELS = 0, ST_CLOSEST, ST_SHADOW, ST_NODES,
+    ST_BVH0, ST_BVH1, ST_BVH2, ST_BVH3,
+    ST_BR0, ST_BR1, ST_BR2, ST_BR3,
+    ST_UPD, ST_HITS, ST_COUNT
+};
+
+// ---------------------------------------------------------------------------
+// Pack kernels
+
+__global__ void k_pack_shapes(const FlatShape* __restrict__ src, int S, const int* __restrict__ idx, int I,
+                              float4* __restrict__ geo_lin, float4* __restrict__ geo_leaf,
+                              float4* __restrict__ mat) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    int total = S + I;
+    if (j >= total) return;
+    const bool leaf_slot = j >= S;
+    const int si = leaf_slot ? idx[j - S] : j;
+    const FlatShape& s = src[si];
+    GeoRec g;
+    for (int k = 0; k < 18; ++k) g.f[k] = 0.f;
+    g.type = s.type;
+    g.idx = si;
+    if (s.type == RT_SPHERE) {
+        g.f[0] = s.sphereCenter.x; g.f[1] = s.sphereCenter.y; g.f[2] = s.sphereCenter.z;
+        g.f[3] = s.sphereRadius;
+    } else {
+        V n = mk(s.planeNormal.x, s.planeNormal.y, s.planeNormal.z);
+        g.f[0] = n.x; g.f[1] = n.y; g.f[2] = n.z; g.f[3] = s.planeD;
+        if (s.type == RT_WALL) {
+            g.f[4] = s.wallStart.x; g.f[5] = s.wallStart.y; g.f[6] = s.wallStart.z;
+            g.f[7] = s.wallWidth; g.f[8] = s.wallHeight;
+            // gpu_shader.comp:305-307, a function of the normal only.
+            V u = normalize(cross(n, mk(0.f, 1.f, 0.f)));
+            if (len(u) < 1e-5f) u = normalize(cross(n, mk(1.f, 0.f, 0.f)));
+            V v = normalize(cross(n, u));
+            g.f[9] = u.x; g.f[10] = u.y; g.f[11] = u.z;
+            g.f[12] = v.x; g.f[13] = v.y; g.f[14] = v.z;
+        } else if (s.type == RT_TRIANGLE) {
+            V p1 = mk(s.triP1.x, s.triP1.y, s.triP1.z);
+            V e1 = mk(s.triP2.x, s.triP2.y, s.triP2.z) - p1;
+            V e2 = mk(s.triP3.x, s.triP3.y, s.triP3.z) - p1;
+            // gpu_shader.comp:218-229, ray-independent part.
+            float d00 = dot(e1, e1), d01 = dot(e1, e2), d11 = dot(e2, e2);
+            g.f[4] = p1.x; g.f[5] = p1.y; g.f[6] = p1.z;
+            g.f[7] = e1.x; g.f[8] = e1.y; g.f[9] = e1.z;
+            g.f[10] = e2.x; g.f[11] = e2.y; g.f[12] = e2.z;
+            g.f[13] = d00; g.f[14] = d01; g.f[15] = d11;
+            g.f[16] = d00 * d11 - d01 * d01;
+        }
+    }
+    float4* out = leaf_slot ? geo_leaf + 5 * static_cast<size_t>(j - S) : geo_lin + 5 * static_cast<size_t>(j);
+    const float4* in = reinterpret_cast<const float4*>(&g);
+    for (int k = 0; k < 5; ++k) out[k] = in[k];
+    if (!leaf_slot) {
+        const FlatMaterial& m = s.material;
+        mat[2 * j] = make_float4(m.color.x, m.color.y, m.color.z, m.fresnelStrength);
+        mat[2 * j + 1] = make_float4(m.ambientStrength, m.diffuseStrength, m.specularStrength,
+                                     static_cast<float>(m.shininess));
+    }
+}
+
+__global__ void k_pack_nodes(const FlatNode* __restrict__ src, int N, float4* __restrict__ nodes) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    const FlatNode& n = src[k];
+    int a, b;
+    if (n.leftChild == -1) {
+        a = -(n.startShapeIdx + 1);
+        b = n.numShapes;
+    } else {
+        a = n.leftChild;
+        b = n.rightChild;
+    }
+    nodes[2 * k] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, __int_as_float(a));
+    nodes[2 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, __int_as_float(b));
+}
+
+// ---------------------------------------------------------------------------
+// Shared per-pixel plumbing
+
+struct PixelCoord {
+    int x, r, y;
+    bool active;
+};
+
+__device__ __forceinline__ PixelCoord pixel_of(const KParams& kp) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    PixelCoord pc;
+    pc.x = blockIdx.x * kTileW + wave * 8 + (lane & 7);
+    pc.r = blockIdx.y * kTileH + (lane >> 3);
+    pc.active = pc.x < kp.width && pc.r < kp.out_rows;
+    pc.y = pc.active ? image_row(kp, pc.r) : 0;
+    pc.active = pc.active && pc.y < kp.height;
+    return pc;
+}
+
+// Background gradient (gpu_shader.comp:436).
+__device__ __forceinline__ V background(const KParams& kp, int y) {
+    return mix(mk(0.05f, 0.07f, 0.1f), mk(0.5f, 0.7f, 1.0f), static_cast<float>(y) / kp.resY);
+}
+
+__device__ __forceinline__ Ray primary_ray(const KParams& kp, int x, int y) {
+    return get_ray(kp, 2.0f * static_cast<float>(x) / kp.resX - 1.0f, 1.0f - 2.0f * static_cast<float>(y) / kp.resY);
+}
+
+struct Counters {
+    unsigned c[ST_COUNT];
+};
+
+// Lighting of one bounce (gpu_shader.comp:482-516): adds to acc/att and
+// updates the ray; returns true if the path continues.
+__device__ __forceinline__ bool shade_bounce(const KParams& kp, Ray& ray, V hp, V hn, const Mat& m, bool shadow,
+                                             V& acc, V& att, float offset_reflect) {
+    V pc = phong(hp, hn, ray.d, kp.light_pos, kp.light_color, m);
+    if (shadow) pc = pc * 0.3f;
+    acc = acc + mulv(att, pc);
+    if (m.specular > 0.0f) {
+        V rd = reflect(ray.d, hn);
+        ray.o = hp + hn * offset_reflect;
+        ray.d = rd;
+        if (kp.useFresnel) {
+            float fr = powf(1.0f - gmax(dot(-ray.d, hn), 0.0f), 5.0f);
+            fr = gmin(gmax(fr, 0.0f), 0.8f);
+            float rw = m.fresnel * fr;
+            float mw = 1.0f - rw;
+            att = mulv(att, mix(m.color, mk(1.f, 1.f, 1.f), rw));
+            acc = acc + mulv(mw * m.color, pc);
+        } else {
+            att = att * m.specular;
+        }
+        return true;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// k_lane: the reference walk, one ray per lane.
+
+struct LaneHit {
+    bool found;
+    float d;
+    V p;
+    int slot;
+};
+
+template <bool STATS>
+__device__ LaneHit lane_closest_bvh(const KParams& kp, const float4* __restrict__ nodes,
+                                    const float4* __restrict__ geo, Ray r, int* stk, Counters& c) {
+    LaneHit res{false, 1e20f, mk(0.f, 0.f, 0.f), -1};
+    if (kp.N <= 0) return res;
+    const V inv = inv_dir(r.d);
+    int sp = 0;
+    stk[0] = kp.N - 1;
+    sp = 1;
+    while (sp > 0) {
+        --sp;
+        const int k = stk[sp * kBlock];
+        const float4 a = nodes[2 * k], b = nodes[2 * k + 1];
+        if (STATS) c.c[ST_NODES]++;
+        if (!ray_aabb(r.o, inv, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z))) continue;
+        const int ia = __float_as_int(a.w), ib = __float_as_int(b.w);
+        if (ia < 0) {
+            const int start = -ia - 1;
+            for (int i = 0; i < ib; ++i) {
+                const GeoRec g = load_rec(geo, start + i);
+                if (STATS && g.type >= 0 && g.type < 4) c.c[ST_BVH0 + g.type]++;
+                const Hit h = intersect(g, r, kp.useMT);
+                if (h.type == INNER) {
+                    const float d = dist(r.o, h.p);
+                    if (d < res.d) {
+                        res = LaneHit{true, d, h.p, start + i};
+                        if (STATS) c.c[ST_UPD]++;
+                    }
+                }
+            }
+        } else {
+            if (sp + 2 > kp.max_stack) return LaneHit{false, 1e20f, mk(0.f, 0.f, 0.f), -1};
+            stk[sp * kBlock] = ia;
+            stk[(sp + 1) * kBlock] = ib;
+            sp += 2;
+        }
+    }
+    return res;
+}
+
+template <bool STATS>
+__device__ LaneHit lane_closest_brute(const KParams& kp, const float4* __restrict__ geo, Ray r, Counters& c) {
+    LaneHit res{false, 1e20f, mk(0.f, 0.f, 0.f), -1};
+    for (int i = 0; i < kp.S; ++i) {
+        const GeoRec g = load_rec(geo, i);
+        if (STATS && g.type >= 0 && g.type < 4) c.c[ST_BR0 + g.type]++;
+        const Hit h = intersect(g, r, kp.useMT);
+        if (h.type == INNER) {
+            const float d = dist(r.o, h.p);
+            if (d < res.d) {
+                res = LaneHit{true, d, h.p, i};
+                if (STATS) c.c[ST_UPD]++;
+            }
+        }
+    }
+    return res;
+}
+
+// Brute-force shadow loop (gpu_shader.comp:569-580): stops at the first
+// INNER hit nearer than the light.
+template <bool STATS>
+__device__ bool lane_shadow_brute(const KParams& kp, const float4* __restrict__ geo, Ray sr, float ld, Counters& c) {
+    for (int i = 0; i < kp.S; ++i) {
+        const GeoRec g = load_rec(geo, i);
+        if (STATS && g.type >= 0 && g.type < 4) c.c[ST_BR0 + g.type]++;
+        const Hit h = intersect(g, sr, kp.useMT);
+        if (h.type == INNER && dist(sr.o, h.p) < ld) return true;
+    }
+    return false;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(kBlock) void k_lane(const float4* __restrict__ geo_leaf,
+                                                 const float4* __restrict__ geo_lin,
+                                                 const float4* __restrict__ mat,
+                                                 const float4* __restrict__ nodes, KParams kp) {
+    extern __shared__ int lds_stack[];
+    int* stk = lds_stack + threadIdx.x;  // entry s of this lane at stk[s * kBlock]
+    const PixelCoord pc = pixel_of(kp);
+    Counters c;
+    if (STATS)
+        for (int i = 0; i < ST_COUNT; ++i) c.c[i] = 0;
+    if (pc.active) {
+        const V bg = background(kp, pc.y);
+        Ray ray = primary_ray(kp, pc.x, pc.y);
+        V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
+        if (STATS) c.c[ST_PIXELS]++;
+        const float shadow_off = kp.useBVH ? 1e-3f : 1e-5f;  // :469 vs :565
+        for (int depth = 0; depth < kp.maxBounces; ++depth) {
+            if (STATS) c.c[ST_CLOSEST]++;
+            LaneHit hit = kp.useBVH ? lane_closest_bvh<STATS>(kp, nodes, geo_leaf, ray, stk, c)
+                                    : lane_closest_brute<STATS>(kp, geo_lin, ray, c);
+            if (!hit.found) {
+                acc = acc + mulv(att, bg);
+                break;
+            }
+            if (STATS) c.c[ST_HITS]++;
+            const GeoRec g = load_rec(kp.useBVH ? geo_leaf : geo_lin, hit.slot);
+            const V hn = shape_normal(g, hit.p);
+            const Mat m = load_mat(mat, g.idx);
+            Ray sr{hit.p + hn * shadow_off, normalize(kp.light_pos - hit.p)};
+            const float ld = dist(kp.light_pos, hit.p);
+            bool shadow;
+            if (STATS) c.c[ST_SHADOW]++;
+            if (kp.useBVH) {
+                // Full closest-hit walk, as gpu_shader.comp:473-480.
+                LaneHit sh = lane_closest_bvh<STATS>(kp, nodes, geo_leaf, sr, stk, c);
+                shadow = sh.found && sh.d < ld;
+            } else {
+                shadow = lane_shadow_brute<STATS>(kp, geo_lin, sr, ld, c);
+            }
+            if (!shade_bounce(kp, ray, hit.p, hn, m, shadow, acc, att, 1e-3f)) break;
+        }
+        store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+    }
+    if (STATS) {
+        for (int i = 0; i < ST_COUNT; ++i) {
+            unsigned long long v = c.c[i];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if ((threadIdx.x & 63) == 0 && v) atomicAdd(kp.stats + i, v);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_packet: the wave64 packet walk.
+
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// Wave-uniform stack of (node, 64-bit mask) held in three VGPRs: entry j in lane j.
+struct WaveStack {
+    int node, lo, hi;
+    int sp;  // uniform
+    __device__ __forceinline__ void push(int k, unsigned long long m) {
+        const bool mine = lane_id() == sp;  // v_writelane equivalent
+        node = mine ? k : node;
+        lo = mine ? static_cast<int>(m & 0xffffffffu) : lo;
+        hi = mine ? static_cast<int>(m >> 32) : hi;
+        ++sp;
+    }
+    __device__ __forceinline__ void pop(int& k, unsigned long long& m) {
+        --sp;
+        k = __builtin_amdgcn_readlane(node, sp);
+        const unsigned l = static_cast<unsigned>(__builtin_amdgcn_readlane(lo, sp));
+        const unsigned h = static_cast<unsigned>(__builtin_amdgcn_readlane(hi, sp));
+        m = (static_cast<unsigned long long>(h) << 32) | l;
+    }
+};
+
+__device__ __forceinline__ bool lane_in(unsigned long long m) { return (m >> lane_id()) & 1ull; }
+
+// Closest hit for every lane in `active` (reference walk order per lane).
+__device__ LaneHit packet_closest_bvh(const KParams& kp, const float4* __restrict__ nodes,
+                                      const float4* __restrict__ geo, const Ray& r, bool active) {
+    LaneHit res{false, 1e20f, mk(0.f, 0.f, 0.f), -1};
+    const unsigned long long m0 = __ballot(active);
+    if (kp.N <= 0 || m0 == 0) return res;
+    const V inv = inv_dir(r.d);
+    WaveStack st{0, 0, 0, 0};
+    st.push(kp.N - 1, m0);
+    while (st.sp > 0) {
+        int k;
+        unsigned long long m;
+        st.pop(k, m);
+        k = uni(k);
+        const float4 a = nodes[2 * k], b = nodes[2 * k + 1];
+        const bool hb = lane_in(m) && ray_aabb(r.o, inv, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
+        const unsigned long long mh = __ballot(hb);
+        if (mh == 0) continue;
+        const int ia = uni(__float_as_int(a.w)), ib = uni(__float_as_int(b.w));
+        if (ia < 0) {
+            const int start = -ia - 1;
+            for (int i = 0; i < ib; ++i) {
+                const GeoRec g = load_rec(geo, start + i);
+                if (hb) {
+                    const Hit h = intersect(g, r, kp.useMT);
+                    if (h.type == INNER) {
+                        const float d = dist(r.o, h.p);
+                        if (d < res.d) res = LaneHit{true, d, h.p, start + i};
+                    }
+                }
+            }
+        } else {
+            if (st.sp + 2 > kMaxStack) {
+                // Unreachable: the host rejects trees deeper than the stack.
+                return LaneHit{false, 1e20f, mk(0.f, 0.f, 0.f), -1};
+            }
+            st.push(ia, mh);
+            st.push(ib, mh);
+        }
+    }
+    return res;
+}
+
+// Shadow query: true iff the lane's reference closest-hit shadow walk would
+// find a hit nearer than `ld` (and than the 1e20 start value). Lanes retire at
+// their first such hit.
+__device__ bool packet_shadow_bvh(const KParams& kp, const float4* __restrict__ nodes,
+                                  const float4* __restrict__ geo, const Ray& r, float ld, bool active) {
+    bool shadow = false;
+    const unsigned long long m0 = __ballot(active);
+    if (kp.N <= 0 || m0 == 0) return false;
+    const float lim = gmin(ld, 1e20f);
+    const V inv = inv_dir(r.d);
+    WaveStack st{0, 0, 0, 0};
+    st.push(kp.N - 1, m0);
+    unsigned long long done = 0;
+    while (st.sp > 0) {
+        int k;
+        unsigned long long m;
+        st.pop(k, m);
+        m &= ~done;
+        if (m == 0) continue;
+        k = uni(k);
+        const float4 a = nodes[2 * k], b = nodes[2 * k + 1];
+        const bool hb = lane_in(m) && ray_aabb(r.o, inv, mk(a.x, a.y, a.z), mk(b.x, b.y, b.z));
+        const unsigned long long mh = __ballot(hb);
+        if (mh == 0) continue;
+        const int ia = uni(__float_as_int(a.w)), ib = uni(__float_as_int(b.w));
+        if (ia < 0) {
+            const int start = -ia - 1;
+            bool live = hb;
+            for (int i = 0; i < ib; ++i) {
+                const GeoRec g = load_rec(geo, start + i);
+                if (live) {
+                    const Hit h = intersect(g, r, kp.useMT);
+                    if (h.type == INNER && dist(r.o, h.p) < lim) {
+                        shadow = true;
+                        live = false;
+                    }
+                }
+                if (__ballot(live) == 0) break;
+            }
+            done = __ballot(shadow);
+            if ((m0 & ~done) == 0) break;
+        } else {
+            if (st.sp + 2 > kMaxStack) return shadow;
+            st.push(ia, mh);
+            st.push(ib, mh);
+        }
+    }
+    return shadow;
+}
+
+__device__ LaneHit packet_closest_brute(const KParams& kp, const float4* __restrict__ geo, const Ray& r,
+                                        bool active) {
+    LaneHit res{false, 1e20f, mk(0.f, 0.f, 0.f), -1};
+    if (__ballot(active) == 0) return res;
+    for (int i = 0; i < kp.S; ++i) {
+        const GeoRec g = load_rec(geo, i);
+        if (active) {
+            const Hit h = intersect(g, r, kp.useMT);
+            if (h.type == INNER) {
+                const float d = dist(r.o, h.p);
+                if (d < res.d) res = LaneHit{true, d, h.p, i};
+            }
+        }
+    }
+    return res;
+}
+
+__device__ bool packet_shadow_brute(const KParams& kp, const float4* __restrict__ geo, const Ray& r, float ld,
+                                    bool active) {
+    bool live = active, shadow = false;
+    if (__ballot(live) == 0) return false;
+    for (int i = 0; i < kp.S; ++i) {
+        const GeoRec g = load_rec(geo, i);
+        if (live) {
+            const Hit h = intersect(g, r, kp.useMT);
+            if (h.type == INNER && dist(r.o, h.p) < ld) {
+                shadow = true;
+                live = false;
+            }
+        }
+        if (__ballot(live) == 0) break;
+    }
+    return shadow;
+}
+
+__global__ __launch_bounds__(kBlock) void k_packet(const float4* __restrict__ geo_leaf,
+                                                   const float4* __restrict__ geo_lin,
+                                                   const float4* __restrict__ mat,
+                                                   const float4* __restrict__ nodes, KParams kp) {
+    const PixelCoord pc = pixel_of(kp);
+    const V bg = background(kp, pc.y);
+    Ray ray = primary_ray(kp, pc.x, pc.y);
+    V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
+    bool alive = pc.active;
+    const float shadow_off = kp.useBVH ? 1e-3f : 1e-5f;
+    for (int depth = 0; depth < kp.maxBounces; ++depth) {
+        if (__ballot(alive) == 0) break;
+        LaneHit hit = kp.useBVH ? packet_closest_bvh(kp, nodes, geo_leaf, ray, alive)
+                                : packet_closest_brute(kp, geo_lin, ray, alive);
+        if (alive && !hit.found) {
+            acc = acc + mulv(att, bg);
+            alive = false;
+        }
+        V hn = mk(0.f, 0.f, 0.f);
+        Mat m{};
+        Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
+        float ld = 0.f;
+        if (alive) {
+            const GeoRec g = load_rec(kp.useBVH ? geo_leaf : geo_lin, hit.slot);
+            hn = shape_normal(g, hit.p);
+            m = load_mat(mat, g.idx);
+            sr = Ray{hit.p + hn * shadow_off, normalize(kp.light_pos - hit.p)};
+            ld = dist(kp.light_pos, hit.p);
+        }
+        const bool shadow = kp.useBVH ? packet_shadow_bvh(kp, nodes, geo_leaf, sr, ld, alive)
+                                      : packet_shadow_brute(kp, geo_lin, sr, ld, alive);
+        if (alive) alive = shade_bounce(kp, ray, hit.p, hn, m, shadow, acc, att, 1e-3f);
+    }
+    if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;      // used once the ring is full
+    hipEvent_t last0 = nullptr, last1 = nullptr;  // events of the latest dispatch
+    bool timed = false;
+    // per-dispatch event pairs since the last rt_kernel_times call
+    std::vector<hipEvent_t> ring0, ring1;
+    int ring_used = 0;
+    // scene
+    float4 *geo_lin = nullptr, *geo_leaf = nullptr, *mat = nullptr, *nodes = nullptr;
+    int S = 0, N = 0, I = 0, max_stack = 1;
+    bool have_scene = false, have_cam = false, have_light = false;
+    std::vector<FlatNode> host_nodes;  // topology check for rt_update_nodes
+    FlatShape* staging_shapes = nullptr;
+    size_t staging_shapes_cap = 0;
+    FlatNode* staging_nodes = nullptr;
+    size_t staging_nodes_cap = 0;
+    int* staging_idx = nullptr;
+    size_t staging_idx_cap = 0;
+    std::vector<int> host_idx;
+    // frame constants
+    FlatCamera cam{};
+    FlatLight light{};
+    rt_params params{0.f, 0.f, 0, 0, 0, 0};  // the reference's first frame sees zeros
+    int kernel = RT_KERNEL_AUTO;
+    // own surface
+    float* img = nullptr;
+    size_t img_pitch = 0;
+    int img_w = 0, img_h = 0;
+    unsigned long long* stats_dev = nullptr;
+};
+
+namespace {
+
+#pragma clang diagnostic ignored "-Wunused-result"
+#define HIP_TRY(x)                                  \
+    do {                                            \
+        hipError_t e__ = (x);                       \
+        if (e__ != hipSuccess) return RT_ERR_DEVICE; \
+    } while (0)
+
+int set_dev(rt_ctx* c) {
+    HIP_TRY(hipSetDevice(c->device));
+    return RT_OK;
+}
+
+template <class T>
+int ensure_staging(T*& p, size_t& cap, size_t n) {
+    if (n <= cap && p) return RT_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, n * sizeof(T) > 0 ? n * sizeof(T) : sizeof(T)) != hipSuccess) return RT_ERR_NO_MEMORY;
+    cap = n;
+    return RT_OK;
+}
+
+void free_scene(rt_ctx* c) {
+    hipFree(c->geo_lin);
+    hipFree(c->geo_leaf);
+    hipFree(c->mat);
+    hipFree(c->nodes);
+    c->geo_lin = c->geo_leaf = c->mat = c->nodes = nullptr;
+    c->have_scene = false;
+}
+
+// Checks the arrays the way the reference shader would dereference them and
+// measures the reference walk's worst-case stack need (every box hit).
+int check_tree(const FlatNode* nodes, int N, const int* idx, int I, int S, int* max_stack) {
+    for (int i = 0; i < I; ++i)
+        if (idx[i] < 0 || idx[i] >= S) return RT_ERR_BVH;
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& n = nodes[k];
+        if (n.leftChild == -1) {
+            if (n.numShapes > 0 && (n.startShapeIdx < 0 || n.startShapeIdx > I - n.numShapes)) return RT_ERR_BVH;
+        } else if (n.leftChild < 0 || n.leftChild >= N || n.rightChild < 0 || n.rightChild >= N) {
+            return RT_ERR_BVH;
+        }
+    }
+    int ms = N > 0 ? 1 : 0;
+    if (N > 0) {
+        std::vector<int> st;
+        st.push_back(N - 1);
+        long long visits = 0;
+        while (!st.empty()) {
+            int k = st.back();
+            st.pop_back();
+            if (++visits > 4ll * N + 8) return RT_ERR_BVH;  // cycle or exploding DAG
+            if (nodes[k].leftChild != -1) {
+                st.push_back(nodes[k].leftChild);
+                st.push_back(nodes[k].rightChild);
+                ms = static_cast<int>(st.size()) > ms ? static_cast<int>(st.size()) : ms;
+            }
+        }
+    }
+    if (ms > kMaxStack) return RT_ERR_BVH;
+    *max_stack = ms;
+    return RT_OK;
+}
+
+int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
+                 size_t pitch, KParams& kp) {
+    if (!c->have_scene || !c->have_cam || !c->have_light) return RT_ERR_NO_SCENE;
+    if (width <= 0 || height <= 0 || stripe <= 0 || step <= 0 || out_rows < 0 || y0 < 0 || !dst ||
+        pitch < static_cast<size_t>(width) * 16 || (pitch % 16) != 0)
+        return RT_ERR_INVALID;
+    std::memset(&kp, 0, sizeof kp);
+    kp.geo_leaf = c->geo_leaf;
+    kp.geo_lin = c->geo_lin;
+    kp.mat = c->mat;
+    kp.nodes = c->nodes;
+    kp.S = c->S;
+    kp.N = c->N;
+    kp.I = c->I;
+    kp.max_stack = c->max_stack < 1 ? 1 : c->max_stack;
+    const FlatCamera& cam = c->cam;
+    kp.cam_pos = V{cam.Position.x, cam.Position.y, cam.Position.z};
+    kp.cam_front = V{cam.Front.x, cam.Front.y, cam.Front.z};
+    kp.cam_right = V{cam.Right.x, cam.Right.y, cam.Right.z};
+    kp.cam_up = V{cam.Up.x, cam.Up.y, cam.Up.z};
+    // gpu_shader.comp:156-157 (radians = deg * 0.0174532925..., glm/GLSL).
+    const float h = 2.0f * std::tan((cam.fov / 2.0f) * 0.01745329251994329576923690768489f);
+    kp.plane_h = h;
+    kp.plane_w = h * cam.aspectRatio;
+    kp.light_pos = V{c->light.position.x, c->light.position.y, c->light.position.z};
+    kp.light_color = V{c->light.color.x, c->light.color.y, c->light.color.z};
+    kp.resX = c->params.resX;
+    kp.resY = c->params.resY;
+    kp.maxBounces = c->params.maxBounces;
+    kp.useBVH = c->params.useBVH;
+    kp.useFresnel = c->params.useFresnel;
+    kp.useMT = c->params.useMollerTrumbore;
+    kp.width = width;
+    kp.height = height;
+    kp.y0 = y0;
+    kp.stripe = stripe;
+    kp.step = step;
+    kp.out_rows = out_rows;
+    kp.dst = reinterpret_cast<char*>(dst);
+    kp.pitch = pitch;
+    return RT_OK;
+}
+
+int launch(rt_ctx* c, const KParams& kp, bool stats) {
+    if (kp.out_rows == 0) return RT_OK;
+    dim3 grid((kp.width + kTileW - 1) / kTileW, (kp.out_rows + kTileH - 1) / kTileH);
+    if (grid.y > 65535u) return RT_ERR_INVALID;
+    int kind = c->kernel == RT_KERNEL_AUTO ? RT_KERNEL_PACKET : c->kernel;
+    const size_t lds = static_cast<size_t>(kp.max_stack) * kBlock * sizeof(int);
+    hipEvent_t e0 = c->ev0, e1 = c->ev1;
+    if (!stats && c->ring_used < static_cast<int>(c->ring0.size())) {
+        e0 = c->ring0[c->ring_used];
+        e1 = c->ring1[c->ring_used];
+    }
+    if (!stats) HIP_TRY(hipEventRecord(e0, c->stream));
+    if (stats) {
+        hipLaunchKernelGGL(k_lane<true>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
+                           c->nodes, kp);
+    } else if (kind == RT_KERNEL_LANE) {
+        hipLaunchKernelGGL(k_lane<false>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
+                           c->nodes, kp);
+    } else {
+        hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
+                           kp);
+    }
+    HIP_TRY(hipGetLastError());
+    if (!stats) {
+        HIP_TRY(hipEventRecord(e1, c->stream));
+        c->last0 = e0;
+        c->last1 = e1;
+        if (c->ring_used < static_cast<int>(c->ring0.size())) ++c->ring_used;
+        c->timed = true;
+    }
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rt_status_string(int s) {
+    switch (s) {
+        case RT_OK: return "ok";
+        case RT_ERR_INVALID: return "invalid argument";
+        case RT_ERR_DEVICE: return "HIP runtime error";
+        case RT_ERR_NO_MEMORY: return "device allocation failed";
+        case RT_ERR_NO_SCENE: return "scene, camera or light not uploaded";
+        case RT_ERR_BVH: return "node/index arrays out of range or deeper than the 64-entry stack";
+        case RT_ERR_NO_DEVICE: return "no such HIP device";
+        default: return "unknown status";
+    }
+}
+
+int rt_create(rt_ctx** out, int device) {
+    if (!out) return RT_ERR_INVALID;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return RT_ERR_NO_DEVICE;
+    rt_ctx* c = new (std::nothrow) rt_ctx();
+    if (!c) return RT_ERR_NO_MEMORY;
+    c->device = device;
+    if (set_dev(c) != RT_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipMalloc(&c->stats_dev, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
+        rt_destroy(c);
+        return RT_ERR_DEVICE;
+    }
+    c->own_stream = true;
+    c->ring0.resize(kRing, nullptr);
+    c->ring1.resize(kRing, nullptr);
+    for (int i = 0; i < kRing; ++i)
+        if (hipEventCreate(&c->ring0[i]) != hipSuccess || hipEventCreate(&c->ring1[i]) != hipSuccess) {
+            rt_destroy(c);
+            return RT_ERR_DEVICE;
+        }
+    *out = c;
+    return RT_OK;
+}
+
+int rt_destroy(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    free_scene(c);
+    hipFree(c->staging_shapes);
+    hipFree(c->staging_nodes);
+    hipFree(c->staging_idx);
+    hipFree(c->img);
+    hipFree(c->stats_dev);
+    for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
+    for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
+    if (c->ev0) hipEventDestroy(c->ev0);
+    if (c->ev1) hipEventDestroy(c->ev1);
+    if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return RT_OK;
+}
+
+int rt_set_stream(rt_ctx* c, void* s) {
+    if (!c) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->own_stream) hipStreamDestroy(c->stream);
+    if (s) {
+        c->stream = static_cast<hipStream_t>(s);
+        c->own_stream = false;
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        c->own_stream = true;
+    }
+    return RT_OK;
+}
+
+int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx,
+                    int I) {
+    if (!c || S < 0 || N < 0 || I < 0 || (S > 0 && !shapes) || (N > 0 && !nodes) || (I > 0 && !idx))
+        return RT_ERR_INVALID;
+    int ms = 0;
+    int rc = check_tree(nodes, N, idx, I, S, &ms);
+    if (rc != RT_OK) return rc;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    free_scene(c);
+    const size_t sS = S > 0 ? S : 1, sI = I > 0 ? I : 1, sN = N > 0 ? N : 1;
+    if (hipMalloc(&c->geo_lin, sS * 5 * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->geo_leaf, sI * 5 * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->mat, sS * 2 * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->nodes, sN * 2 * sizeof(float4)) != hipSuccess) {
+        free_scene(c);
+        return RT_ERR_NO_MEMORY;
+    }
+    if ((rc = ensure_staging(c->staging_shapes, c->staging_shapes_cap, sS)) != RT_OK) return rc;
+    if ((rc = ensure_staging(c->staging_nodes, c->staging_nodes_cap, sN)) != RT_OK) return rc;
+    if ((rc = ensure_staging(c->staging_idx, c->staging_idx_cap, sI)) != RT_OK) return rc;
+    if (S > 0) HIP_TRY(hipMemcpyAsync(c->staging_shapes, shapes, S * sizeof(FlatShape), hipMemcpyHostToDevice, c->stream));
+    if (N > 0) HIP_TRY(hipMemcpyAsync(c->staging_nodes, nodes, N * sizeof(FlatNode), hipMemcpyHostToDevice, c->stream));
+    if (I > 0) HIP_TRY(hipMemcpyAsync(c->staging_idx, idx, I * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (S + I > 0)
+        hipLaunchKernelGGL(k_pack_shapes, dim3((S + I + 255) / 256), dim3(256), 0, c->stream, c->staging_shapes, S,
+                           c->staging_idx, I, c->geo_lin, c->geo_leaf, c->mat);
+    if (N > 0)
+        hipLaunchKernelGGL(k_pack_nodes, dim3((N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, N,
+                           c->nodes);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->S = S;
+    c->N = N;
+    c->I = I;
+    c->max_stack = ms;
+    c->host_nodes.assign(nodes, nodes + N);
+    c->host_idx.assign(idx, idx + I);
+    c->have_scene = true;
+    return RT_OK;
+}
+
+int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
+    if (!c || !c->have_scene || first < 0 || count < 0 || first > c->S - count || (count > 0 && !shapes))
+        return RT_ERR_INVALID;
+    if (count == 0) return RT_OK;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    // Rewrite the shape-order records of [first, first+count), then every
+    // leaf slot; the leaf copy is re-packed from the full staging array.
+    HIP_TRY(hipMemcpyAsync(c->staging_shapes + first, shapes, count * sizeof(FlatShape), hipMemcpyHostToDevice,
+                           c->stream));
+    hipLaunchKernelGGL(k_pack_shapes, dim3((c->S + c->I + 255) / 256), dim3(256), 0, c->stream, c->staging_shapes,
+                       c->S, c->staging_idx, c->I, c->geo_lin, c->geo_leaf, c->mat);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));  // glBufferSubData semantics: the host array may be reused
+    return RT_OK;
+}
+
+int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
+    if (!c || !c->have_scene || N != c->N || (N > 0 && !nodes)) return RT_ERR_INVALID;
+    for (int k = 0; k < N; ++k) {
+        const FlatNode &a = nodes[k], &b = c->host_nodes[k];
+        if (a.leftChild != b.leftChild || a.rightChild != b.rightChild ||
+            (a.leftChild == -1 && (a.startShapeIdx != b.startShapeIdx || a.numShapes != b.numShapes)))
+            return RT_ERR_BVH;  // topology must not change: use rt_upload_scene
+    }
+    if (N == 0) return RT_OK;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipMemcpyAsync(c->staging_nodes, nodes, N * sizeof(FlatNode), hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_pack_nodes, dim3((N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, N, c->nodes);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));  // the host array may be reused after return
+    return RT_OK;
+}
+
+int rt_set_camera(rt_ctx* c, const FlatCamera* cam) {
+    if (!c || !cam) return RT_ERR_INVALID;
+    c->cam = *cam;
+    c->have_cam = true;
+    return RT_OK;
+}
+
+int rt_set_light(rt_ctx* c, const FlatLight* l) {
+    if (!c || !l) return RT_ERR_INVALID;
+    c->light = *l;
+    c->have_light = true;
+    return RT_OK;
+}
+
+int rt_set_params(rt_ctx* c, const rt_params* p) {
+    if (!c || !p || p->maxBounces < 0) return RT_ERR_INVALID;
+    c->params = *p;
+    return RT_OK;
+}
+
+int rt_set_kernel(rt_ctx* c, int kernel) {
+    if (!c || kernel < RT_KERNEL_AUTO || kernel > RT_KERNEL_PACKET) return RT_ERR_INVALID;
+    c->kernel = kernel;
+    return RT_OK;
+}
+
+int rt_dispatch_rows(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
+                     size_t pitch) {
+    if (!c) return RT_ERR_INVALID;
+    KParams kp;
+    int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, dst, pitch, kp);
+    if (rc != RT_OK) return rc;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    return launch(c, kp, false);
+}
+
+int rt_dispatch(rt_ctx* c, int width, int height, int y0, int y1) {
+    if (!c || width <= 0 || height <= 0 || y0 < 0 || y1 > height || y0 > y1) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    if (width != c->img_w || height != c->img_h || !c->img) {
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        hipFree(c->img);
+        c->img = nullptr;
+        c->img_w = c->img_h = 0;
+        size_t pitch = 0;
+        if (hipMallocPitch(reinterpret_cast<void**>(&c->img), &pitch, static_cast<size_t>(width) * 16, height) !=
+            hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        HIP_TRY(hipMemset2DAsync(c->img, pitch, 0, static_cast<size_t>(width) * 16, height, c->stream));
+        c->img_pitch = pitch;
+        c->img_w = width;
+        c->img_h = height;
+    }
+    return rt_dispatch_rows(c, width, height, y0, 1, 1, y1 - y0,
+                            reinterpret_cast<float*>(reinterpret_cast<char*>(c->img) + y0 * c->img_pitch),
+                            c->img_pitch);
+}
+
+int rt_sync(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_read_image(rt_ctx* c, float* dst, size_t pitch) {
+    if (!c || !dst || !c->img || pitch < static_cast<size_t>(c->img_w) * 16) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipMemcpy2DAsync(dst, pitch, c->img, c->img_pitch, static_cast<size_t>(c->img_w) * 16, c->img_h,
+                             hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_device_image(rt_ctx* c, void** p, size_t* pitch) {
+    if (!c || !p || !pitch || !c->img) return RT_ERR_INVALID;
+    *p = c->img;
+    *pitch = c->img_pitch;
+    return RT_OK;
+}
+
+int rt_collect_stats(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, rt_stats* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    // The counting kernel needs a destination; use a scratch surface.
+    float* scratch = nullptr;
+    const size_t pitch = static_cast<size_t>(width > 0 ? width : 1) * 16;
+    if (hipMalloc(&scratch, pitch * static_cast<size_t>(out_rows > 0 ? out_rows : 1)) != hipSuccess)
+        return RT_ERR_NO_MEMORY;
+    KParams kp;
+    int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, scratch, pitch, kp);
+    if (rc == RT_OK) {
+        kp.stats = c->stats_dev;
+        if (hipMemsetAsync(c->stats_dev, 0, ST_COUNT * sizeof(unsigned long long), c->stream) != hipSuccess)
+            rc = RT_ERR_DEVICE;
+        if (rc == RT_OK) rc = launch(c, kp, true);
+        unsigned long long h[ST_COUNT];
+        if (rc == RT_OK && (hipMemcpyAsync(h, c->stats_dev, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+                            hipStreamSynchronize(c->stream) != hipSuccess))
+            rc = RT_ERR_DEVICE;
+        if (rc == RT_OK) {
+            out->pixels = h[ST_PIXELS];
+            out->closest_rays = h[ST_CLOSEST];
+            out->shadow_rays = h[ST_SHADOW];
+            out->node_visits = h[ST_NODES];
+            for (int i = 0; i < 4; ++i) {
+                out->bvh_tests[i] = h[ST_BVH0 + i];
+                out->brute_tests[i] = h[ST_BR0 + i];
+            }
+            out->closest_updates = h[ST_UPD];
+            out->hits = h[ST_HITS];
+        }
+    }
+    hipStreamSynchronize(c->stream);
+    hipFree(scratch);
+    return rc;
+}
+
+int rt_kernel_times(rt_ctx* c, float* ms, int cap) {
+    if (!c || (cap > 0 && !ms) || cap < 0) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    const int n = c->ring_used;
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(hipEventSynchronize(c->ring1[i]));
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, c->ring0[i], c->ring1[i]));
+        if (i < cap) ms[i] = t;
+    }
+    c->ring_used = 0;
+    return n;
+}
+
+int rt_last_kernel_ms(rt_ctx* c, float* ms) {
+    if (!c || !ms || !c->timed) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipEventSynchronize(c->last1));
+    HIP_TRY(hipEventElapsedTime(ms, c->last0, c->last1));
+    return RT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,410 @@
+"""rtamd — Python host binding of the MI355X ray tracer.
+
+Thin ctypes layer over the two product libraries built in-tree by
+``opengl-ray-tracer_amd/Makefile``:
+
+* ``lib/librtamd.so``  — the HIP renderer, C ABI ``include/rt_api.h``: the drop-in
+  for the reference's compute-shader dispatch (``src/computeShader.hpp``,
+  ``src/main.cpp:238-370``).
+* ``lib/librtscene.so`` — the host scene library, C ABI ``include/rt_scene.h``:
+  shapes, ``buildBVH``/``split``, ``serializeScene`` (``src/main.cpp:806-1193``).
+
+Class and method names mirror the reference (``Scene.buildBVH``,
+``Scene.serializeScene``, ``ComputeShader.dispatch`` ...). Loading fails loudly:
+there is no CPU fallback anywhere in this module.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIBDIR = os.path.join(HERE, "lib")
+
+# ---------------------------------------------------------------------------
+# Record layouts (include/rt_flat.h; sizes pinned by static asserts there).
+
+def _vec(off):
+    return [("x", off), ("y", off + 4), ("z", off + 8)]
+
+
+MATERIAL_DTYPE = np.dtype({
+    "names": ["color", "fresnelStrength", "ambientStrength", "diffuseStrength", "specularStrength", "shininess"],
+    "formats": [("<f4", 3), "<f4", "<f4", "<f4", "<f4", "<i4"],
+    "offsets": [0, 12, 16, 20, 24, 28],
+    "itemsize": 32,
+})
+
+SHAPE_DTYPE = np.dtype({
+    "names": ["type", "material", "sphereCenter", "sphereRadius", "planeNormal", "planeD",
+              "wallStart", "wallWidth", "wallHeight", "triP1", "triP2", "triP3"],
+    "formats": ["<i4", MATERIAL_DTYPE, ("<f4", 3), "<f4", ("<f4", 3), "<f4",
+                ("<f4", 3), "<f4", "<f4", ("<f4", 3), ("<f4", 3), ("<f4", 3)],
+    "offsets": [0, 32, 64, 76, 80, 92, 96, 108, 112, 144, 160, 176],
+    "itemsize": 192,
+})
+
+NODE_DTYPE = np.dtype({
+    "names": ["boundsMin", "boundsMax", "leftChild", "rightChild", "startShapeIdx", "numShapes"],
+    "formats": [("<f4", 3), ("<f4", 3), "<i4", "<i4", "<i4", "<i4"],
+    "offsets": [0, 16, 32, 36, 40, 44],
+    "itemsize": 48,
+})
+
+CAMERA_DTYPE = np.dtype({
+    "names": ["Position", "aspectRatio", "Front", "Up", "Right", "fov"],
+    "formats": [("<f4", 3), "<f4", ("<f4", 3), ("<f4", 3), ("<f4", 3), "<f4"],
+    "offsets": [0, 12, 16, 32, 48, 64],
+    "itemsize": 80,
+})
+
+LIGHT_DTYPE = np.dtype({
+    "names": ["position", "color"],
+    "formats": [("<f4", 3), ("<f4", 3)],
+    "offsets": [0, 16],
+    "itemsize": 32,
+})
+
+SPHERE, PLANE, WALL, TRIANGLE = 0, 1, 2, 3
+KERNEL_AUTO, KERNEL_LANE, KERNEL_PACKET = 0, 1, 2
+
+
+class rt_params(C.Structure):
+    """Uniforms of gpu_shader.comp:126-130."""
+    _fields_ = [("resX", C.c_float), ("resY", C.c_float), ("maxBounces", C.c_int), ("useBVH", C.c_int),
+                ("useFresnel", C.c_int), ("useMollerTrumbore", C.c_int)]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [("pixels", C.c_uint64), ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+                ("node_visits", C.c_uint64), ("bvh_tests", C.c_uint64 * 4), ("brute_tests", C.c_uint64 * 4),
+                ("closest_updates", C.c_uint64), ("hits", C.c_uint64)]
+
+    def as_dict(self):
+        return {"pixels": self.pixels, "closest_rays": self.closest_rays, "shadow_rays": self.shadow_rays,
+                "node_visits": self.node_visits, "bvh_tests": list(self.bvh_tests),
+                "brute_tests": list(self.brute_tests), "closest_updates": self.closest_updates, "hits": self.hits}
+
+
+# Bytes of the reference's records that a test of each shape type reads
+# (SURVEY §8(d)): 4 B type tag + sphere 16 | plane 16 | wall 36 | triangle 52 (36 for MT).
+P_TYPE = {0: 4 + 16, 1: 4 + 16, 2: 4 + 36, 3: 4 + 52}
+P_TYPE_MT = {0: 4 + 16, 1: 4 + 16, 2: 4 + 36, 3: 4 + 36}
+
+
+def algorithmic_bytes(st: dict, pixels_written: int, use_mt: bool = False) -> int:
+    """B_alg of SURVEY §8(d): 40 B per node visit, (4 B index + record bytes) per
+    BVH leaf test, record bytes per brute-force test, 32 B material per closest
+    update, 16 B per RGBA32F pixel store."""
+    p = P_TYPE_MT if use_mt else P_TYPE
+    b = 40 * st["node_visits"] + 32 * st["closest_updates"] + 16 * pixels_written
+    b += sum((4 + p[t]) * n for t, n in enumerate(st["bvh_tests"]))
+    b += sum(p[t] * n for t, n in enumerate(st["brute_tests"]))
+    return int(b)
+
+
+STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
+          -4: "scene, camera or light not uploaded", -5: "node/index arrays out of range or deeper than the 64-entry stack",
+          -6: "no such HIP device"}
+
+
+class RTError(RuntimeError):
+    def __init__(self, what, code):
+        super().__init__(f"{what} failed: {STATUS.get(code, code)} ({code})")
+        self.code = code
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+_P = C.c_void_p
+_I = C.c_int
+
+
+def _load(name):
+    path = os.path.join(LIBDIR, name)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `make -C opengl-ray-tracer_amd` "
+                           f"(or __graft_entry__.build()); there is no fallback path")
+    return C.CDLL(path)
+
+
+_scene_lib = None
+_rt_lib = None
+
+SCENE_SYMBOLS = {
+    "rts_new": (_P, []), "rts_free": (None, [_P]), "rts_clear": (_I, [_P]),
+    "rts_add_sphere": (_I, [_P, _P, C.c_float, _P]),
+    "rts_add_plane": (_I, [_P, _P, _P, _P]),
+    "rts_add_wall": (_I, [_P, _P, C.c_float, C.c_float, _P, _P]),
+    "rts_add_triangle": (_I, [_P, _P, _P, _P, _I, _P]),
+    "rts_add_mesh": (_I, [_P, _P, _I, _P, _I, _P, _P]),
+    "rts_add_mesh_oriented": (_I, [_P, _P, _I, _P, _I, _P, _P]),
+    "rts_set_camera": (_I, [_P, _P, C.c_float, C.c_float]),
+    "rts_camera_look_at": (_I, [_P, _P]),
+    "rts_set_light": (_I, [_P, _P, _P, C.c_float]),
+    "rts_build_bvh": (_I, [_P, _I]),
+    "rts_counts": (_I, [_P, _P, _P, _P]),
+    "rts_serialize": (_I, [_P, _P, _P, _P, _P, _P]),
+    "rts_bvh_stats": (_I, [_P, _P, _P, _P, _P]),
+    "rts_generate": (_I, [_P, _I, _I, C.c_float]),
+}
+
+RT_SYMBOLS = {
+    "rt_create": (_I, [_P, _I]), "rt_destroy": (_I, [_P]), "rt_set_stream": (_I, [_P, _P]),
+    "rt_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
+    "rt_update_shapes": (_I, [_P, _I, _I, _P]),
+    "rt_update_nodes": (_I, [_P, _P, _I]),
+    "rt_set_camera": (_I, [_P, _P]), "rt_set_light": (_I, [_P, _P]),
+    "rt_set_params": (_I, [_P, _P]), "rt_set_kernel": (_I, [_P, _I]),
+    "rt_dispatch": (_I, [_P, _I, _I, _I, _I]),
+    "rt_dispatch_rows": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t]),
+    "rt_sync": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t]),
+    "rt_device_image": (_I, [_P, _P, _P]),
+    "rt_collect_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
+    "rt_last_kernel_ms": (_I, [_P, _P]),
+    "rt_kernel_times": (_I, [_P, _P, _I]),
+    "rt_status_string": (C.c_char_p, [_I]),
+}
+
+
+def _bind(lib, table):
+    for name, (res, args) in table.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def scene_lib():
+    global _scene_lib
+    if _scene_lib is None:
+        _scene_lib = _bind(_load("librtscene.so"), SCENE_SYMBOLS)
+    return _scene_lib
+
+
+def rt_lib():
+    global _rt_lib
+    if _rt_lib is None:
+        _rt_lib = _bind(_load("librtamd.so"), RT_SYMBOLS)
+    return _rt_lib
+
+
+def _f3(v):
+    return (C.c_float * 3)(*[float(x) for x in v])
+
+
+def material(color=(1, 1, 1), fresnel=1.0, ambient=0.4, diffuse=1.0, specular=0.5, shininess=32):
+    """Material(c, fresnel, ambient, diffuse, specular, shine) (src/material.hpp:23)."""
+    m = np.zeros(1, MATERIAL_DTYPE)
+    m["color"] = color
+    m["fresnelStrength"] = fresnel
+    m["ambientStrength"] = ambient
+    m["diffuseStrength"] = diffuse
+    m["specularStrength"] = specular
+    m["shininess"] = shininess
+    return m
+
+
+# ---------------------------------------------------------------------------
+@dataclass
+class FlatScene:
+    """serializeScene output: the five SSBO images (src/flatStructures.hpp:80-108)."""
+    shapes: np.ndarray
+    nodes: np.ndarray
+    indices: np.ndarray
+    camera: np.ndarray
+    light: np.ndarray
+
+
+class Scene:
+    """The reference's `Scene` (src/main.cpp:92-100) on the host scene library."""
+
+    def __init__(self):
+        self._lib = scene_lib()
+        self._h = self._lib.rts_new()
+        if not self._h:
+            raise MemoryError("rts_new")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._lib.rts_free(self._h)
+            self._h = None
+
+    def _chk(self, rc, what):
+        if rc < 0:
+            raise RTError(what, rc)
+        return rc
+
+    @staticmethod
+    def _mat(m):
+        return _ptr(m) if m is not None else None
+
+    def add_sphere(self, center, radius, mat=None):
+        return self._chk(self._lib.rts_add_sphere(self._h, _f3(center), radius, self._mat(mat)), "add_sphere")
+
+    def add_plane(self, normal, point, mat=None):
+        return self._chk(self._lib.rts_add_plane(self._h, _f3(normal), _f3(point), self._mat(mat)), "add_plane")
+
+    def add_wall(self, start, width, height, normal, mat=None):
+        return self._chk(self._lib.rts_add_wall(self._h, _f3(start), width, height, _f3(normal), self._mat(mat)),
+                         "add_wall")
+
+    def add_triangle(self, a, b, c, invert=False, mat=None):
+        return self._chk(self._lib.rts_add_triangle(self._h, _f3(a), _f3(b), _f3(c), int(invert), self._mat(mat)),
+                         "add_triangle")
+
+    def add_mesh(self, vertices, indices, origin=(0, 0, 0), mat=None, oriented=False):
+        v = np.ascontiguousarray(vertices, np.float32).reshape(-1, 3)
+        i = np.ascontiguousarray(indices, np.uint32).reshape(-1)
+        fn = self._lib.rts_add_mesh_oriented if oriented else self._lib.rts_add_mesh
+        return self._chk(fn(self._h, _ptr(v), len(v), _ptr(i), len(i), _f3(origin), self._mat(mat)), "add_mesh")
+
+    def set_camera(self, position, fov=60.0, aspect=1.0):
+        self._chk(self._lib.rts_set_camera(self._h, _f3(position), fov, aspect), "set_camera")
+
+    def LookAt(self, target):
+        self._chk(self._lib.rts_camera_look_at(self._h, _f3(target)), "LookAt")
+
+    def set_light(self, position, color=(1, 1, 1), intensity=1.0):
+        self._chk(self._lib.rts_set_light(self._h, _f3(position), _f3(color), intensity), "set_light")
+
+    def buildBVH(self, maxDepth=15):
+        self._chk(self._lib.rts_build_bvh(self._h, maxDepth), "buildBVH")
+
+    def generate(self, config, variant=0, aspect=16 / 9):
+        self._chk(self._lib.rts_generate(self._h, config, variant, aspect), "generate")
+        return self
+
+    def counts(self):
+        s, n, i = C.c_int(), C.c_int(), C.c_int()
+        self._chk(self._lib.rts_counts(self._h, C.byref(s), C.byref(n), C.byref(i)), "counts")
+        return s.value, n.value, i.value
+
+    def bvh_stats(self):
+        v = [C.c_int() for _ in range(4)]
+        self._chk(self._lib.rts_bvh_stats(self._h, *[C.byref(x) for x in v]), "bvh_stats")
+        return dict(zip(["leaves", "max_leaf", "depth", "max_stack"], [x.value for x in v]))
+
+    def serializeScene(self) -> FlatScene:
+        s, n, i = self.counts()
+        shapes = np.zeros(s, SHAPE_DTYPE)
+        nodes = np.zeros(n, NODE_DTYPE)
+        idx = np.zeros(i, np.int32)
+        cam = np.zeros(1, CAMERA_DTYPE)
+        light = np.zeros(1, LIGHT_DTYPE)
+        self._chk(self._lib.rts_serialize(self._h, _ptr(shapes), _ptr(nodes), _ptr(idx), _ptr(cam), _ptr(light)),
+                  "serializeScene")
+        return FlatScene(shapes, nodes, idx, cam, light)
+
+
+def generate(config, variant=0, width=1920, height=1080) -> FlatScene:
+    """One of the BASELINE configurations as serialised arrays."""
+    sc = Scene().generate(config, variant, float(width) / float(height))
+    return sc.serializeScene()
+
+
+# ---------------------------------------------------------------------------
+class ComputeShader:
+    """The GPU operator: ComputeShader("gpu_shader.comp") + its SSBOs + uniforms
+    (src/computeShader.hpp, src/main.cpp:238-370) on one HIP device."""
+
+    def __init__(self, device=0):
+        self._lib = rt_lib()
+        h = C.c_void_p()
+        self._chk(self._lib.rt_create(C.byref(h), device), "rt_create")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.rt_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def _chk(rc, what):
+        if rc != 0:
+            raise RTError(what, rc)
+
+    def set_stream(self, stream_handle):
+        self._chk(self._lib.rt_set_stream(self._h, C.c_void_p(stream_handle) if stream_handle else None),
+                  "rt_set_stream")
+
+    def upload(self, fs: FlatScene):
+        self._keep = fs
+        self._chk(self._lib.rt_upload_scene(self._h, _ptr(fs.shapes), len(fs.shapes), _ptr(fs.nodes), len(fs.nodes),
+                                            _ptr(fs.indices), len(fs.indices)), "rt_upload_scene")
+        self.set_camera(fs.camera)
+        self.set_light(fs.light)
+
+    def update_shapes(self, first, shapes):
+        shapes = np.ascontiguousarray(shapes, SHAPE_DTYPE)
+        self._chk(self._lib.rt_update_shapes(self._h, first, len(shapes), _ptr(shapes)), "rt_update_shapes")
+
+    def update_nodes(self, nodes):
+        nodes = np.ascontiguousarray(nodes, NODE_DTYPE)
+        self._chk(self._lib.rt_update_nodes(self._h, _ptr(nodes), len(nodes)), "rt_update_nodes")
+
+    def set_camera(self, cam):
+        cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+        self._chk(self._lib.rt_set_camera(self._h, _ptr(cam)), "rt_set_camera")
+
+    def set_light(self, light):
+        light = np.ascontiguousarray(light, LIGHT_DTYPE)
+        self._chk(self._lib.rt_set_light(self._h, _ptr(light)), "rt_set_light")
+
+    def set_params(self, resX, resY, maxBounces=3, useBVH=True, useFresnel=False, useMollerTrumbore=False):
+        p = rt_params(float(resX), float(resY), int(maxBounces), int(bool(useBVH)), int(bool(useFresnel)),
+                      int(bool(useMollerTrumbore)))
+        self._chk(self._lib.rt_set_params(self._h, C.byref(p)), "rt_set_params")
+
+    def set_kernel(self, kernel):
+        self._chk(self._lib.rt_set_kernel(self._h, int(kernel)), "rt_set_kernel")
+
+    def dispatch(self, width, height, y0=0, y1=None):
+        self._chk(self._lib.rt_dispatch(self._h, width, height, y0, height if y1 is None else y1), "rt_dispatch")
+
+    def dispatch_rows(self, width, height, y0, stripe, step, out_rows, dst_ptr, pitch):
+        self._chk(self._lib.rt_dispatch_rows(self._h, width, height, y0, stripe, step, out_rows,
+                                             C.c_void_p(dst_ptr), pitch), "rt_dispatch_rows")
+
+    def sync(self):
+        self._chk(self._lib.rt_sync(self._h), "rt_sync")
+
+    def read_image(self, width, height):
+        out = np.empty((height, width, 4), np.float32)
+        self._chk(self._lib.rt_read_image(self._h, _ptr(out), width * 16), "rt_read_image")
+        return out
+
+    def render(self, width, height, y0=0, y1=None):
+        """dispatch + barrier + readback of the full surface."""
+        self.dispatch(width, height, y0, y1)
+        self.sync()
+        return self.read_image(width, height)
+
+    def collect_stats(self, width, height, y0=0, stripe=1, step=1, out_rows=None):
+        st = rt_stats()
+        rows = height - y0 if out_rows is None else out_rows
+        self._chk(self._lib.rt_collect_stats(self._h, width, height, y0, stripe, step, rows, C.byref(st)),
+                  "rt_collect_stats")
+        return st.as_dict()
+
+    def kernel_times(self, cap=1024):
+        """Device ms of each render dispatch since the last call (HIP events on the ctx stream)."""
+        buf = np.zeros(cap, np.float32)
+        n = self._lib.rt_kernel_times(self._h, _ptr(buf), cap)
+        if n < 0:
+            raise RTError("rt_kernel_times", n)
+        return buf[:min(n, cap)].copy()
+
+    def last_kernel_ms(self):
+        ms = C.c_float()
+        self._chk(self._lib.rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
+        return ms.value

@@ -1,0 +1,52 @@
+"""The C-ABI libraries load and export every entry point include/*.h declares
+(no compute calls: this runs without a GPU)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+import rtamd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DECL = re.compile(r"^\s*(?:const\s+)?(?:int|void|char|struct\s+\w+)\s*\*?\s*(r[a-z]*_\w+)\s*\(", re.M)
+
+
+def declared(header):
+    with open(os.path.join(ROOT, "include", header)) as f:
+        text = re.sub(r"/\*.*?\*/", "", f.read(), flags=re.S)
+    return sorted(set(DECL.findall(text)))
+
+
+@pytest.mark.parametrize("header,lib", [("rt_api.h", "librtamd.so"), ("rt_scene.h", "librtscene.so")])
+def test_exports(header, lib):
+    names = declared(header)
+    assert len(names) >= 12, names
+    so = C.CDLL(os.path.join(rtamd.LIBDIR, lib))
+    missing = [n for n in names if not hasattr(so, n)]
+    assert not missing, missing
+    table = rtamd.RT_SYMBOLS if lib == "librtamd.so" else rtamd.SCENE_SYMBOLS
+    assert sorted(table) == names, "binding table out of sync with the header"
+
+
+def test_status_strings():
+    lib = rtamd.rt_lib()
+    for code in range(0, -7, -1):
+        assert lib.rt_status_string(code).decode() == rtamd.STATUS[code]
+
+
+def test_no_device_fails_loudly():
+    """Without a HIP device rt_create must fail with a status, never crash."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(rtamd.RTError) as e:
+        rtamd.ComputeShader(0)
+    assert e.value.code in (-6, -2)
+
+
+def test_kernel_is_gfx950():
+    """The HIP code object inside librtamd.so targets gfx950."""
+    with open(os.path.join(rtamd.LIBDIR, "librtamd.so"), "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob

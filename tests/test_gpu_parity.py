@@ -1,0 +1,259 @@
+"""HIP renderer parity against the CPU oracle (-m gpu; needs an MI355X).
+
+Every comparison goes through the C ABI (librtamd.so). Tolerance: 1e-4 per
+channel (BASELINE.json north_star); the kernels are built to reproduce the
+oracle's IEEE sequence, so the expected difference is 0 except for powf
+(device ocml vs glibc), which only moves the specular term by ulps.
+Oracle sizes are kept to a few seconds of CPU; full-size frames are checked
+through size-independent properties (packet == lane, stripe-split invariance,
+determinism, band == crop).
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import rtamd
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+CFG_BOUNCES = {1: 3, 2: 1, 3: 3, 5: 3}
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = rtamd.ComputeShader(0)
+    yield c
+    c.close()
+
+
+def gpu_rows(ctx, fs, W, H, p, y0=0, rows=None, kernel=rtamd.KERNEL_PACKET):
+    rows = H - y0 if rows is None else rows
+    ctx.upload(fs)
+    ctx.set_params(p.resX, p.resY, p.maxBounces, p.useBVH, p.useFresnel, p.useMollerTrumbore)
+    ctx.set_kernel(kernel)
+    out = torch.full((rows, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
+    ctx.dispatch_rows(W, H, y0, 1, 1, rows, out.data_ptr(), W * 16)
+    ctx.sync()
+    return out.cpu().numpy()
+
+
+def check(img, ref, what):
+    diff = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    bad = int((diff > TOL).any(axis=-1).sum())
+    assert np.isfinite(img).all() == np.isfinite(ref).all(), what
+    assert bad == 0, f"{what}: {bad} pixels over {TOL}, max diff {np.nanmax(diff):.3g}"
+
+
+CASES = [
+    # cfg, W, H, y0, rows, maxBounces, bvh, fresnel, mt
+    (1, 160, 120, 0, None, 3, 1, 0, 0),
+    (1, 160, 120, 0, None, 3, 0, 0, 0),
+    (2, 200, 150, 0, None, 1, 1, 0, 0),
+    (2, 200, 150, 0, None, 4, 1, 1, 0),
+    (2, 120, 90, 0, None, 2, 0, 1, 1),
+    (2, 800, 600, 280, 24, 1, 1, 0, 0),
+    (3, 1920, 1080, 520, 24, 3, 1, 0, 0),
+    (3, 1920, 1080, 600, 16, 3, 1, 1, 1),
+    (3, 240, 135, 0, None, 3, 0, 0, 0),
+    (5, 1920, 1080, 500, 24, 3, 1, 0, 0),
+    (5, 480, 270, 0, None, 2, 1, 1, 1),
+]
+
+
+@pytest.mark.parametrize("kernel", [rtamd.KERNEL_PACKET, rtamd.KERNEL_LANE])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "c%d_%dx%d_y%d_b%d_bvh%d_f%d_mt%d" % (
+    c[0], c[1], c[2], c[3], c[5], c[6], c[7], c[8]))
+def test_parity_vs_oracle(ctx, case, kernel):
+    cfg, W, H, y0, rows, mb, bvh, fr, mt = case
+    fs = rtamd.generate(cfg, 0, W, H)
+    p = oracle.params(W, H, mb, bvh, fr, mt)
+    ref, _ = oracle.render(fs, W, H, p, y0=y0, out_rows=rows)
+    img = gpu_rows(ctx, fs, W, H, p, y0, rows, kernel)
+    check(img, ref, f"cfg{cfg} kernel{kernel}")
+
+
+@pytest.mark.parametrize("case", [(1, 160, 120, 0, 120, 3, 1), (1, 160, 120, 0, 120, 3, 0),
+                                  (2, 200, 150, 0, 150, 1, 1), (2, 100, 75, 0, 75, 3, 0),
+                                  (3, 1920, 1080, 520, 16, 3, 1), (5, 1920, 1080, 500, 16, 3, 1)])
+def test_stats_match_oracle_counts(ctx, case):
+    """The counting kernel's totals are the oracle's, exactly (they price B_alg)."""
+    cfg, W, H, y0, rows, mb, bvh = case
+    fs = rtamd.generate(cfg, 0, W, H)
+    p = oracle.params(W, H, mb, bvh)
+    _, st_ref = oracle.render(fs, W, H, p, y0=y0, out_rows=rows, stats=True)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, bvh)
+    st = ctx.collect_stats(W, H, y0, 1, 1, rows)
+    assert st == st_ref
+
+
+def test_golden_frames_on_gpu(golden_dir):
+    """The committed oracle frames, rendered by the HIP kernels."""
+    import os
+    from make_golden import FRAME_CASES
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    data = np.load(os.path.join(golden_dir, "frames.npz"))
+    c = rtamd.ComputeShader(0)
+    for (cfg, w, h, mb, bvh, fr, mt) in FRAME_CASES:
+        fs = rtamd.generate(cfg, 0, w, h)
+        key = f"c{cfg}_w{w}_h{h}_b{mb}_bvh{bvh}_f{fr}_mt{mt}"
+        for k in (rtamd.KERNEL_PACKET, rtamd.KERNEL_LANE):
+            img = gpu_rows(c, fs, w, h, oracle.params(w, h, mb, bvh, fr, mt), kernel=k)
+            check(img, data[key], key)
+    c.close()
+
+
+# --------------------------------------------------------------------------
+# Full-size properties (no oracle at 1920x1080)
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_full_frame_packet_equals_lane(ctx, cfg):
+    W, H = 1920, 1080
+    fs = rtamd.generate(cfg, 0, W, H)
+    p = oracle.params(W, H, CFG_BOUNCES[cfg])
+    a = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_PACKET)
+    b = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_LANE)
+    assert np.array_equal(a, b)
+    assert (a[..., 3] == 1).all()
+
+
+def test_full_frame_stripes_reassemble(ctx):
+    """Rendering the 4 interleaved stripe sets of a 4-GPU plan and scattering
+    them back gives the single-dispatch frame, bit for bit (the multi-GPU path
+    minus the RCCL gather)."""
+    import tiling
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    p = oracle.params(W, H, 3)
+    full = gpu_rows(ctx, fs, W, H, p)
+    plan = tiling.StripePlan(H, 4, 8)
+    bufs = torch.zeros((4, plan.rows_max, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    for r in range(4):
+        ctx.dispatch_rows(W, H, plan.y0(r), 8, 4, plan.rows(r), bufs[r].data_ptr(), W * 16)
+    ctx.sync()
+    img = tiling.unpermute(bufs, plan).cpu().numpy()
+    assert np.array_equal(img, full)
+
+
+def test_deterministic_and_band_equals_crop(ctx):
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    p = oracle.params(W, H, 3)
+    a = gpu_rows(ctx, fs, W, H, p)
+    b = gpu_rows(ctx, fs, W, H, p)
+    assert np.array_equal(a, b)
+    band = gpu_rows(ctx, fs, W, H, p, y0=333, rows=77)
+    assert np.array_equal(band, a[333:410])
+
+
+def test_own_surface_dispatch_and_readback(ctx):
+    W, H = 96, 64
+    fs = rtamd.generate(2, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 1, True)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    img = ctx.render(W, H)
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 1))
+    check(img, ref, "own surface")
+    ms = ctx.last_kernel_ms()
+    assert ms > 0
+    assert len(ctx.kernel_times()) >= 1
+
+
+# --------------------------------------------------------------------------
+# Edge cases the reference exercises implicitly
+
+def _empty_scene(W, H):
+    fs = rtamd.generate(1, 0, W, H)
+    return rtamd.FlatScene(fs.shapes[:0].copy(), fs.nodes[:0].copy(), fs.indices[:0].copy(), fs.camera, fs.light)
+
+
+@pytest.mark.parametrize("bvh", [1, 0])
+def test_empty_scene_is_background(ctx, bvh):
+    W, H = 37, 29  # not multiples of the 8x8 tile
+    fs = _empty_scene(W, H)
+    p = oracle.params(W, H, 3, bvh)
+    ref, _ = oracle.render(fs, W, H, p)
+    check(gpu_rows(ctx, fs, W, H, p), ref, "empty")
+
+
+def test_no_nodes_with_shapes(ctx):
+    """N = 0: the BVH branch sees nothing, the brute branch sees the shapes."""
+    W, H = 64, 48
+    fs = rtamd.generate(2, 0, W, H)
+    fs0 = rtamd.FlatScene(fs.shapes, fs.nodes[:0].copy(), fs.indices[:0].copy(), fs.camera, fs.light)
+    for bvh in (1, 0):
+        p = oracle.params(W, H, 2, bvh)
+        ref, _ = oracle.render(fs0, W, H, p)
+        check(gpu_rows(ctx, fs0, W, H, p), ref, f"N=0 bvh{bvh}")
+
+
+def test_zero_bounces_is_black(ctx):
+    W, H = 32, 16
+    fs = rtamd.generate(2, 0, W, H)
+    img = gpu_rows(ctx, fs, W, H, oracle.params(W, H, 0))
+    assert (img[..., :3] == 0).all() and (img[..., 3] == 1).all()
+
+
+def test_bad_tree_is_rejected(ctx):
+    fs = rtamd.generate(2, 0, 64, 48)
+    bad = fs.nodes.copy()
+    inner = np.where(bad["leftChild"] != -1)[0][0]
+    bad["rightChild"][inner] = len(bad) + 5
+    with pytest.raises(rtamd.RTError) as e:
+        ctx.upload(rtamd.FlatScene(fs.shapes, bad, fs.indices, fs.camera, fs.light))
+    assert e.value.code == -5
+    badidx = fs.indices.copy()
+    badidx[0] = len(fs.shapes)
+    with pytest.raises(rtamd.RTError):
+        ctx.upload(rtamd.FlatScene(fs.shapes, fs.nodes, badidx, fs.camera, fs.light))
+
+
+def test_update_shapes_and_nodes(ctx):
+    """Partial shape upload + node refit (the reference's animate path,
+    src/main.cpp:336-346) match a full re-upload of the same arrays."""
+    W, H = 160, 120
+    fs = rtamd.generate(2, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3, True)
+    moved = fs.shapes.copy()
+    moved["sphereCenter"][0] += np.float32([0, -2, 0])   # bounceSphere
+    nodes = fs.nodes.copy()
+    nodes["boundsMin"][-1] -= 3
+    nodes["boundsMax"][-1] += 3
+    ctx.update_shapes(0, moved[:1])
+    ctx.update_nodes(nodes)
+    out = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+    ctx.sync()
+    fs2 = rtamd.FlatScene(moved, nodes, fs.indices, fs.camera, fs.light)
+    ref, _ = oracle.render(fs2, W, H, oracle.params(W, H, 3))
+    check(out.cpu().numpy(), ref, "update")
+    changed = nodes.copy()
+    changed["leftChild"][-1], changed["rightChild"][-1] = changed["rightChild"][-1], changed["leftChild"][-1]
+    with pytest.raises(rtamd.RTError):
+        ctx.update_nodes(changed)
+
+
+def test_pitched_destination(ctx):
+    W, H = 72, 40
+    fs = rtamd.generate(2, 0, W, H)
+    p = oracle.params(W, H, 2)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 2, True)
+    pitch_px = W + 5
+    out = torch.full((H, pitch_px, 4), 9.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), pitch_px * 16)
+    ctx.sync()
+    o = out.cpu().numpy()
+    ref, _ = oracle.render(fs, W, H, p)
+    check(o[:, :W], ref, "pitched")
+    assert (o[:, W:] == 9.0).all()
