@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=3, choices=sorted(WORKLOADS))
     ap.add_argument("--variant", type=int, default=0, help="car road: 0 = 2-triangle quad, 1 = 222 strips")
-    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet", "accel"])
     ap.add_argument("--stripe", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
@@ -108,7 +108,7 @@ def main():
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
     ctx.upload(fs)
     ctx.set_params(W, H, mb, True, False, False)
-    ctx.set_kernel({"auto": 0, "lane": 1, "packet": 2}[a.kernel])
+    ctx.set_kernel({"auto": 0, "lane": 1, "packet": 2, "accel": 3}[a.kernel])
 
     plan = tiling.StripePlan(H, world, a.stripe)
     rows = plan.rows(rank)
@@ -153,6 +153,8 @@ def main():
     elapsed = float(el[0])
 
     kt = ctx.kernel_times()
+    info = ctx.accel_info()
+    kname = {1: "k_lane", 2: "k_packet", 3: "k_accel"}.get(info["last_kernel"], "?")
     k_ms = float(np.mean(kt)) if len(kt) else float("nan")
     k_med = float(np.median(kt)) if len(kt) else float("nan")
 
@@ -195,8 +197,9 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": b_alg_rank,
-                "kernel": "k_packet" if a.kernel in ("auto", "packet") else "k_lane",
+                "kernel": kname,
             },
+            "accel": info,
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu:

@@ -50,8 +50,21 @@ typedef struct rt_params {
 enum rt_kernel {
     RT_KERNEL_AUTO = 0,      /* pick the fastest for the uploaded scene               */
     RT_KERNEL_LANE = 1,      /* one ray per lane, per-lane LDS stack (reference walk) */
-    RT_KERNEL_PACKET = 2     /* wave64 packet walk, wave-uniform stack + active mask  */
+    RT_KERNEL_PACKET = 2,    /* wave64 packet walk, wave-uniform stack + active mask  */
+    RT_KERNEL_ACCEL = 3      /* packet walk + exact-result leaf accelerator (default  */
+                             /* for BVH + barycentric; falls back to PACKET otherwise)*/
 };
+
+/* Accelerator statistics of the uploaded scene (rt_accel_info). */
+typedef struct rt_accel_info {
+    int built;               /* 1 if the accelerator is in use for this scene         */
+    int local_nodes;         /* local BVH nodes inside large reference leaves         */
+    int local_leaves;
+    int bounded_prims;       /* shapes under a conservative box                       */
+    int always_prims;        /* shapes tested whenever their leaf is entered          */
+    int max_stack;           /* worst-case wave stack entries                          */
+    int last_kernel;         /* rt_kernel of the latest render dispatch               */
+} rt_accel_info;
 
 /* Work counted on the reference's own traversal (gpu_shader.comp:380-430 and
  * :523-580) — what the reference shader would load. Filled by
@@ -132,6 +145,9 @@ int rt_last_kernel_ms(struct rt_ctx* ctx, float* ms);
  * (up to 1024 are kept), written to ms[0..min(n,cap)). Returns n >= 0 and
  * restarts the record. Waits for those dispatches to finish. */
 int rt_kernel_times(struct rt_ctx* ctx, float* ms, int cap);
+
+/* Accelerator statistics for the uploaded scene. */
+int rt_accel_info_get(struct rt_ctx* ctx, rt_accel_info* out);
 
 /* Human-readable status string. */
 const char* rt_status_string(int status);

@@ -1,0 +1,392 @@
+// accel.cpp — host-side builder of the exact-result accelerator. See accel.h
+// for the contract; the bounds below are what makes skipping a shape safe.
+#include "accel.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <numeric>
+
+namespace rta {
+namespace {
+
+struct D3 {
+    double x, y, z;
+};
+inline D3 d3(rt_vec3 v) { return D3{v.x, v.y, v.z}; }
+inline D3 operator+(D3 a, D3 b) { return D3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline D3 operator-(D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline D3 operator*(D3 a, double s) { return D3{a.x * s, a.y * s, a.z * s}; }
+inline double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline D3 cross(D3 a, D3 b) { return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline bool finite3(D3 a) { return std::isfinite(a.x) && std::isfinite(a.y) && std::isfinite(a.z); }
+inline double maxabs(D3 a) { return std::max({std::fabs(a.x), std::fabs(a.y), std::fabs(a.z)}); }
+
+// float normalize exactly as the kernels do it (only used to rebuild the
+// wall basis; the box is then padded, so bit-exactness is not required).
+inline void fnormalize(float v[3]) {
+    float s = 1.0f / std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    v[0] *= s;
+    v[1] *= s;
+    v[2] *= s;
+}
+
+struct BoxAcc {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    void add(D3 p) {
+        const double v[3] = {p.x, p.y, p.z};
+        for (int i = 0; i < 3; ++i) {
+            lo[i] = std::min(lo[i], v[i]);
+            hi[i] = std::max(hi[i], v[i]);
+        }
+    }
+    Box3 padded(double pad) const {
+        Box3 b;
+        for (int i = 0; i < 3; ++i) {
+            // round outwards after padding
+            b.lo[i] = std::nextafter(static_cast<float>(lo[i] - pad), -INFINITY);
+            b.hi[i] = std::nextafter(static_cast<float>(hi[i] + pad), INFINITY);
+        }
+        return b;
+    }
+    double extent() const { return std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]}); }
+    double mag() const {
+        double m = 0;
+        for (int i = 0; i < 3; ++i) m = std::max({m, std::fabs(lo[i]), std::fabs(hi[i])});
+        return m;
+    }
+};
+
+// Relative padding: float error of every quantity the reference test computes
+// is ~1e-7 of the coordinates' magnitude (1e-3 of it for the barycentric
+// solve on the thinnest triangle admitted, 3e-4 for a grazing sphere root at
+// 1000 units); 1e-3 of (size + magnitude) covers all of them with room.
+constexpr double kPadRel = 1e-3;
+constexpr double kMinSin2 = 1e-3;  // thinnest triangle bounded (sin^2 of its corner angle)
+
+Box3 finish(const BoxAcc& acc) { return acc.padded(kPadRel * (acc.extent() + acc.mag() + 1.0) + 1e-6); }
+
+Box3 empty_box() {
+    Box3 b;
+    for (int i = 0; i < 3; ++i) {
+        b.lo[i] = INFINITY;
+        b.hi[i] = -INFINITY;
+    }
+    return b;
+}
+
+void grow(Box3& a, const Box3& b) {
+    for (int i = 0; i < 3; ++i) {
+        a.lo[i] = std::min(a.lo[i], b.lo[i]);
+        a.hi[i] = std::max(a.hi[i], b.hi[i]);
+    }
+}
+
+float area(const Box3& b) {
+    float e[3];
+    for (int i = 0; i < 3; ++i) e[i] = std::max(0.f, b.hi[i] - b.lo[i]);
+    return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
+}
+
+enum { UNBOUNDED = 0, BOUNDED = 1, NEVER = 2 };
+
+// 0: no finite bound; 1: bounded; 2: the reference test never returns INNER.
+int classify(const FlatShape& s, Box3& out) {
+    BoxAcc acc;
+    switch (s.type) {
+        case RT_SPHERE: {
+            D3 c = d3(s.sphereCenter);
+            double r = std::fabs(static_cast<double>(s.sphereRadius));
+            if (!finite3(c) || !std::isfinite(r)) return UNBOUNDED;
+            acc.add(c - D3{r, r, r});
+            acc.add(c + D3{r, r, r});
+            out = finish(acc);
+            return BOUNDED;
+        }
+        case RT_WALL: {
+            float n[3] = {s.planeNormal.x, s.planeNormal.y, s.planeNormal.z};
+            // the intersection basis of gpu_shader.comp:305-307
+            float u[3] = {n[1] * 0.f - 1.f * n[2], n[2] * 0.f - 0.f * n[0], n[0] * 1.f - 0.f * n[1]};
+            fnormalize(u);
+            if (std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]) < 1e-5f) {  // NaN stays NaN (:306)
+                float u2[3] = {n[1] * 0.f - 0.f * n[2], n[2] * 1.f - 0.f * n[0], n[0] * 0.f - 1.f * n[1]};
+                std::memcpy(u, u2, sizeof u);
+                fnormalize(u);
+            }
+            D3 N{n[0], n[1], n[2]}, U{u[0], u[1], u[2]};
+            D3 V = cross(N, U);
+            double vl = std::sqrt(dot(V, V));
+            if (!finite3(U) || !(vl > 0) || !std::isfinite(vl)) return UNBOUNDED;  // ±Y: NaN basis, never rejected
+            V = V * (1.0 / vl);
+            D3 st = d3(s.wallStart);
+            double nn = dot(N, N), W = s.wallWidth, H = s.wallHeight, D = s.planeD;
+            if (!finite3(st) || !(nn > 0) || !std::isfinite(W) || !std::isfinite(H) || !std::isfinite(D))
+                return UNBOUNDED;
+            D3 c0 = st - N * ((dot(N, st) + D) / nn);  // start projected on the stored plane
+            acc.add(c0);
+            acc.add(c0 + U * W);
+            acc.add(c0 + V * H);
+            acc.add(c0 + U * W + V * H);
+            out = finish(acc);
+            return BOUNDED;
+        }
+        case RT_TRIANGLE: {
+            D3 p1 = d3(s.triP1), p2 = d3(s.triP2), p3 = d3(s.triP3), N = d3(s.planeNormal);
+            double D = s.planeD;
+            if (!finite3(p1) || !finite3(p2) || !finite3(p3) || !finite3(N) || !std::isfinite(D)) return UNBOUNDED;
+            D3 e1 = p2 - p1, e2 = p3 - p1, cr = cross(e1, e2);
+            double d00 = dot(e1, e1), d11 = dot(e2, e2), c2 = dot(cr, cr);
+            if (!(d00 > 0) || !(d11 > 0) || !(c2 >= kMinSin2 * d00 * d11)) return UNBOUNDED;  // thin: error unbounded
+            D3 nt = cr * (1.0 / std::sqrt(c2));
+            double nl = std::sqrt(dot(N, N));
+            if (std::fabs(nl - 1.0) > 1e-3 || std::fabs(dot(N, nt)) < nl * (1.0 - 1e-4)) return UNBOUNDED;
+            double mag = std::max({maxabs(p1), maxabs(p2), maxabs(p3)}) + 1.0;
+            for (D3 p : {p1, p2, p3})
+                if (std::fabs(dot(N, p) + D) > 1e-4 * mag) return UNBOUNDED;  // stored plane off the vertices
+            acc.add(p1);
+            acc.add(p2);
+            acc.add(p3);
+            out = finish(acc);
+            return BOUNDED;
+        }
+        case RT_PLANE:
+            return UNBOUNDED;
+        default:
+            return NEVER;  // get_intersection has no branch for it (gpu_shader.comp:246-325)
+    }
+}
+
+struct Item {
+    int shape, seq;
+    Box3 box;
+    float c[3];
+};
+
+struct LocalBuilder {
+    AccelHost& out;
+    std::vector<Item> items;
+    int max_depth_seen = 0;
+
+    int leaf(int b, int e) {
+        int k = static_cast<int>(out.lbox.size());
+        Box3 box = empty_box();
+        for (int i = b; i < e; ++i) grow(box, items[i].box);
+        out.lbox.push_back(box);
+        out.la.push_back(-(static_cast<int>(out.prim_shape.size()) + 1));
+        out.lb.push_back(e - b);
+        // keep the reference order inside a leaf (cheaper ties, same result)
+        std::sort(items.begin() + b, items.begin() + e, [](const Item& x, const Item& y) { return x.seq < y.seq; });
+        for (int i = b; i < e; ++i) {
+            out.prim_shape.push_back(items[i].shape);
+            out.prim_seq.push_back(items[i].seq);
+        }
+        ++out.local_leaves;
+        return k;
+    }
+
+    // Binned SAH over centroids; `budget` = levels still allowed.
+    int build(int b, int e, int depth, int budget) {
+        max_depth_seen = std::max(max_depth_seen, depth);
+        const int n = e - b;
+        if (n <= 4 || budget <= 0) return leaf(b, e);
+        Box3 box = empty_box();
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < e; ++i) {
+            grow(box, items[i].box);
+            for (int a = 0; a < 3; ++a) {
+                clo[a] = std::min(clo[a], items[i].c[a]);
+                chi[a] = std::max(chi[a], items[i].c[a]);
+            }
+        }
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+        int mid = b;
+        const float ext = chi[axis] - clo[axis];
+        if (ext > 0) {
+            constexpr int kBins = 16;
+            int cnt[kBins] = {0};
+            Box3 bb[kBins];
+            for (auto& x : bb) x = empty_box();
+            auto bin_of = [&](const Item& it) {
+                int k = static_cast<int>((it.c[axis] - clo[axis]) / ext * kBins);
+                return std::min(kBins - 1, std::max(0, k));
+            };
+            for (int i = b; i < e; ++i) {
+                int k = bin_of(items[i]);
+                ++cnt[k];
+                grow(bb[k], items[i].box);
+            }
+            float best = INFINITY;
+            int best_k = -1;
+            Box3 lacc = empty_box();
+            int lcnt = 0;
+            float lcost[kBins];
+            for (int k = 0; k < kBins - 1; ++k) {
+                grow(lacc, bb[k]);
+                lcnt += cnt[k];
+                lcost[k] = lcnt ? area(lacc) * lcnt : 0.f;
+            }
+            Box3 racc = empty_box();
+            int rcnt = 0;
+            for (int k = kBins - 1; k >= 1; --k) {
+                grow(racc, bb[k]);
+                rcnt += cnt[k];
+                float c = lcost[k - 1] + (rcnt ? area(racc) * rcnt : 0.f);
+                if (rcnt && rcnt < n && c < best) {
+                    best = c;
+                    best_k = k;
+                }
+            }
+            if (best_k > 0) {
+                auto it = std::partition(items.begin() + b, items.begin() + e,
+                                         [&](const Item& x) { return bin_of(x) < best_k; });
+                mid = static_cast<int>(it - items.begin());
+            }
+        }
+        if (mid <= b || mid >= e) {  // all centroids equal or no useful split: halve by count
+            mid = b + n / 2;
+            std::nth_element(items.begin() + b, items.begin() + mid, items.begin() + e,
+                             [&](const Item& x, const Item& y) { return x.c[axis] < y.c[axis]; });
+        }
+        const int k = static_cast<int>(out.lbox.size());
+        out.lbox.push_back(box);
+        out.la.push_back(0);
+        out.lb.push_back(0);
+        const int l = build(b, mid, depth + 1, budget - 1);
+        const int r = build(mid, e, depth + 1, budget - 1);
+        out.la[k] = l;
+        out.lb[k] = r | (axis << 30);
+        return k;
+    }
+};
+
+}  // namespace
+
+bool shape_bound(const FlatShape& s, Box3& b) { return classify(s, b) == BOUNDED; }
+
+bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                 int leaf_threshold, int stack_cap, AccelHost& out) {
+    (void)I;
+    out = AccelHost();
+    out.content.assign(N, empty_box());
+    out.flags.assign(N, 0);
+    out.plain_start.assign(N, 0);
+    out.plain_count.assign(N, 0);
+    out.local_root.assign(N, -1);
+    if (N == 0) return true;
+
+    std::vector<Box3> sbox(S);
+    std::vector<int> scls(S);
+    for (int i = 0; i < S; ++i) scls[i] = classify(shapes[i], sbox[i]);
+
+    // Reference walk order (gpu_shader.comp:384-426: pop right first): the
+    // rank of each leaf's shapes, and each node's depth (pending stack bound).
+    std::vector<int> seq_base(N, -1), depth(N, 0);
+    std::vector<char> reach(N, 0);
+    {
+        std::vector<std::pair<int, int>> st{{N - 1, 1}};
+        int running = 0;
+        while (!st.empty()) {
+            auto [k, d] = st.back();
+            st.pop_back();
+            reach[k] = 1;
+            depth[k] = std::max(depth[k], d);
+            const FlatNode& nd = nodes[k];
+            if (nd.leftChild == -1) {
+                if (seq_base[k] < 0) {
+                    seq_base[k] = running;
+                    running += std::max(0, nd.numShapes);
+                }
+            } else {
+                st.push_back({nd.leftChild, d + 1});
+                st.push_back({nd.rightChild, d + 1});
+            }
+        }
+    }
+
+    // Leaves: always-tested prims and local BVHs.
+    int max_stack = 1;
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = nodes[k];
+        if (!reach[k] || nd.leftChild != -1) continue;
+        std::vector<Item> bounded;
+        std::vector<std::pair<int, int>> plain;  // (shape, seq)
+        Box3 content = empty_box();
+        bool unb = false;
+        for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
+            const int si = idx[nd.startShapeIdx + i];
+            const int seq = seq_base[k] + i;
+            if (scls[si] == NEVER) continue;
+            if (scls[si] == UNBOUNDED) {
+                plain.push_back({si, seq});
+                unb = true;
+                continue;
+            }
+            grow(content, sbox[si]);
+            Item it{si, seq, sbox[si], {}};
+            for (int a = 0; a < 3; ++a) it.c[a] = 0.5f * (sbox[si].lo[a] + sbox[si].hi[a]);
+            bounded.push_back(it);
+        }
+        out.content[k] = content;
+        out.flags[k] = unb ? 0 : 8;
+        if (static_cast<int>(bounded.size()) <= leaf_threshold) {
+            for (const Item& it : bounded) plain.push_back({it.shape, it.seq});
+            std::sort(plain.begin(), plain.end(), [](auto& a, auto& b) { return a.second < b.second; });
+            bounded.clear();
+        }
+        out.plain_start[k] = static_cast<int>(out.prim_shape.size());
+        out.plain_count[k] = static_cast<int>(plain.size());
+        for (auto [si, seq] : plain) {
+            out.prim_shape.push_back(si);
+            out.prim_seq.push_back(seq);
+        }
+        out.always_prims += static_cast<int>(plain.size());
+        if (!bounded.empty()) {
+            LocalBuilder lb{out, std::move(bounded)};
+            const int budget = stack_cap - depth[k] - 2;
+            if (budget < 1) return false;
+            out.local_root[k] = lb.build(0, static_cast<int>(lb.items.size()), 0, budget);
+            out.bounded_prims += static_cast<int>(lb.items.size());
+            max_stack = std::max(max_stack, depth[k] + lb.max_depth_seen + 2);
+        }
+        max_stack = std::max(max_stack, depth[k] + 1);
+    }
+
+    // Content boxes of inner nodes (children first) and the visit-order hint.
+    std::vector<char> done(N, 0);
+    std::function<void(int)> visit = [&](int k) {
+        if (done[k]) return;
+        done[k] = 1;
+        const FlatNode& nd = nodes[k];
+        if (nd.leftChild == -1) return;
+        visit(nd.leftChild);
+        visit(nd.rightChild);
+        const int l = nd.leftChild, r = nd.rightChild;
+        Box3 c = out.content[l];
+        grow(c, out.content[r]);
+        out.content[k] = c;
+        const bool bounded = (out.flags[l] & 8) && (out.flags[r] & 8);
+        int axis = 0;
+        float best = -1.f;
+        for (int a = 0; a < 3; ++a) {
+            float dl = 0.5f * (out.content[l].lo[a] + out.content[l].hi[a]);
+            float dr = 0.5f * (out.content[r].lo[a] + out.content[r].hi[a]);
+            float g = std::fabs(dl - dr);
+            if (std::isfinite(g) && g > best) {
+                best = g;
+                axis = a;
+            }
+        }
+        float cl = 0.5f * (out.content[l].lo[axis] + out.content[l].hi[axis]);
+        float crr = 0.5f * (out.content[r].lo[axis] + out.content[r].hi[axis]);
+        const int swap = (std::isfinite(cl) && std::isfinite(crr) && cl > crr) ? 1 : 0;
+        out.flags[k] = axis | (swap << 2) | (bounded ? 8 : 0);
+    };
+    visit(N - 1);
+    out.max_stack = max_stack;
+    return max_stack <= stack_cap;
+}
+
+}  // namespace rta

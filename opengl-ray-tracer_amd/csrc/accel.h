@@ -1,0 +1,60 @@
+// accel.h — host-side builder of the exact-result accelerator (librtamd.so).
+//
+// The reference tests every shape of every leaf whose box a ray enters
+// (gpu_shader.comp:399-421) and keeps the nearest INNER hit, the first one in
+// walk order on a tie. Its spatial-midpoint tree collapses into leaves of
+// thousands of shapes, so most of the work is those scans.
+// The accelerator keeps the reference's result bit for bit while skipping
+// shapes that provably cannot win:
+//
+//   * the set of shapes a ray may hit is still decided by the reference's own
+//     nodes and exact box test (which leaves a lane enters never changes);
+//   * inside a large leaf, shapes are grouped under a local BVH whose boxes
+//     are *conservative*: each contains every point the reference test can
+//     return as an INNER hit for that shape, padded well beyond float error.
+//     Shapes without such a bound (planes, walls with a ±Y normal whose basis
+//     is NaN, triangles whose stored plane disagrees with their vertices or
+//     that are too thin to bound their barycentric error) are tested always;
+//   * a lane skips a local box only if its entry distance exceeds the lane's
+//     best hit by a relative margin, and every candidate carries its rank in
+//     the reference walk ("seq"), so the winner is the lexicographic minimum
+//     of (distance, seq): exactly the reference's strict-< first-wins rule.
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/rt_flat.h"
+
+namespace rta {
+
+struct Box3 {
+    float lo[3], hi[3];
+};
+
+struct AccelHost {
+    // prims: the shapes in the order the accelerated kernel reads them.
+    std::vector<int> prim_shape;  // shape index per prim slot
+    std::vector<int> prim_seq;    // rank in the reference walk
+    // Per top-level (reference) node: content box + flags, and for leaves
+    // the plain-scan range [plain_start, +plain_count) and the local root.
+    std::vector<Box3> content;
+    std::vector<int> flags;       // bit0-1 order axis, bit2 swap, bit3 bounded
+    std::vector<int> plain_start, plain_count, local_root;
+    // Local BVH nodes: box; inner: left, right | axis<<30; leaf: -(start+1), count.
+    std::vector<Box3> lbox;
+    std::vector<int> la, lb;
+    int max_stack = 0;            // worst-case wave stack entries
+    int always_prims = 0, bounded_prims = 0, local_leaves = 0;
+};
+
+// Builds the accelerator for a validated reference tree (see check_tree).
+// leaf_threshold: leaves with more shapes than this get a local BVH.
+bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                 int leaf_threshold, int stack_cap, AccelHost& out);
+
+// Conservative bound of every INNER hit point of a shape (barycentric mode).
+// Returns false when no finite bound exists.
+bool shape_bound(const FlatShape& s, Box3& b);
+
+}  // namespace rta

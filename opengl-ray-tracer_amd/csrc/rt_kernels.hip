@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/rt_api.h"
+#include "accel.h"
 #include "rt_device.h"
 
 using namespace rtd;
@@ -41,7 +42,8 @@ constexpr int kBlock = 256;
 constexpr int kTileW = 32;  // pixels per block row (4 waves x 8)
 constexpr int kTileH = 8;
 constexpr int kMaxStack = 64;  // gpu_shader.comp:384
-constexpr int kRing = 1024;    // dispatch timings kept between rt_kernel_times calls
+constexpr int kRing = 1024;
+constexpr int kLeafScan = 8;   // leaves with more shapes get a local BVH (accel.h)    // dispatch timings kept between rt_kernel_times calls
 
 // Stats slots, in rt_stats field order.
 enum {
@@ -506,6 +508,300 @@ __global__ __launch_bounds__(kBlock) void k_packet(const float4* __restrict__ ge
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
 }
 
+// ---------------------------------------------------------------------------
+// k_accel: the packet walk over the reference tree plus the exact-result
+// accelerator (accel.h). Which reference leaves a lane enters is decided by
+// the reference's own box test; inside them, conservative local boxes and a
+// distance margin skip shapes that cannot win; every candidate carries its
+// rank in the reference walk so that ties resolve exactly as the reference's
+// strict "<" in walk order does (lexicographic minimum of (distance, rank)).
+// Barycentric triangle test only (the default); Moller-Trumbore frames use
+// k_packet.
+
+struct AccelPtrs {
+    const float4* __restrict__ anodes;  // 4 float4 per reference node
+    const float4* __restrict__ lnodes;  // 2 float4 per local node
+    const float4* __restrict__ prims;   // 5 float4 per prim, f[17] = rank
+    int N;
+};
+
+struct Best {
+    float d;
+    int seq;
+    V p;
+    int slot;
+};
+
+constexpr float kPruneRel = 1.002f;  // distance margin for skipping a box (accel.h)
+
+__device__ __forceinline__ bool lex_better(float d, int seq, const Best& b) {
+    return d < b.d || (d == b.d && seq < b.seq);
+}
+
+// gpu_shader.comp:242-328 for one candidate, taking the winner test early:
+// the hit point and distance are computed exactly as the reference does, and
+// the remaining (wall / barycentric) checks only run when the candidate could
+// win. Same result as testing first and comparing after.
+__device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray& r, Best& b) {
+    const float* f = g.f;
+    const int seq = __float_as_int(f[17]);
+    if (g.type == 0) {
+        V c = mk(f[0], f[1], f[2]);
+        V oc = r.o - c;
+        float aa = dot(r.d, r.d);
+        float bb = 2.0f * dot(r.d, oc);
+        float cc = dot(oc, oc) - f[3] * f[3];
+        float D = bb * bb - 4.0f * aa * cc;
+        if (D > 0.0f) {
+            float t1 = (-bb - __builtin_sqrtf(D)) / (2.0f * aa);
+            if (t1 > 0.0f) {
+                V p = r.o + t1 * r.d;
+                float d = dist(r.o, p);
+                if (lex_better(d, seq, b)) b = Best{d, seq, p, slot};
+            }
+        }
+        return;
+    }
+    if (g.type < 1 || g.type > 3) return;
+    V n = mk(f[0], f[1], f[2]);
+    float np = dot(n, r.d);
+    if (np == 0.0f) return;
+    float t = -(f[3] + dot(n, r.o)) / np;
+    if (!(t > 0.0f) || !(np > 0.0f)) return;
+    V p = r.o + t * r.d;
+    float d = dist(r.o, p);
+    if (!lex_better(d, seq, b)) return;
+    if (g.type == 2) {
+        V lp = p - mk(f[4], f[5], f[6]);
+        float up = dot(lp, mk(f[9], f[10], f[11]));
+        float vp = dot(lp, mk(f[12], f[13], f[14]));
+        if (up < 0.0f || up > f[7] || vp < 0.0f || vp > f[8]) return;
+    } else if (g.type == 3) {
+        V tp = p - mk(f[4], f[5], f[6]);
+        float d20 = dot(tp, mk(f[7], f[8], f[9]));
+        float d21 = dot(tp, mk(f[10], f[11], f[12]));
+        float v = (f[15] * d20 - f[14] * d21) / f[16];
+        float w = (f[13] * d21 - f[14] * d20) / f[16];
+        float u = 1.0f - v - w;
+        if (u < 0.0f || v < 0.0f || w < 0.0f) return;
+    }
+    b = Best{d, seq, p, slot};
+}
+
+// Shadow candidate: an INNER hit nearer than lim (gpu_shader.comp:473-480).
+__device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float lim) {
+    const float* f = g.f;
+    if (g.type == 0) {
+        V c = mk(f[0], f[1], f[2]);
+        V oc = r.o - c;
+        float aa = dot(r.d, r.d);
+        float bb = 2.0f * dot(r.d, oc);
+        float cc = dot(oc, oc) - f[3] * f[3];
+        float D = bb * bb - 4.0f * aa * cc;
+        if (!(D > 0.0f)) return false;
+        float t1 = (-bb - __builtin_sqrtf(D)) / (2.0f * aa);
+        return t1 > 0.0f && dist(r.o, r.o + t1 * r.d) < lim;
+    }
+    if (g.type < 1 || g.type > 3) return false;
+    V n = mk(f[0], f[1], f[2]);
+    float np = dot(n, r.d);
+    if (np == 0.0f) return false;
+    float t = -(f[3] + dot(n, r.o)) / np;
+    if (!(t > 0.0f) || !(np > 0.0f)) return false;
+    V p = r.o + t * r.d;
+    if (!(dist(r.o, p) < lim)) return false;
+    if (g.type == 2) {
+        V lp = p - mk(f[4], f[5], f[6]);
+        float up = dot(lp, mk(f[9], f[10], f[11]));
+        float vp = dot(lp, mk(f[12], f[13], f[14]));
+        return !(up < 0.0f || up > f[7] || vp < 0.0f || vp > f[8]);
+    }
+    if (g.type == 3) {
+        V tp = p - mk(f[4], f[5], f[6]);
+        float d20 = dot(tp, mk(f[7], f[8], f[9]));
+        float d21 = dot(tp, mk(f[10], f[11], f[12]));
+        float v = (f[15] * d20 - f[14] * d21) / f[16];
+        float w = (f[13] * d21 - f[14] * d20) / f[16];
+        float u = 1.0f - v - w;
+        return !(u < 0.0f || v < 0.0f || w < 0.0f);
+    }
+    return true;
+}
+
+// Conservative slab test on a padded box: NaN-free (zero direction components
+// use a huge finite reciprocal), accepts iff the ray's forward part meets the
+// box no farther than `limp` (in distance units, dlen = |dir|).
+__device__ __forceinline__ bool padded_hit(V o, V invs, float dlen, float4 lo, float4 hi, float limp) {
+    float tx0 = (lo.x - o.x) * invs.x, tx1 = (hi.x - o.x) * invs.x;
+    float ty0 = (lo.y - o.y) * invs.y, ty1 = (hi.y - o.y) * invs.y;
+    float tz0 = (lo.z - o.z) * invs.z, tz1 = (hi.z - o.z) * invs.z;
+    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+    float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return tmax >= fmaxf(tmin, 0.0f) && tmin * dlen <= limp;
+}
+
+__device__ __forceinline__ float safe_inv(float d) { return d == 0.0f ? copysignf(1e30f, d) : 1.0f / d; }
+
+__device__ __forceinline__ float axis_of(V v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+// Direction component of the first lane of `m` along `axis` (wave-uniform).
+__device__ __forceinline__ float rep_dir(V d, int axis, unsigned long long m) {
+    const int lane = __builtin_ctzll(m);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(axis_of(d, axis)), lane));
+}
+
+template <bool SHADOW>
+__device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
+                           bool& shadow) {
+    const unsigned long long m0 = __ballot(active);
+    if (A.N <= 0 || m0 == 0) return;
+    const V inv = inv_dir(r.d);  // exact reciprocal: the reference box test
+    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
+    const float dlen = len(r.d);
+    WaveStack st{0, 0, 0, 0};
+    st.push(A.N - 1, m0);
+    unsigned long long done = 0;
+    while (st.sp > 0) {
+        int code;
+        unsigned long long m;
+        st.pop(code, m);
+        if (SHADOW) m &= ~done;
+        if (m == 0) continue;
+        code = uni(code);
+        const float lim = SHADOW ? lim_shadow : b.d;
+        const float limp = lim * kPruneRel + 1e-6f;
+        if (code >= 0) {
+            // reference node: exact box (which leaves the lane enters), then
+            // the conservative content box (distance pruning) when bounded
+            const float4* q = A.anodes + 4 * static_cast<size_t>(code);
+            const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
+            const int flags = uni(__float_as_int(c0.w));
+            bool hb = lane_in(m) && ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z));
+            if (flags & 8) hb = hb && padded_hit(r.o, invs, dlen, c0, c1, limp);
+            const unsigned long long mh = __ballot(hb);
+            if (mh == 0) continue;
+            const int ia = uni(__float_as_int(e0.w)), ib = uni(__float_as_int(e1.w));
+            if (ia < 0) {
+                const int start = -ia - 1;
+                bool live = hb;
+                for (int i = 0; i < ib; ++i) {
+                    const GeoRec g = load_rec(A.prims, start + i);
+                    if (live) {
+                        if (SHADOW) {
+                            if (try_shadow(g, r, lim_shadow)) {
+                                shadow = true;
+                                live = false;
+                            }
+                        } else {
+                            try_closest(g, start + i, r, b);
+                        }
+                    }
+                    if (SHADOW && __ballot(live) == 0) break;
+                }
+                const int lroot = uni(__float_as_int(c1.w));
+                unsigned long long ml = mh;
+                if (SHADOW) {
+                    done = __ballot(shadow);
+                    ml &= ~done;
+                }
+                if (lroot >= 0 && ml) st.push(-(lroot + 1), ml);
+            } else {
+                const int axis = flags & 3;
+                const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
+                const bool fwd = rep_dir(r.d, axis, mh) >= 0.0f;
+                st.push(fwd ? upper : lower, mh);  // far first, near popped next
+                st.push(fwd ? lower : upper, mh);
+            }
+        } else {
+            const int j = -code - 1;
+            const float4* q = A.lnodes + 2 * static_cast<size_t>(j);
+            const float4 lo = q[0], hi = q[1];
+            const bool hb = lane_in(m) && padded_hit(r.o, invs, dlen, lo, hi, limp);
+            const unsigned long long mh = __ballot(hb);
+            if (mh == 0) continue;
+            const int la = uni(__float_as_int(lo.w)), lb = uni(__float_as_int(hi.w));
+            if (la < 0) {
+                const int start = -la - 1;
+                bool live = hb;
+                for (int i = 0; i < lb; ++i) {
+                    const GeoRec g = load_rec(A.prims, start + i);
+                    if (live) {
+                        if (SHADOW) {
+                            if (try_shadow(g, r, lim_shadow)) {
+                                shadow = true;
+                                live = false;
+                            }
+                        } else {
+                            try_closest(g, start + i, r, b);
+                        }
+                    }
+                    if (SHADOW && __ballot(live) == 0) break;
+                }
+                if (SHADOW) {
+                    done = __ballot(shadow);
+                    if ((m0 & ~done) == 0) break;
+                }
+            } else {
+                const int axis = (lb >> 30) & 3, right = lb & 0x3fffffff;
+                const bool fwd = rep_dir(r.d, axis, mh) >= 0.0f;
+                st.push(fwd ? right : la, mh);
+                st.push(fwd ? la : right, mh);
+            }
+        }
+    }
+}
+
+// Same stack encoding for local nodes: code = -(j+1).
+__global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ anodes,
+                                                  const float4* __restrict__ lnodes,
+                                                  const float4* __restrict__ prims,
+                                                  const float4* __restrict__ mat, KParams kp) {
+    const AccelPtrs A{anodes, lnodes, prims, kp.N};
+    const PixelCoord pc = pixel_of(kp);
+    const V bg = background(kp, pc.y);
+    Ray ray = primary_ray(kp, pc.x, pc.y);
+    V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
+    bool alive = pc.active;
+    for (int depth = 0; depth < kp.maxBounces; ++depth) {
+        if (__ballot(alive) == 0) break;
+        Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
+        bool unused = false;
+        accel_walk<false>(A, ray, alive, 0.f, best, unused);
+        if (alive && best.slot < 0) {
+            acc = acc + mulv(att, bg);
+            alive = false;
+        }
+        V hn = mk(0.f, 0.f, 0.f);
+        Mat m{};
+        Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
+        float ld = 0.f;
+        if (alive) {
+            const GeoRec g = load_rec(prims, best.slot);
+            hn = shape_normal(g, best.p);
+            m = load_mat(mat, g.idx);
+            sr = Ray{best.p + hn * 1e-3f, normalize(kp.light_pos - best.p)};
+            ld = dist(kp.light_pos, best.p);
+        }
+        bool shadow = false;
+        Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
+        accel_walk<true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow);
+        if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
+    }
+    if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+}
+
+__global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __restrict__ prim_shape,
+                             const int* __restrict__ prim_seq, int P, float4* __restrict__ prims) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= P) return;
+    const float4* src = geo_lin + 5 * static_cast<size_t>(prim_shape[j]);
+    float4* dst = prims + 5 * static_cast<size_t>(j);
+    for (int k = 0; k < 4; ++k) dst[k] = src[k];
+    float4 last = src[4];
+    last.w = __int_as_float(prim_seq[j]);  // f[17]: rank in the reference walk
+    dst[4] = last;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -533,11 +829,18 @@ struct rt_ctx {
     int* staging_idx = nullptr;
     size_t staging_idx_cap = 0;
     std::vector<int> host_idx;
+    std::vector<FlatShape> host_shapes;
+    // exact-result accelerator (accel.h)
+    float4 *anodes = nullptr, *lnodes = nullptr, *prims = nullptr;
+    int* prim_idx_dev = nullptr;
+    bool accel_ok = false;
+    rta::AccelHost accel;
     // frame constants
     FlatCamera cam{};
     FlatLight light{};
     rt_params params{0.f, 0.f, 0, 0, 0, 0};  // the reference's first frame sees zeros
     int kernel = RT_KERNEL_AUTO;
+    int last_kind = 0;
     // own surface
     float* img = nullptr;
     size_t img_pitch = 0;
@@ -576,6 +879,13 @@ void free_scene(rt_ctx* c) {
     hipFree(c->mat);
     hipFree(c->nodes);
     c->geo_lin = c->geo_leaf = c->mat = c->nodes = nullptr;
+    hipFree(c->anodes);
+    hipFree(c->lnodes);
+    hipFree(c->prims);
+    hipFree(c->prim_idx_dev);
+    c->anodes = c->lnodes = c->prims = nullptr;
+    c->prim_idx_dev = nullptr;
+    c->accel_ok = false;
     c->have_scene = false;
 }
 
@@ -610,6 +920,75 @@ int check_tree(const FlatNode* nodes, int N, const int* idx, int I, int S, int* 
     }
     if (ms > kMaxStack) return RT_ERR_BVH;
     *max_stack = ms;
+    return RT_OK;
+}
+
+inline float bits_f(int v) {
+    float f;
+    std::memcpy(&f, &v, sizeof f);
+    return f;
+}
+
+// Builds the accelerator from the host copies of the scene and uploads it;
+// expects geo_lin to be packed (k_pack_prims copies from it). On failure the
+// context keeps rendering with k_packet.
+int upload_accel(rt_ctx* c) {
+    hipFree(c->anodes);
+    hipFree(c->lnodes);
+    hipFree(c->prims);
+    hipFree(c->prim_idx_dev);
+    c->anodes = c->lnodes = c->prims = nullptr;
+    c->prim_idx_dev = nullptr;
+    c->accel_ok = false;
+    const int N = c->N;
+    if (N == 0) return RT_OK;
+    rta::AccelHost& A = c->accel;
+    if (!rta::build_accel(c->host_shapes.data(), c->S, c->host_nodes.data(), N, c->host_idx.data(), c->I,
+                          kLeafScan, kMaxStack, A))
+        return RT_OK;
+    std::vector<float4> an(4 * static_cast<size_t>(N));
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& n = c->host_nodes[k];
+        int a, b;
+        if (n.leftChild == -1) {
+            a = -(A.plain_start[k] + 1);
+            b = A.plain_count[k];
+        } else {
+            a = n.leftChild;
+            b = n.rightChild;
+        }
+        const rta::Box3& cb = A.content[k];
+        an[4 * k + 0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(a));
+        an[4 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(b));
+        an[4 * k + 2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[k]));
+        an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], bits_f(A.local_root[k]));
+    }
+    const size_t M = A.lbox.size(), P = A.prim_shape.size();
+    std::vector<float4> ln(2 * (M ? M : 1));
+    for (size_t j = 0; j < M; ++j) {
+        const rta::Box3& bx = A.lbox[j];
+        ln[2 * j] = make_float4(bx.lo[0], bx.lo[1], bx.lo[2], bits_f(A.la[j]));
+        ln[2 * j + 1] = make_float4(bx.hi[0], bx.hi[1], bx.hi[2], bits_f(A.lb[j]));
+    }
+    std::vector<int> ps(2 * (P ? P : 1));
+    for (size_t i = 0; i < P; ++i) {
+        ps[i] = A.prim_shape[i];
+        ps[P + i] = A.prim_seq[i];
+    }
+    if (hipMalloc(&c->anodes, an.size() * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->lnodes, ln.size() * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->prims, 5 * (P ? P : 1) * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->prim_idx_dev, ps.size() * sizeof(int)) != hipSuccess)
+        return RT_ERR_NO_MEMORY;
+    HIP_TRY(hipMemcpyAsync(c->anodes, an.data(), an.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->lnodes, ln.data(), ln.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->prim_idx_dev, ps.data(), ps.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (P > 0)
+        hipLaunchKernelGGL(k_pack_prims, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->geo_lin, c->prim_idx_dev,
+                           c->prim_idx_dev + P, static_cast<int>(P), c->prims);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));  // the host vectors die here
+    c->accel_ok = true;
     return RT_OK;
 }
 
@@ -660,7 +1039,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     if (kp.out_rows == 0) return RT_OK;
     dim3 grid((kp.width + kTileW - 1) / kTileW, (kp.out_rows + kTileH - 1) / kTileH);
     if (grid.y > 65535u) return RT_ERR_INVALID;
-    int kind = c->kernel == RT_KERNEL_AUTO ? RT_KERNEL_PACKET : c->kernel;
+    int kind = c->kernel;
+    const bool accel_usable = c->accel_ok && kp.useBVH && !kp.useMT;
+    if (kind == RT_KERNEL_AUTO) kind = accel_usable ? RT_KERNEL_ACCEL : RT_KERNEL_PACKET;
+    if (kind == RT_KERNEL_ACCEL && !accel_usable) kind = RT_KERNEL_PACKET;  // same image either way
     const size_t lds = static_cast<size_t>(kp.max_stack) * kBlock * sizeof(int);
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (!stats && c->ring_used < static_cast<int>(c->ring0.size())) {
@@ -674,10 +1056,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     } else if (kind == RT_KERNEL_LANE) {
         hipLaunchKernelGGL(k_lane<false>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
                            c->nodes, kp);
+    } else if (kind == RT_KERNEL_ACCEL) {
+        hipLaunchKernelGGL(k_accel, grid, dim3(kBlock), 0, c->stream, c->anodes, c->lnodes, c->prims, c->mat, kp);
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
                            kp);
     }
+    c->last_kind = stats ? RT_KERNEL_LANE : kind;
     HIP_TRY(hipGetLastError());
     if (!stats) {
         HIP_TRY(hipEventRecord(e1, c->stream));
@@ -804,8 +1189,9 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->max_stack = ms;
     c->host_nodes.assign(nodes, nodes + N);
     c->host_idx.assign(idx, idx + I);
+    c->host_shapes.assign(shapes, shapes + S);
     c->have_scene = true;
-    return RT_OK;
+    return upload_accel(c);
 }
 
 int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
@@ -821,7 +1207,8 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
                        c->S, c->staging_idx, c->I, c->geo_lin, c->geo_leaf, c->mat);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));  // glBufferSubData semantics: the host array may be reused
-    return RT_OK;
+    std::copy(shapes, shapes + count, c->host_shapes.begin() + first);
+    return upload_accel(c);  // moved shapes change the conservative bounds
 }
 
 int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
@@ -838,7 +1225,8 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
     hipLaunchKernelGGL(k_pack_nodes, dim3((N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, N, c->nodes);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host array may be reused after return
-    return RT_OK;
+    c->host_nodes.assign(nodes, nodes + N);
+    return upload_accel(c);
 }
 
 int rt_set_camera(rt_ctx* c, const FlatCamera* cam) {
@@ -862,7 +1250,7 @@ int rt_set_params(rt_ctx* c, const rt_params* p) {
 }
 
 int rt_set_kernel(rt_ctx* c, int kernel) {
-    if (!c || kernel < RT_KERNEL_AUTO || kernel > RT_KERNEL_PACKET) return RT_ERR_INVALID;
+    if (!c || kernel < RT_KERNEL_AUTO || kernel > RT_KERNEL_ACCEL) return RT_ERR_INVALID;
     c->kernel = kernel;
     return RT_OK;
 }
@@ -982,3 +1370,15 @@ int rt_last_kernel_ms(rt_ctx* c, float* ms) {
 }
 
 }  // extern "C"
+
+extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    out->built = c->accel_ok ? 1 : 0;
+    out->local_nodes = static_cast<int>(c->accel.lbox.size());
+    out->local_leaves = c->accel.local_leaves;
+    out->bounded_prims = c->accel.bounded_prims;
+    out->always_prims = c->accel.always_prims;
+    out->max_stack = c->accel.max_stack;
+    out->last_kernel = c->last_kind;
+    return RT_OK;
+}

@@ -69,13 +69,18 @@ LIGHT_DTYPE = np.dtype({
 })
 
 SPHERE, PLANE, WALL, TRIANGLE = 0, 1, 2, 3
-KERNEL_AUTO, KERNEL_LANE, KERNEL_PACKET = 0, 1, 2
+KERNEL_AUTO, KERNEL_LANE, KERNEL_PACKET, KERNEL_ACCEL = 0, 1, 2, 3
 
 
 class rt_params(C.Structure):
     """Uniforms of gpu_shader.comp:126-130."""
     _fields_ = [("resX", C.c_float), ("resY", C.c_float), ("maxBounces", C.c_int), ("useBVH", C.c_int),
                 ("useFresnel", C.c_int), ("useMollerTrumbore", C.c_int)]
+
+
+class rt_accel_info(C.Structure):
+    _fields_ = [(n, C.c_int) for n in ("built", "local_nodes", "local_leaves", "bounded_prims", "always_prims",
+                                       "max_stack", "last_kernel")]
 
 
 class rt_stats(C.Structure):
@@ -168,6 +173,7 @@ RT_SYMBOLS = {
     "rt_collect_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
     "rt_last_kernel_ms": (_I, [_P, _P]),
     "rt_kernel_times": (_I, [_P, _P, _I]),
+    "rt_accel_info_get": (_I, [_P, _P]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
 
@@ -403,6 +409,11 @@ class ComputeShader:
         if n < 0:
             raise RTError("rt_kernel_times", n)
         return buf[:min(n, cap)].copy()
+
+    def accel_info(self):
+        a = rt_accel_info()
+        self._chk(self._lib.rt_accel_info_get(self._h, C.byref(a)), "rt_accel_info_get")
+        return {n: getattr(a, n) for n, _ in rt_accel_info._fields_}
 
     def last_kernel_ms(self):
         ms = C.c_float()

@@ -64,7 +64,10 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("kernel", [rtamd.KERNEL_PACKET, rtamd.KERNEL_LANE])
+KERNELS = [rtamd.KERNEL_ACCEL, rtamd.KERNEL_PACKET, rtamd.KERNEL_LANE]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("case", CASES, ids=lambda c: "c%d_%dx%d_y%d_b%d_bvh%d_f%d_mt%d" % (
     c[0], c[1], c[2], c[3], c[5], c[6], c[7], c[8]))
 def test_parity_vs_oracle(ctx, case, kernel):
@@ -102,7 +105,7 @@ def test_golden_frames_on_gpu(golden_dir):
     for (cfg, w, h, mb, bvh, fr, mt) in FRAME_CASES:
         fs = rtamd.generate(cfg, 0, w, h)
         key = f"c{cfg}_w{w}_h{h}_b{mb}_bvh{bvh}_f{fr}_mt{mt}"
-        for k in (rtamd.KERNEL_PACKET, rtamd.KERNEL_LANE):
+        for k in KERNELS:
             img = gpu_rows(c, fs, w, h, oracle.params(w, h, mb, bvh, fr, mt), kernel=k)
             check(img, data[key], key)
     c.close()
@@ -118,7 +121,10 @@ def test_full_frame_packet_equals_lane(ctx, cfg):
     p = oracle.params(W, H, CFG_BOUNCES[cfg])
     a = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_PACKET)
     b = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_LANE)
+    c = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+    assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL
     assert np.array_equal(a, b)
+    assert np.array_equal(a, c)
     assert (a[..., 3] == 1).all()
 
 
@@ -257,3 +263,67 @@ def test_pitched_destination(ctx):
     ref, _ = oracle.render(fs, W, H, p)
     check(o[:, :W], ref, "pitched")
     assert (o[:, W:] == 9.0).all()
+
+
+# --------------------------------------------------------------------------
+# The accelerator's exactness on adversarial scenes: giant leaves that mix
+# bounded shapes with unbounded ones (planes, ±Y walls, thin triangles,
+# triangles whose stored plane is off their vertices), exact distance ties.
+
+def _soup(seed, n_tri=2500):
+    rng = np.random.default_rng(seed)
+    sc = rtamd.Scene()
+    for i in range(n_tri):
+        c = rng.uniform(-20, 20, 3)
+        c[1] = rng.uniform(-4, 4)
+        v = c + rng.normal(size=(3, 3)) * rng.uniform(0.3, 2.0)
+        if i % 97 == 0:  # sliver: third vertex on the first edge
+            v[2] = v[0] + (v[1] - v[0]) * 0.37 + rng.normal(size=3) * 1e-4
+        sc.add_triangle(v[0], v[1], v[2], invert=bool(i % 2),
+                        mat=rtamd.material(color=rng.uniform(0, 1, 3), specular=0.3 if i % 5 == 0 else 0.0))
+    for i in range(40):
+        sc.add_sphere(rng.uniform(-20, 20, 3), rng.uniform(0.3, 2.5),
+                      mat=rtamd.material(color=rng.uniform(0, 1, 3)))
+    sc.add_wall((-30, 6, -30), 60, 60, (0, 1, 0), mat=rtamd.material(color=(0.6, 0.2, 0.3), specular=0.0))
+    sc.add_wall((-10, -10, -25), 20, 15, (0.1, 0.2, 1.0), mat=rtamd.material(specular=0.8))
+    sc.add_plane((0, 0, 1), (0, 0, -40), mat=rtamd.material(color=(0.2, 0.5, 0.2), specular=0.0))
+    sc.set_camera((5, -25, 45), 60, 4 / 3)
+    sc.LookAt((0, 0, 0))
+    sc.set_light((10, -30, 20), (1, 1, 1), 40)
+    sc.buildBVH(1)  # one split: two leaves of ~1,300 shapes each
+    fs = sc.serializeScene()
+    tri = np.where(fs.shapes["type"] == 3)[0]
+    # stored plane shifted off the vertices for a few triangles
+    fs.shapes["planeD"][tri[::211]] += np.float32(0.5)
+    return fs
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+@pytest.mark.parametrize("fresnel", [0, 1])
+def test_accel_exact_on_adversarial_soup(ctx, seed, fresnel):
+    W, H = 200, 150
+    fs = _soup(seed)
+    p = oracle.params(W, H, 3, True, fresnel)
+    ref, _ = oracle.render(fs, W, H, p)
+    img = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+    info = ctx.accel_info()
+    assert info["built"] and info["last_kernel"] == rtamd.KERNEL_ACCEL and info["always_prims"] > 0
+    check(img, ref, f"soup {seed}")
+
+
+def test_accel_ties_resolve_like_the_reference(ctx):
+    """Each road triangle duplicated with another colour: identical distances;
+    the reference keeps the first in its walk order."""
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    road = np.where((fs.shapes["type"] == 3) & (fs.shapes["material"]["specularStrength"] > 0.2))[0]
+    dup = fs.shapes[road].copy()
+    dup["material"]["color"] = (1.0, 0.0, 0.0)
+    shapes = np.concatenate([fs.shapes, dup])
+    sc_nodes, sc_idx = oracle.build_bvh(shapes, 25)
+    fs2 = rtamd.FlatScene(shapes, sc_nodes, sc_idx, fs.camera, fs.light)
+    p = oracle.params(W, H, 3)
+    ref, _ = oracle.render(fs2, W, H, p, y0=900, out_rows=40)
+    for k in KERNELS:
+        img = gpu_rows(ctx, fs2, W, H, p, y0=900, rows=40, kernel=k)
+        check(img, ref, f"ties kernel {k}")
