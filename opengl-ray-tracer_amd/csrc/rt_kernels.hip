@@ -744,8 +744,8 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
             } else {
                 const int axis = (lb >> 30) & 3, right = lb & 0x3fffffff;
                 const bool fwd = rep_dir(r.d, axis, mh) >= 0.0f;
-                st.push(fwd ? right : la, mh);
-                st.push(fwd ? la : right, mh);
+                st.push(-((fwd ? right : la) + 1), mh);  // local codes are negative
+                st.push(-((fwd ? la : right) + 1), mh);
             }
         }
     }

@@ -126,6 +126,16 @@ def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
 
 
+def as_records(a, dtype):
+    """Contiguous array with exactly the C record layout. numpy may pack a
+    padded structured dtype (np.concatenate does), which would hand the C side
+    records of the wrong size."""
+    a = np.asarray(a)
+    if a.dtype != dtype:
+        a = a.astype(dtype)
+    return np.ascontiguousarray(a)
+
+
 _P = C.c_void_p
 _I = C.c_int
 
@@ -225,6 +235,13 @@ class FlatScene:
     indices: np.ndarray
     camera: np.ndarray
     light: np.ndarray
+
+    def __post_init__(self):
+        self.shapes = as_records(self.shapes, SHAPE_DTYPE)
+        self.nodes = as_records(self.nodes, NODE_DTYPE)
+        self.indices = np.ascontiguousarray(self.indices, np.int32)
+        self.camera = as_records(self.camera, CAMERA_DTYPE).reshape(1)
+        self.light = as_records(self.light, LIGHT_DTYPE).reshape(1)
 
 
 class Scene:
@@ -351,19 +368,19 @@ class ComputeShader:
         self.set_light(fs.light)
 
     def update_shapes(self, first, shapes):
-        shapes = np.ascontiguousarray(shapes, SHAPE_DTYPE)
+        shapes = as_records(shapes, SHAPE_DTYPE)
         self._chk(self._lib.rt_update_shapes(self._h, first, len(shapes), _ptr(shapes)), "rt_update_shapes")
 
     def update_nodes(self, nodes):
-        nodes = np.ascontiguousarray(nodes, NODE_DTYPE)
+        nodes = as_records(nodes, NODE_DTYPE)
         self._chk(self._lib.rt_update_nodes(self._h, _ptr(nodes), len(nodes)), "rt_update_nodes")
 
     def set_camera(self, cam):
-        cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+        cam = as_records(cam, CAMERA_DTYPE)
         self._chk(self._lib.rt_set_camera(self._h, _ptr(cam)), "rt_set_camera")
 
     def set_light(self, light):
-        light = np.ascontiguousarray(light, LIGHT_DTYPE)
+        light = as_records(light, LIGHT_DTYPE)
         self._chk(self._lib.rt_set_light(self._h, _ptr(light)), "rt_set_light")
 
     def set_params(self, resX, resY, maxBounces=3, useBVH=True, useFresnel=False, useMollerTrumbore=False):

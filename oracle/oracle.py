@@ -102,6 +102,7 @@ def cpu_raytracer(fs: rtamd.FlatScene, width, height, y0=0, y1=None, threads=1, 
 
 def build_bvh(shapes: np.ndarray, max_depth: int):
     """Independent restatement of buildBVH + serializeBVH; returns (nodes, indices)."""
+    shapes = rtamd.as_records(shapes, rtamd.SHAPE_DTYPE)
     n, i = C.c_int(), C.c_int()
     lib().orc_build_bvh(_p(shapes), len(shapes), max_depth, None, 0, None, 0, C.byref(n), C.byref(i))
     nodes = np.zeros(n.value, rtamd.NODE_DTYPE)
@@ -114,6 +115,7 @@ def build_bvh(shapes: np.ndarray, max_depth: int):
 
 
 def intersect(shape_rec: np.ndarray, o, d, use_mt=False):
+    shape_rec = rtamd.as_records(shape_rec, rtamd.SHAPE_DTYPE)
     o = np.asarray(o, np.float32)
     d = np.asarray(d, np.float32)
     hit = np.zeros(3, np.float32)
@@ -122,6 +124,7 @@ def intersect(shape_rec: np.ndarray, o, d, use_mt=False):
 
 
 def intersect_cpu(shape_rec: np.ndarray, o, d):
+    shape_rec = rtamd.as_records(shape_rec, rtamd.SHAPE_DTYPE)
     o = np.asarray(o, np.float32)
     d = np.asarray(d, np.float32)
     hit = np.zeros(3, np.float32)

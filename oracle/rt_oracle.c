@@ -36,6 +36,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <float.h>
+#include <stddef.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -708,5 +709,32 @@ int orc_ray_aabb(const float* o, const float* d, const float* bmin, const float*
 int orc_wall_end(const FlatShape* s, float* e) {
     v3 v = wall_end(s);
     e[0] = v.x; e[1] = v.y; e[2] = v.z;
+    return 0;
+}
+
+/* Closest-hit (shape index or -1, distance) and shadow query (any INNER hit
+ * nearer than lim) of the reference walk for arbitrary rays: the checker for
+ * tests/native/accel_check.cpp. */
+int orc_trace_rays(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                   const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
+                   int* out_shadow) {
+    rt_params p = {1, 1, 1, 1, 0, 0};
+    scene_t sc = {shapes, S, nodes, N, idx, I, NULL, NULL, p};
+#pragma omp parallel for schedule(dynamic, 64)
+    for (int i = 0; i < R; ++i) {
+        ray_t r;
+        r.o = mk(o[3 * i], o[3 * i + 1], o[3 * i + 2]);
+        r.d = mk(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+        hit_t h = intersect_scene2(&sc, r, NULL);
+        out_shape[i] = -1;
+        out_d[i] = 1e20f;
+        if (h.type == INNER) {
+            out_shape[i] = (int)((const FlatShape*)((const char*)h.mat - offsetof(FlatShape, material)) - shapes);
+            out_d[i] = distance3(r.o, h.hit);
+        }
+        float best = 1e20f;
+        (void)best;
+        out_shadow[i] = (h.type == INNER && distance3(r.o, h.hit) < lim[i]) ? 1 : 0;
+    }
     return 0;
 }

@@ -1,0 +1,162 @@
+// accel_check.cpp — TEST HARNESS: scalar CPU emulation of k_accel's walk over
+// the accelerator built by the product's accel.cpp, for checking the
+// accelerator's exactness rules on CPU (tests/test_accel_cpu.py compares its
+// closest-hit choice with the oracle's reference walk). Not product code.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../opengl-ray-tracer_amd/csrc/accel.h"
+
+namespace {
+struct V { float x, y, z; };
+V mk(float x, float y, float z) { return V{x, y, z}; }
+V operator+(V a, V b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+V operator-(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+V operator*(float s, V a) { return {s * a.x, s * a.y, s * a.z}; }
+float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+V cross(V a, V b) { return {a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y}; }
+V normalize(V a) { float s = 1.0f / std::sqrt(dot(a, a)); return {a.x * s, a.y * s, a.z * s}; }
+float dist(V a, V b) { V d = b - a; return std::sqrt(dot(d, d)); }
+float gmin(float a, float b) { return (b < a) ? b : a; }
+float gmax(float a, float b) { return (a < b) ? b : a; }
+V fv(rt_vec3 v) { return {v.x, v.y, v.z}; }
+
+struct Best { float d; int seq; V p; int shape; };
+
+// INNER hit of a shape, GLSL semantics (barycentric), or false.
+bool isect(const FlatShape& s, V o, V d, V& p) {
+    if (s.type == 0) {
+        V c = fv(s.sphereCenter), oc = o - c;
+        float aa = dot(d, d), bb = 2.0f * dot(d, oc), cc = dot(oc, oc) - s.sphereRadius * s.sphereRadius;
+        float D = bb * bb - 4.0f * aa * cc;
+        if (!(D > 0.0f)) return false;
+        float t1 = (-bb - std::sqrt(D)) / (2.0f * aa);
+        if (!(t1 > 0.0f)) return false;
+        p = o + t1 * d;
+        return true;
+    }
+    if (s.type < 1 || s.type > 3) return false;
+    V n = fv(s.planeNormal);
+    float np = dot(n, d);
+    if (np == 0.0f) return false;
+    float t = -(s.planeD + dot(n, o)) / np;
+    if (!(t > 0.0f) || !(np > 0.0f)) return false;
+    p = o + t * d;
+    if (s.type == 2) {
+        V u = normalize(cross(n, mk(0, 1, 0)));
+        if (std::sqrt(dot(u, u)) < 1e-5f) u = normalize(cross(n, mk(1, 0, 0)));
+        V v = normalize(cross(n, u));
+        V lp = p - fv(s.wallStart);
+        float up = dot(lp, u), vp = dot(lp, v);
+        if (up < 0.0f || up > s.wallWidth || vp < 0.0f || vp > s.wallHeight) return false;
+    } else if (s.type == 3) {
+        V p1 = fv(s.triP1), e1 = fv(s.triP2) - p1, e2 = fv(s.triP3) - p1, tp = p - p1;
+        float d00 = dot(e1, e1), d01 = dot(e1, e2), d11 = dot(e2, e2), d20 = dot(tp, e1), d21 = dot(tp, e2);
+        float den = d00 * d11 - d01 * d01;
+        float v = (d11 * d20 - d01 * d21) / den, w = (d00 * d21 - d01 * d20) / den, u = 1.0f - v - w;
+        if (u < 0.0f || v < 0.0f || w < 0.0f) return false;
+    }
+    return true;
+}
+
+bool ref_aabb(V o, V inv, const rt_vec3& lo, const rt_vec3& hi) {
+    float tx0 = (lo.x - o.x) * inv.x, tx1 = (hi.x - o.x) * inv.x;
+    float ty0 = (lo.y - o.y) * inv.y, ty1 = (hi.y - o.y) * inv.y;
+    float tz0 = (lo.z - o.z) * inv.z, tz1 = (hi.z - o.z) * inv.z;
+    float tmin = gmax(gmax(gmin(tx0, tx1), gmin(ty0, ty1)), gmin(tz0, tz1));
+    float tmax = gmin(gmin(gmax(tx0, tx1), gmax(ty0, ty1)), gmax(tz0, tz1));
+    return tmax >= tmin && tmax > 0.0f;
+}
+
+float safe_inv(float d) { return d == 0.0f ? std::copysign(1e30f, d) : 1.0f / d; }
+
+bool padded(V o, V invs, float dlen, const rta::Box3& b, float limp) {
+    float tx0 = (b.lo[0] - o.x) * invs.x, tx1 = (b.hi[0] - o.x) * invs.x;
+    float ty0 = (b.lo[1] - o.y) * invs.y, ty1 = (b.hi[1] - o.y) * invs.y;
+    float tz0 = (b.lo[2] - o.z) * invs.z, tz1 = (b.hi[2] - o.z) * invs.z;
+    float tmin = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmin(tz0, tz1));
+    float tmax = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmax(tz0, tz1));
+    return tmax >= std::fmax(tmin, 0.0f) && tmin * dlen <= limp;
+}
+}  // namespace
+
+extern "C" {
+
+// For each ray (o[i], d[i]): the accelerated closest hit (shape index or -1)
+// and the rays' shadow query against lim[i]. Returns -1 if the accelerator
+// cannot be built for this tree.
+int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
+                int* out_shadow, int* out_info) {
+    rta::AccelHost A;
+    if (!rta::build_accel(shapes, S, nodes, N, idx, I, 8, 64, A)) return -1;
+    out_info[0] = static_cast<int>(A.lbox.size());
+    out_info[1] = A.always_prims;
+    out_info[2] = A.bounded_prims;
+    out_info[3] = A.max_stack;
+    long long tests = 0;
+    for (int r = 0; r < R; ++r) {
+        V ro = mk(o[3 * r], o[3 * r + 1], o[3 * r + 2]), rd = mk(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
+        V inv = mk(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
+        V invs = mk(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
+        float dlen = std::sqrt(dot(rd, rd));
+        for (int pass = 0; pass < 2; ++pass) {
+            const bool shadow = pass == 1;
+            Best b{1e20f, 0x7fffffff, mk(0, 0, 0), -1};
+            bool hit_shadow = false;
+            std::vector<int> st;
+            if (N > 0) st.push_back(N - 1);
+            while (!st.empty() && !(shadow && hit_shadow)) {
+                int code = st.back();
+                st.pop_back();
+                float l = shadow ? lim[r] : b.d;
+                float limp = l * 1.002f + 1e-6f;
+                auto scan = [&](int start, int cnt) {
+                    for (int i = 0; i < cnt && !(shadow && hit_shadow); ++i) {
+                        const int si = A.prim_shape[start + i], seq = A.prim_seq[start + i];
+                        V p;
+                        ++tests;
+                        if (!isect(shapes[si], ro, rd, p)) continue;
+                        float dd = dist(ro, p);
+                        if (shadow) {
+                            if (dd < lim[r]) hit_shadow = true;
+                        } else if (dd < b.d || (dd == b.d && seq < b.seq)) {
+                            b = Best{dd, seq, p, si};
+                        }
+                    }
+                };
+                if (std::getenv("ACDBG")) std::printf("pop %d lim %g best %d %g\n", code, limp, b.shape, b.d);
+                if (code >= 0) {
+                    const FlatNode& nd = nodes[code];
+                    if (!ref_aabb(ro, inv, nd.boundsMin, nd.boundsMax)) continue;
+                    if ((A.flags[code] & 8) && !padded(ro, invs, dlen, A.content[code], limp)) continue;
+                    if (nd.leftChild == -1) {
+                        scan(A.plain_start[code], A.plain_count[code]);
+                        if (A.local_root[code] >= 0) st.push_back(-(A.local_root[code] + 1));
+                    } else {
+                        st.push_back(nd.leftChild);
+                        st.push_back(nd.rightChild);
+                    }
+                } else {
+                    const int j = -code - 1;
+                    if (!padded(ro, invs, dlen, A.lbox[j], limp)) continue;
+                    if (A.la[j] < 0) {
+                        scan(-A.la[j] - 1, A.lb[j]);
+                    } else {
+                        st.push_back(-(A.la[j] + 1));
+                        st.push_back(-((A.lb[j] & 0x3fffffff) + 1));
+                    }
+                }
+            }
+            if (shadow) out_shadow[r] = hit_shadow ? 1 : 0;
+            else { out_shape[r] = b.shape; out_d[r] = b.d; }
+        }
+    }
+    out_info[4] = static_cast<int>(tests / (R > 0 ? R : 1));
+    return 0;
+}
+}

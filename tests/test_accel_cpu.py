@@ -1,0 +1,117 @@
+"""The exact-result accelerator's rules, checked on CPU.
+
+tests/native/accel_check.cpp walks the accelerator that the product's
+accel.cpp builds (scalar emulation of k_accel's walk: reference boxes decide
+which leaves are entered, conservative local boxes + distance margin prune,
+(distance, walk rank) decides ties) and must pick exactly the shape the
+oracle's reference walk picks, for camera rays, reflection-like random rays
+and shadow queries, on the benchmark scenes and on adversarial soups.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle
+import rtamd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def check_lib(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("accel") / "accel_check.so")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-o", out,
+                    os.path.join(ROOT, "tests", "native", "accel_check.cpp"),
+                    os.path.join(ROOT, "opengl-ray-tracer_amd", "csrc", "accel.cpp")], check=True)
+    lib = C.CDLL(out)
+    lib.accel_check.restype = C.c_int
+    lib.accel_check.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int] + \
+        [C.c_void_p] * 3 + [C.c_int] + [C.c_void_p] * 4
+    o = oracle.lib()
+    o.orc_trace_rays.restype = C.c_int
+    o.orc_trace_rays.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int] + \
+        [C.c_void_p] * 3 + [C.c_int] + [C.c_void_p] * 3
+    return lib
+
+
+def _p(a):
+    return C.c_void_p(a.ctypes.data) if a.size else None
+
+
+def compare(lib, fs, o, d, lim):
+    fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)  # enforce record layout
+    R = len(o)
+    o = np.ascontiguousarray(o, np.float32)
+    d = np.ascontiguousarray(d, np.float32)
+    lim = np.ascontiguousarray(lim, np.float32)
+    outs = [np.zeros(R, np.int32), np.zeros(R, np.float32), np.zeros(R, np.int32)]
+    refs = [np.zeros(R, np.int32), np.zeros(R, np.float32), np.zeros(R, np.int32)]
+    info = np.zeros(8, np.int32)
+    args = [_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes), _p(fs.indices), len(fs.indices),
+            _p(o), _p(d), _p(lim), R]
+    assert lib.accel_check(*args, *[_p(x) for x in outs], _p(info)) == 0
+    assert oracle.lib().orc_trace_rays(*args, *[_p(x) for x in refs]) == 0
+    bad = np.where(outs[0] != refs[0])[0]
+    assert bad.size == 0, f"{bad.size} closest-hit mismatches, e.g. ray {bad[0]}: {outs[0][bad[0]]} vs {refs[0][bad[0]]}"
+    assert np.array_equal(outs[1], refs[1])
+    assert np.array_equal(outs[2], refs[2])
+    return info
+
+
+def camera_rays(fs, W, H):
+    o, d = [], []
+    for y in range(H):
+        for x in range(W):
+            ro, rd = oracle.get_ray(fs.camera, 2.0 * x / W - 1, 1.0 - 2.0 * y / H)
+            o.append(ro)
+            d.append(rd)
+    return np.array(o), np.array(d)
+
+
+def random_rays(rng, R, box=30.0):
+    o = rng.uniform(-box, box, (R, 3))
+    t = rng.uniform(-box / 2, box / 2, (R, 3))
+    d = t - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return o, d
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_accel_matches_reference_walk(check_lib, cfg):
+    W, H = 96, 54
+    fs = rtamd.generate(cfg, 0, W, H)
+    o, d = camera_rays(fs, W, H)
+    rng = np.random.default_rng(cfg)
+    o2, d2 = random_rays(rng, 4000)
+    o, d = np.concatenate([o, o2]), np.concatenate([d, d2])
+    lim = rng.uniform(1, 80, len(o))
+    info = compare(check_lib, fs, o, d, lim)
+    if cfg == 3:
+        assert info[0] > 100  # local BVHs were built for the giant leaves
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_accel_matches_on_soup(check_lib, seed):
+    import test_gpu_parity as tg  # the adversarial scene generator
+    fs = tg._soup(seed)
+    rng = np.random.default_rng(seed)
+    o, d = random_rays(rng, 6000)
+    o1, d1 = camera_rays(fs, 64, 48)
+    o, d = np.concatenate([o, o1]), np.concatenate([d, d1])
+    lim = rng.uniform(1, 80, len(o))
+    info = compare(check_lib, fs, o, d, lim)
+    assert info[1] > 0  # unbounded shapes present
+
+
+def test_accel_ties(check_lib):
+    """Duplicated shapes (equal distances): the first in walk order wins."""
+    fs = rtamd.generate(3, 0, 96, 54)
+    dup = fs.shapes.copy()
+    shapes = np.concatenate([fs.shapes, dup])
+    nodes, idx = oracle.build_bvh(shapes, 25)
+    fs2 = rtamd.FlatScene(shapes, nodes, idx, fs.camera, fs.light)
+    o, d = camera_rays(fs2, 96, 54)
+    compare(check_lib, fs2, o, d, np.full(len(o), 50.0))
