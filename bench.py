@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo: rehearse the N>1 path with every rank on one GPU")
     return ap.parse_args()
 
 
@@ -91,7 +93,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 and a.backend == "gloo":
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo")
+    elif world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
@@ -120,6 +125,7 @@ def main():
                         dtype=torch.float64, device=dev)
     total = mine.clone()
     if world > 1:
+        total = total.cpu() if a.backend == "gloo" else total
         dist.all_reduce(total)
     rays_frame = float(total[0] + total[1])
     b_alg_rank = float(mine[2])
@@ -147,7 +153,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if a.backend == "gloo" else dev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el[0])
@@ -179,6 +185,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural stand-in meshes, fixed seed; the reference's .obj assets are absent)",
+            "backend": a.backend if world > 1 else None,
             "config": {"workload": f"config {a.config}: {desc}" + (" (222-strip road)" if a.variant else ""),
                        "width": W, "height": H, "maxBounces": mb, "useBVH": 1, "useFresnel": 0,
                        "triangle_test": "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),

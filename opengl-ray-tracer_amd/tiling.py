@@ -61,6 +61,10 @@ def gather_to_root(local: torch.Tensor, plan: StripePlan, group=None) -> torch.T
     rank = dist.get_rank(group)
     if world == 1:
         return unpermute(local.unsqueeze(0), plan)
+    if local.is_cuda and dist.get_backend(group) == "gloo":
+        # rehearsal path (several ranks sharing one GPU): gloo gathers host tensors
+        out = gather_to_root(local.cpu(), plan, group)
+        return None if out is None else out.to(local.device)
     if rank == 0:
         bufs = torch.empty((world, *local.shape), dtype=local.dtype, device=local.device)
         dist.gather(local, gather_list=list(bufs.unbind(0)), dst=0, group=group)
