@@ -146,6 +146,10 @@ int rt_last_kernel_ms(struct rt_ctx* ctx, float* ms);
  * restarts the record. Waits for those dispatches to finish. */
 int rt_kernel_times(struct rt_ctx* ctx, float* ms, int cap);
 
+/* Launch shape of the accelerated kernel: 1, 2 or 4 waves (8x8 tiles) per
+ * workgroup; persistent != 0 = a resident grid pulling tiles from a counter. */
+int rt_set_launch(struct rt_ctx* ctx, int waves_per_block, int persistent);
+
 /* Accelerator statistics for the uploaded scene. */
 int rt_accel_info_get(struct rt_ctx* ctx, rt_accel_info* out);
 

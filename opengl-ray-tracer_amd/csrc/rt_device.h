@@ -84,6 +84,9 @@ struct KParams {
     char* __restrict__ dst;
     size_t pitch;
     unsigned long long* __restrict__ stats;  // rt_stats layout, STATS kernels only
+    int* __restrict__ tile_counter;          // persistent launches: next 8x8 tile (zeroed per launch)
+    unsigned long long* __restrict__ tile_times;  // optional: start/end wall clock per tile
+    int tiles_x, tiles;                      // 8x8 tiles per row, total
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).

@@ -751,13 +751,20 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
     }
 }
 
-// Same stack encoding for local nodes: code = -(j+1).
-__global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ anodes,
-                                                  const float4* __restrict__ lnodes,
-                                                  const float4* __restrict__ prims,
-                                                  const float4* __restrict__ mat, KParams kp) {
-    const AccelPtrs A{anodes, lnodes, prims, kp.N};
-    const PixelCoord pc = pixel_of(kp);
+// One 8x8 tile per wave (lane l: pixel (l&7, l>>3) of the tile).
+__device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
+    const int lane = threadIdx.x & 63;
+    PixelCoord pc;
+    pc.x = (tile % kp.tiles_x) * 8 + (lane & 7);
+    pc.r = (tile / kp.tiles_x) * 8 + (lane >> 3);
+    pc.active = pc.x < kp.width && pc.r < kp.out_rows;
+    pc.y = pc.active ? image_row(kp, pc.r) : 0;
+    pc.active = pc.active && pc.y < kp.height;
+    return pc;
+}
+
+__device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile) {
+    const PixelCoord pc = tile_pixel(kp, tile);
     const V bg = background(kp, pc.y);
     Ray ray = primary_ray(kp, pc.x, pc.y);
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
@@ -776,7 +783,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
         Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
         float ld = 0.f;
         if (alive) {
-            const GeoRec g = load_rec(prims, best.slot);
+            const GeoRec g = load_rec(A.prims, best.slot);
             hn = shape_normal(g, best.p);
             m = load_mat(mat, g.idx);
             sr = Ray{best.p + hn * 1e-3f, normalize(kp.light_pos - best.p)};
@@ -788,6 +795,37 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
     }
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+}
+
+// PERSISTENT: each wave pulls tiles from one device counter until none is
+// left (every wave reaches the exit); otherwise one tile per wave. TIMED
+// writes each tile's start/end wall clock (diagnostics only).
+template <bool PERSISTENT, bool TIMED>
+__global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ anodes,
+                                                  const float4* __restrict__ lnodes,
+                                                  const float4* __restrict__ prims,
+                                                  const float4* __restrict__ mat, KParams kp) {
+    const AccelPtrs A{anodes, lnodes, prims, kp.N};
+    const int lane = threadIdx.x & 63;
+    int tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (PERSISTENT) {
+        int t = 0;
+        if (lane == 0) t = atomicAdd(kp.tile_counter, 1);
+        tile = __shfl(t, 0);
+    }
+    while (tile < kp.tiles) {
+        unsigned long long t0 = 0;
+        if (TIMED) t0 = wall_clock64();
+        accel_tile(A, mat, kp, tile);
+        if (TIMED && lane == 0) {
+            kp.tile_times[2 * tile] = t0;
+            kp.tile_times[2 * tile + 1] = wall_clock64();
+        }
+        if (!PERSISTENT) break;
+        int t = 0;
+        if (lane == 0) t = atomicAdd(kp.tile_counter, 1);
+        tile = __shfl(t, 0);
+    }
 }
 
 __global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __restrict__ prim_shape,
@@ -846,6 +884,11 @@ struct rt_ctx {
     size_t img_pitch = 0;
     int img_w = 0, img_h = 0;
     unsigned long long* stats_dev = nullptr;
+    // launch shape of k_accel (rt_set_launch)
+    int waves_per_block = 4, persistent = 0, cu_count = 256;
+    int* tile_counter = nullptr;
+    unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
+    size_t tile_times_cap = 0;
 };
 
 namespace {
@@ -1057,7 +1100,21 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         hipLaunchKernelGGL(k_lane<false>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
                            c->nodes, kp);
     } else if (kind == RT_KERNEL_ACCEL) {
-        hipLaunchKernelGGL(k_accel, grid, dim3(kBlock), 0, c->stream, c->anodes, c->lnodes, c->prims, c->mat, kp);
+        KParams k2 = kp;
+        k2.tiles_x = (kp.width + 7) / 8;
+        k2.tiles = k2.tiles_x * ((kp.out_rows + 7) / 8);
+        k2.tile_counter = c->tile_counter;
+        k2.tile_times = c->tile_times;
+        const int wpb = c->waves_per_block;
+        int blocks = (k2.tiles + wpb - 1) / wpb;
+        if (c->persistent) {
+            HIP_TRY(hipMemsetAsync(c->tile_counter, 0, 16, c->stream));
+            blocks = std::min(blocks, c->cu_count * 20 / wpb);  // resident at 5 waves/SIMD
+        }
+        auto kfn = c->persistent ? (c->tile_times ? k_accel<true, true> : k_accel<true, false>)
+                                 : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
+        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), 0, c->stream, c->anodes, c->lnodes, c->prims, c->mat,
+                           k2);
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
                            kp);
@@ -1101,11 +1158,18 @@ int rt_create(rt_ctx** out, int device) {
     c->device = device;
     if (set_dev(c) != RT_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipMalloc(&c->stats_dev, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->stats_dev, ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->tile_counter, 16) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_DEVICE;
     }
     c->own_stream = true;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, device) == hipSuccess)
+            c->cu_count = prop.multiProcessorCount;
+        if (c->cu_count <= 0) c->cu_count = 256;
+    }
     c->ring0.resize(kRing, nullptr);
     c->ring1.resize(kRing, nullptr);
     for (int i = 0; i < kRing; ++i)
@@ -1127,6 +1191,8 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->staging_idx);
     hipFree(c->img);
     hipFree(c->stats_dev);
+    hipFree(c->tile_counter);
+    hipFree(c->tile_times);
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1380,5 +1446,35 @@ extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
     out->always_prims = c->accel.always_prims;
     out->max_stack = c->accel.max_stack;
     out->last_kernel = c->last_kind;
+    return RT_OK;
+}
+
+extern "C" int rt_set_launch(rt_ctx* c, int waves_per_block, int persistent) {
+    if (!c || (waves_per_block != 1 && waves_per_block != 2 && waves_per_block != 4)) return RT_ERR_INVALID;
+    c->waves_per_block = waves_per_block;
+    c->persistent = persistent ? 1 : 0;
+    return RT_OK;
+}
+
+// Diagnostics (not part of rt_api.h): enable per-tile wall-clock stamps for
+// k_accel (cap tiles; 0 disables) and read them back (2 x u64 per tile,
+// 100 MHz s_memrealtime ticks). Synchronous.
+extern "C" int rt_debug_tile_times(rt_ctx* c, int cap, unsigned long long* out) {
+    if (!c || cap < 0) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (out && c->tile_times && cap > 0) {
+        const size_t n = std::min(static_cast<size_t>(cap), c->tile_times_cap);
+        HIP_TRY(hipMemcpy(out, c->tile_times, n * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        return static_cast<int>(n);
+    }
+    hipFree(c->tile_times);
+    c->tile_times = nullptr;
+    c->tile_times_cap = 0;
+    if (cap > 0) {
+        if (hipMalloc(&c->tile_times, static_cast<size_t>(cap) * 2 * sizeof(unsigned long long)) != hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        c->tile_times_cap = cap;
+    }
     return RT_OK;
 }

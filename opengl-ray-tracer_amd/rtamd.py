@@ -184,6 +184,7 @@ RT_SYMBOLS = {
     "rt_last_kernel_ms": (_I, [_P, _P]),
     "rt_kernel_times": (_I, [_P, _P, _I]),
     "rt_accel_info_get": (_I, [_P, _P]),
+    "rt_set_launch": (_I, [_P, _I, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
 
@@ -426,6 +427,24 @@ class ComputeShader:
         if n < 0:
             raise RTError("rt_kernel_times", n)
         return buf[:min(n, cap)].copy()
+
+    def set_launch(self, waves_per_block=4, persistent=False):
+        self._chk(self._lib.rt_set_launch(self._h, int(waves_per_block), int(bool(persistent))), "rt_set_launch")
+
+    def debug_tile_times(self, cap):
+        """cap > 0: enable per-tile stamps (diagnostics); then tile_times(cap) reads them."""
+        fn = self._lib.rt_debug_tile_times
+        fn.argtypes = [_P, _I, _P]
+        self._chk(fn(self._h, int(cap), None), "rt_debug_tile_times")
+
+    def tile_times(self, cap):
+        buf = np.zeros((cap, 2), np.uint64)
+        fn = self._lib.rt_debug_tile_times
+        fn.argtypes = [_P, _I, _P]
+        n = fn(self._h, int(cap), _ptr(buf))
+        if n < 0:
+            raise RTError("rt_debug_tile_times", n)
+        return buf[:n]
 
     def accel_info(self):
         a = rt_accel_info()

@@ -1,0 +1,82 @@
+"""A/B timing of render-kernel variants in one process (interleaved rounds).
+
+    python tools/ab.py [--config 3] [--rounds 5] [--frames 20] [--times]
+
+Prints median device ms per variant (HIP events) and checks that every
+variant renders the identical image.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
+import rtamd  # noqa: E402
+
+WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 1920, 1080, 3)}
+VARIANTS = {
+    "accel_wpb4": dict(kernel=3, wpb=4, persistent=False),
+    "accel_wpb1": dict(kernel=3, wpb=1, persistent=False),
+    "accel_pers4": dict(kernel=3, wpb=4, persistent=True),
+    "accel_pers1": dict(kernel=3, wpb=1, persistent=True),
+    "packet": dict(kernel=2, wpb=4, persistent=False),
+}
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--config", type=int, default=3)
+ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--frames", type=int, default=20)
+ap.add_argument("--variants", default="accel_wpb4,accel_wpb1,accel_pers4,accel_pers1")
+ap.add_argument("--times", action="store_true", help="per-tile wall-clock distribution")
+a = ap.parse_args()
+cfg, W, H, mb = WL[a.config]
+fs = rtamd.generate(cfg, 0, W, H)
+ctx = rtamd.ComputeShader(0)
+ctx.upload(fs)
+ctx.set_params(W, H, mb, True)
+out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+torch.cuda.synchronize()
+names = a.variants.split(",")
+res = {n: [] for n in names}
+ref = None
+for rnd in range(a.rounds):
+    for n in names:
+        v = VARIANTS[n]
+        ctx.set_kernel(v["kernel"])
+        ctx.set_launch(v["wpb"], v["persistent"])
+        ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+        ctx.sync()
+        img = out.cpu().numpy()
+        if ref is None:
+            ref = img
+        assert np.array_equal(img, ref), f"{n} renders a different image"
+        ctx.kernel_times()
+        for _ in range(a.frames):
+            ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+        res[n].extend(ctx.kernel_times().tolist())
+summary = {n: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))} for n, t in res.items()}
+print(json.dumps({"config": a.config, "variants": summary}))
+if a.times:
+    tiles = ((W + 7) // 8) * ((H + 7) // 8)
+    for n in names:
+        v = VARIANTS[n]
+        ctx.set_kernel(v["kernel"])
+        ctx.set_launch(v["wpb"], v["persistent"])
+        ctx.debug_tile_times(tiles)
+        ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+        t = ctx.tile_times(tiles).astype(np.int64)
+        ctx.debug_tile_times(0)
+        dur = (t[:, 1] - t[:, 0]) / 100.0  # us (100 MHz)
+        start = (t[:, 0] - t[:, 0].min()) / 100.0
+        end = (t[:, 1] - t[:, 0].min()) / 100.0
+        q = np.percentile(dur, [50, 90, 99, 100])
+        print(json.dumps({"variant": n, "tile_us_p50_p90_p99_max": q.round(1).tolist(), "tile_us_mean": float(dur.mean()),
+                          "span_us": float(end.max()), "last_start_us": float(start.max()),
+                          "sum_tile_us": float(dur.sum())}))
+        rows = (H + 7) // 8
+        per_row = dur.reshape(rows, -1).mean(axis=1)
+        print("  mean tile us by tile-row (every 10th):", per_row[::10].round(1).tolist())
