@@ -87,6 +87,8 @@ struct KParams {
     int* __restrict__ tile_counter;          // persistent launches: next 8x8 tile (zeroed per launch)
     unsigned long long* __restrict__ tile_times;  // optional: start/end wall clock per tile
     int tiles_x, tiles;                      // 8x8 tiles per row, total
+    int lane_from_depth;                     // k_accel: bounces >= this walk per lane
+    int lane_stack;                          // per-lane LDS stack entries
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).

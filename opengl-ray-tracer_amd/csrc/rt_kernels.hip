@@ -751,6 +751,79 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
     }
 }
 
+// Per-lane variant of accel_walk: every lane walks its own stack (in LDS,
+// entry s of a lane at stk[s * stride]) with per-lane node loads. For
+// incoherent rays (reflections off curved surfaces) the packet walk visits
+// the union of all lanes' nodes; here a wave costs its longest lane. Same
+// visited-set / pruning / tie rules as accel_walk, so the same result.
+template <bool SHADOW>
+__device__ void lane_accel_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
+                                bool& shadow, int* stk, int stride, int cap) {
+    if (A.N <= 0 || !active) return;
+    const V inv = inv_dir(r.d);
+    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
+    const float dlen = len(r.d);
+    int sp = 0;
+    stk[0] = A.N - 1;
+    sp = 1;
+    while (sp > 0) {
+        const int code = stk[--sp * stride];
+        const float lim = SHADOW ? lim_shadow : b.d;
+        const float limp = lim * kPruneRel + 1e-6f;
+        int start = 0, count = 0;
+        if (code >= 0) {
+            const float4* q = A.anodes + 4 * static_cast<size_t>(code);
+            const float4 e0 = q[0], e1 = q[1];
+            if (!ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z))) continue;
+            const float4 c0 = q[2], c1 = q[3];
+            const int flags = __float_as_int(c0.w);
+            if ((flags & 8) && !padded_hit(r.o, invs, dlen, c0, c1, limp)) continue;
+            const int ia = __float_as_int(e0.w), ib = __float_as_int(e1.w);
+            if (ia < 0) {
+                start = -ia - 1;
+                count = ib;
+                const int lroot = __float_as_int(c1.w);
+                if (lroot >= 0 && sp < cap) stk[sp++ * stride] = -(lroot + 1);
+            } else {
+                const int axis = flags & 3;
+                const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
+                const bool fwd = axis_of(r.d, axis) >= 0.0f;
+                if (sp + 2 > cap) continue;  // unreachable: the host bounds the stack
+                stk[sp++ * stride] = fwd ? upper : lower;
+                stk[sp++ * stride] = fwd ? lower : upper;
+                continue;
+            }
+        } else {
+            const float4* q = A.lnodes + 2 * static_cast<size_t>(-code - 1);
+            const float4 lo = q[0], hi = q[1];
+            if (!padded_hit(r.o, invs, dlen, lo, hi, limp)) continue;
+            const int la = __float_as_int(lo.w), lb = __float_as_int(hi.w);
+            if (la < 0) {
+                start = -la - 1;
+                count = lb;
+            } else {
+                const int axis = (lb >> 30) & 3, right = lb & 0x3fffffff;
+                const bool fwd = axis_of(r.d, axis) >= 0.0f;
+                if (sp + 2 > cap) continue;
+                stk[sp++ * stride] = -((fwd ? right : la) + 1);
+                stk[sp++ * stride] = -((fwd ? la : right) + 1);
+                continue;
+            }
+        }
+        for (int i = 0; i < count; ++i) {
+            const GeoRec g = load_rec(A.prims, start + i);
+            if (SHADOW) {
+                if (try_shadow(g, r, lim_shadow)) {
+                    shadow = true;
+                    return;
+                }
+            } else {
+                try_closest(g, start + i, r, b);
+            }
+        }
+    }
+}
+
 // One 8x8 tile per wave (lane l: pixel (l&7, l>>3) of the tile).
 __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     const int lane = threadIdx.x & 63;
@@ -763,7 +836,8 @@ __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     return pc;
 }
 
-__device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile) {
+__device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
+                           int* stk, int cap) {
     const PixelCoord pc = tile_pixel(kp, tile);
     const V bg = background(kp, pc.y);
     Ray ray = primary_ray(kp, pc.x, pc.y);
@@ -773,7 +847,11 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         if (__ballot(alive) == 0) break;
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
         bool unused = false;
-        accel_walk<false>(A, ray, alive, 0.f, best, unused);
+        const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
+        if (lane_mode)
+            lane_accel_walk<false>(A, ray, alive, 0.f, best, unused, stk, blockDim.x, cap);
+        else
+            accel_walk<false>(A, ray, alive, 0.f, best, unused);
         if (alive && best.slot < 0) {
             acc = acc + mulv(att, bg);
             alive = false;
@@ -791,7 +869,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         }
         bool shadow = false;
         Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
-        accel_walk<true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow);
+        if (lane_mode)
+            lane_accel_walk<true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, blockDim.x, cap);
+        else
+            accel_walk<true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow);
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
     }
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
@@ -806,6 +887,8 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
                                                   const float4* __restrict__ prims,
                                                   const float4* __restrict__ mat, KParams kp) {
     const AccelPtrs A{anodes, lnodes, prims, kp.N};
+    extern __shared__ int lds_stack[];
+    int* stk = lds_stack + threadIdx.x;
     const int lane = threadIdx.x & 63;
     int tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (PERSISTENT) {
@@ -816,7 +899,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
     while (tile < kp.tiles) {
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
-        accel_tile(A, mat, kp, tile);
+        accel_tile(A, mat, kp, tile, stk, kp.lane_stack);
         if (TIMED && lane == 0) {
             kp.tile_times[2 * tile] = t0;
             kp.tile_times[2 * tile + 1] = wall_clock64();
@@ -886,6 +969,7 @@ struct rt_ctx {
     unsigned long long* stats_dev = nullptr;
     // launch shape of k_accel (rt_set_launch)
     int waves_per_block = 4, persistent = 0, cu_count = 256;
+    int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
@@ -1113,7 +1197,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         }
         auto kfn = c->persistent ? (c->tile_times ? k_accel<true, true> : k_accel<true, false>)
                                  : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
-        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), 0, c->stream, c->anodes, c->lnodes, c->prims, c->mat,
+        k2.lane_from_depth = c->lane_from_depth;
+        k2.lane_stack = c->accel.max_stack;
+        const size_t lds = k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 4 : 0;
+        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, c->anodes, c->lnodes, c->prims, c->mat,
                            k2);
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
@@ -1446,6 +1533,12 @@ extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
     out->always_prims = c->accel.always_prims;
     out->max_stack = c->accel.max_stack;
     out->last_kernel = c->last_kind;
+    return RT_OK;
+}
+
+extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
+    if (!c || lane_from_depth < 0) return RT_ERR_INVALID;
+    c->lane_from_depth = lane_from_depth;
     return RT_OK;
 }
 

@@ -185,6 +185,7 @@ RT_SYMBOLS = {
     "rt_kernel_times": (_I, [_P, _P, _I]),
     "rt_accel_info_get": (_I, [_P, _P]),
     "rt_set_launch": (_I, [_P, _I, _I]),
+    "rt_set_walk": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
 
@@ -430,6 +431,9 @@ class ComputeShader:
 
     def set_launch(self, waves_per_block=4, persistent=False):
         self._chk(self._lib.rt_set_launch(self._h, int(waves_per_block), int(bool(persistent))), "rt_set_launch")
+
+    def set_walk(self, lane_from_depth):
+        self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
 
     def debug_tile_times(self, cap):
         """cap > 0: enable per-tile stamps (diagnostics); then tile_times(cap) reads them."""

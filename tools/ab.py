@@ -19,21 +19,27 @@ import rtamd  # noqa: E402
 
 WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 1920, 1080, 3)}
 VARIANTS = {
-    "accel_wpb4": dict(kernel=3, wpb=4, persistent=False),
-    "accel_wpb1": dict(kernel=3, wpb=1, persistent=False),
-    "accel_pers4": dict(kernel=3, wpb=4, persistent=True),
-    "accel_pers1": dict(kernel=3, wpb=1, persistent=True),
-    "packet": dict(kernel=2, wpb=4, persistent=False),
+    "accel_wpb4": dict(kernel=3, wpb=4, persistent=False, walk=1),
+    "accel_wpb1": dict(kernel=3, wpb=1, persistent=False, walk=1),
+    "accel_pers4": dict(kernel=3, wpb=4, persistent=True, walk=1),
+    "accel_pers1": dict(kernel=3, wpb=1, persistent=True, walk=1),
+    "accel_packetwalk": dict(kernel=3, wpb=4, persistent=False, walk=99),
+    "accel_lanewalk": dict(kernel=3, wpb=4, persistent=False, walk=0),
+    "accel_lanewalk_w1": dict(kernel=3, wpb=1, persistent=False, walk=0),
+    "accel_walk2": dict(kernel=3, wpb=4, persistent=False, walk=2),
+    "packet": dict(kernel=2, wpb=4, persistent=False, walk=1),
 }
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--frames", type=int, default=20)
-ap.add_argument("--variants", default="accel_wpb4,accel_wpb1,accel_pers4,accel_pers1")
+ap.add_argument("--variants", default="accel_packetwalk,accel_wpb4,accel_lanewalk,accel_lanewalk_w1,accel_walk2,accel_pers4")
+ap.add_argument("--bounces", type=int, default=0, help="override maxBounces")
 ap.add_argument("--times", action="store_true", help="per-tile wall-clock distribution")
 a = ap.parse_args()
 cfg, W, H, mb = WL[a.config]
+mb = a.bounces or mb
 fs = rtamd.generate(cfg, 0, W, H)
 ctx = rtamd.ComputeShader(0)
 ctx.upload(fs)
@@ -48,6 +54,7 @@ for rnd in range(a.rounds):
         v = VARIANTS[n]
         ctx.set_kernel(v["kernel"])
         ctx.set_launch(v["wpb"], v["persistent"])
+        ctx.set_walk(v["walk"])
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         ctx.sync()
         img = out.cpu().numpy()
@@ -59,13 +66,14 @@ for rnd in range(a.rounds):
             ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         res[n].extend(ctx.kernel_times().tolist())
 summary = {n: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t))} for n, t in res.items()}
-print(json.dumps({"config": a.config, "variants": summary}))
+print(json.dumps({"config": a.config, "maxBounces": mb, "variants": summary}))
 if a.times:
     tiles = ((W + 7) // 8) * ((H + 7) // 8)
     for n in names:
         v = VARIANTS[n]
         ctx.set_kernel(v["kernel"])
         ctx.set_launch(v["wpb"], v["persistent"])
+        ctx.set_walk(v["walk"])
         ctx.debug_tile_times(tiles)
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         t = ctx.tile_times(tiles).astype(np.int64)
@@ -80,3 +88,6 @@ if a.times:
         rows = (H + 7) // 8
         per_row = dur.reshape(rows, -1).mean(axis=1)
         print("  mean tile us by tile-row (every 10th):", per_row[::10].round(1).tolist())
+        tx = (W + 7) // 8
+        worst = np.argsort(dur)[::-1][:6]
+        print("  slowest tiles (x8, y8, us):", [(int(w % tx) * 8, int(w // tx) * 8, round(float(dur[w]), 1)) for w in worst])
