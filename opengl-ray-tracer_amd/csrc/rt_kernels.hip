@@ -650,9 +650,14 @@ __device__ __forceinline__ float rep_dir(V d, int axis, unsigned long long m) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(axis_of(d, axis)), lane));
 }
 
-template <bool SHADOW>
+// Diagnostics (TIMED k_accel only): per-lane node pops and primitive tests.
+struct WalkCount {
+    unsigned nodes, tests;
+};
+
+template <bool SHADOW, bool COUNT = false>
 __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
-                           bool& shadow) {
+                           bool& shadow, WalkCount& wc) {
     const unsigned long long m0 = __ballot(active);
     if (A.N <= 0 || m0 == 0) return;
     const V inv = inv_dir(r.d);  // exact reciprocal: the reference box test
@@ -668,6 +673,7 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
         if (SHADOW) m &= ~done;
         if (m == 0) continue;
         code = uni(code);
+        if (COUNT && lane_in(m)) wc.nodes++;
         const float lim = SHADOW ? lim_shadow : b.d;
         const float limp = lim * kPruneRel + 1e-6f;
         if (code >= 0) {
@@ -687,6 +693,7 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
                 for (int i = 0; i < ib; ++i) {
                     const GeoRec g = load_rec(A.prims, start + i);
                     if (live) {
+                        if (COUNT) wc.tests++;
                         if (SHADOW) {
                             if (try_shadow(g, r, lim_shadow)) {
                                 shadow = true;
@@ -726,6 +733,7 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
                 for (int i = 0; i < lb; ++i) {
                     const GeoRec g = load_rec(A.prims, start + i);
                     if (live) {
+                        if (COUNT) wc.tests++;
                         if (SHADOW) {
                             if (try_shadow(g, r, lim_shadow)) {
                                 shadow = true;
@@ -756,9 +764,9 @@ __device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float 
 // incoherent rays (reflections off curved surfaces) the packet walk visits
 // the union of all lanes' nodes; here a wave costs its longest lane. Same
 // visited-set / pruning / tie rules as accel_walk, so the same result.
-template <bool SHADOW>
+template <bool SHADOW, bool COUNT = false>
 __device__ void lane_accel_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
-                                bool& shadow, int* stk, int stride, int cap) {
+                                bool& shadow, int* stk, int stride, int cap, WalkCount& wc) {
     if (A.N <= 0 || !active) return;
     const V inv = inv_dir(r.d);
     const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
@@ -768,6 +776,7 @@ __device__ void lane_accel_walk(const AccelPtrs& A, const Ray& r, bool active, f
     sp = 1;
     while (sp > 0) {
         const int code = stk[--sp * stride];
+        if (COUNT) wc.nodes++;
         const float lim = SHADOW ? lim_shadow : b.d;
         const float limp = lim * kPruneRel + 1e-6f;
         int start = 0, count = 0;
@@ -812,6 +821,7 @@ __device__ void lane_accel_walk(const AccelPtrs& A, const Ray& r, bool active, f
         }
         for (int i = 0; i < count; ++i) {
             const GeoRec g = load_rec(A.prims, start + i);
+            if (COUNT) wc.tests++;
             if (SHADOW) {
                 if (try_shadow(g, r, lim_shadow)) {
                     shadow = true;
@@ -836,8 +846,9 @@ __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     return pc;
 }
 
+template <bool COUNT>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
-                           int* stk, int cap) {
+                           int* stk, int cap, WalkCount& wc) {
     const PixelCoord pc = tile_pixel(kp, tile);
     const V bg = background(kp, pc.y);
     Ray ray = primary_ray(kp, pc.x, pc.y);
@@ -849,9 +860,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         bool unused = false;
         const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
         if (lane_mode)
-            lane_accel_walk<false>(A, ray, alive, 0.f, best, unused, stk, blockDim.x, cap);
+            lane_accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, blockDim.x, cap, wc);
         else
-            accel_walk<false>(A, ray, alive, 0.f, best, unused);
+            accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
         if (alive && best.slot < 0) {
             acc = acc + mulv(att, bg);
             alive = false;
@@ -870,9 +881,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         bool shadow = false;
         Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
         if (lane_mode)
-            lane_accel_walk<true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, blockDim.x, cap);
+            lane_accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, blockDim.x, cap, wc);
         else
-            accel_walk<true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow);
+            accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
     }
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
@@ -899,10 +910,26 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
     while (tile < kp.tiles) {
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
-        accel_tile(A, mat, kp, tile, stk, kp.lane_stack);
-        if (TIMED && lane == 0) {
-            kp.tile_times[2 * tile] = t0;
-            kp.tile_times[2 * tile + 1] = wall_clock64();
+        WalkCount wc{0u, 0u};
+        accel_tile<TIMED>(A, mat, kp, tile, stk, kp.lane_stack, wc);
+        if (TIMED) {
+            const unsigned long long t1 = wall_clock64();
+            unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
+            for (int off = 32; off > 0; off >>= 1) {
+                sn += __shfl_xor(sn, off);
+                st += __shfl_xor(st, off);
+                mn = max(mn, __shfl_xor(mn, off));
+                mt = max(mt, __shfl_xor(mt, off));
+            }
+            if (lane == 0) {
+                unsigned long long* o = kp.tile_times + 6 * static_cast<size_t>(tile);
+                o[0] = t0;
+                o[1] = t1;
+                o[2] = sn;
+                o[3] = st;
+                o[4] = mn;
+                o[5] = mt;
+            }
         }
         if (!PERSISTENT) break;
         int t = 0;
@@ -1550,22 +1577,23 @@ extern "C" int rt_set_launch(rt_ctx* c, int waves_per_block, int persistent) {
 }
 
 // Diagnostics (not part of rt_api.h): enable per-tile wall-clock stamps for
-// k_accel (cap tiles; 0 disables) and read them back (2 x u64 per tile,
-// 100 MHz s_memrealtime ticks). Synchronous.
+// k_accel (cap tiles; 0 disables) and read them back (6 x u64 per tile:
+// start, end in 100 MHz s_memrealtime ticks; node pops and primitive tests
+// summed over the wave's lanes, then their per-lane maxima). Synchronous.
 extern "C" int rt_debug_tile_times(rt_ctx* c, int cap, unsigned long long* out) {
     if (!c || cap < 0) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (out && c->tile_times && cap > 0) {
         const size_t n = std::min(static_cast<size_t>(cap), c->tile_times_cap);
-        HIP_TRY(hipMemcpy(out, c->tile_times, n * 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(out, c->tile_times, n * 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         return static_cast<int>(n);
     }
     hipFree(c->tile_times);
     c->tile_times = nullptr;
     c->tile_times_cap = 0;
     if (cap > 0) {
-        if (hipMalloc(&c->tile_times, static_cast<size_t>(cap) * 2 * sizeof(unsigned long long)) != hipSuccess)
+        if (hipMalloc(&c->tile_times, static_cast<size_t>(cap) * 6 * sizeof(unsigned long long)) != hipSuccess)
             return RT_ERR_NO_MEMORY;
         c->tile_times_cap = cap;
     }

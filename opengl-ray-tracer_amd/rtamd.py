@@ -442,7 +442,7 @@ class ComputeShader:
         self._chk(fn(self._h, int(cap), None), "rt_debug_tile_times")
 
     def tile_times(self, cap):
-        buf = np.zeros((cap, 2), np.uint64)
+        buf = np.zeros((cap, 6), np.uint64)
         fn = self._lib.rt_debug_tile_times
         fn.argtypes = [_P, _I, _P]
         n = fn(self._h, int(cap), _ptr(buf))

@@ -90,4 +90,9 @@ if a.times:
         print("  mean tile us by tile-row (every 10th):", per_row[::10].round(1).tolist())
         tx = (W + 7) // 8
         worst = np.argsort(dur)[::-1][:6]
-        print("  slowest tiles (x8, y8, us):", [(int(w % tx) * 8, int(w // tx) * 8, round(float(dur[w]), 1)) for w in worst])
+        print("  slowest tiles (x8, y8, us, nodes sum/max-lane, tests sum/max-lane):",
+              [(int(w % tx) * 8, int(w // tx) * 8, round(float(dur[w]), 1), int(t[w, 2]), int(t[w, 4]), int(t[w, 3]),
+                int(t[w, 5])) for w in worst])
+        med = np.argsort(dur)[len(dur) // 2]
+        print("  median tile:", (round(float(dur[med]), 1), int(t[med, 2]), int(t[med, 4]), int(t[med, 3]), int(t[med, 5])))
+        print("  totals: nodes", int(t[:, 2].sum()), "tests", int(t[:, 3].sum()))
