@@ -89,6 +89,7 @@ struct KParams {
     int tiles_x, tiles;                      // 8x8 tiles per row, total
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane
     int lane_stack;                          // per-lane LDS stack entries
+    int lane_walk;                           // 1: node-at-pop walk, 2: while-while (lnodes2)
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).

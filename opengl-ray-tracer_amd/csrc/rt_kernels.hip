@@ -523,7 +523,13 @@ struct AccelPtrs {
     const float4* __restrict__ lnodes;  // 2 float4 per local node
     const float4* __restrict__ prims;   // 5 float4 per prim, f[17] = rank
     int N;
+    const float4* __restrict__ lnodes2; // 4 float4 per local inner node: both child boxes + codes
+    const int* __restrict__ lroot2;     // per reference node: local root as a child code, or kNoChild
 };
+
+// Child codes of the per-lane walk's stack and of lnodes2 entries.
+constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u;
+constexpr int kNoChild = 0x7fffffff;
 
 struct Best {
     float d;
@@ -637,6 +643,17 @@ __device__ __forceinline__ bool padded_hit(V o, V invs, float dlen, float4 lo, f
     float tz0 = (lo.z - o.z) * invs.z, tz1 = (hi.z - o.z) * invs.z;
     float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
     float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    return tmax >= fmaxf(tmin, 0.0f) && tmin * dlen <= limp;
+}
+
+__device__ __forceinline__ bool padded_hit_t(V o, V invs, float dlen, float4 lo, float4 hi, float limp,
+                                             float& tentry) {
+    float tx0 = (lo.x - o.x) * invs.x, tx1 = (hi.x - o.x) * invs.x;
+    float ty0 = (lo.y - o.y) * invs.y, ty1 = (hi.y - o.y) * invs.y;
+    float tz0 = (lo.z - o.z) * invs.z, tz1 = (hi.z - o.z) * invs.z;
+    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
+    float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
+    tentry = tmin;
     return tmax >= fmaxf(tmin, 0.0f) && tmin * dlen <= limp;
 }
 
@@ -834,6 +851,101 @@ __device__ void lane_accel_walk(const AccelPtrs& A, const Ray& r, bool active, f
     }
 }
 
+// Per-lane walk, second form ("while-while"): local BVH nodes hold both
+// child boxes, so a culled child costs no iteration, and far children carry
+// their entry distance on the stack (re-checked against the best hit when
+// popped). Each lane first walks until it holds a leaf, then all lanes test
+// their leaves together, so a lane's leaf scan no longer stalls the others'
+// node steps. Stack: code + entry distance per entry, in LDS.
+template <bool SHADOW, bool COUNT = false>
+__device__ void lane_walk2(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
+                           int* stk, float* stt, int stride, int cap, WalkCount& wc) {
+    if (A.N <= 0 || !active) return;
+    const V inv = inv_dir(r.d);
+    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
+    const float dlen = len(r.d);
+    int sp = 1;
+    stk[0] = A.N - 1;
+    stt[0] = -INFINITY;
+    for (;;) {
+        int start = 0, count = 0;
+        while (sp > 0 && count == 0) {
+            --sp;
+            const int code = stk[sp * stride];
+            const float te = stt[sp * stride];
+            if (COUNT) wc.nodes++;
+            const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+            if (te * dlen > limp) continue;  // a nearer hit was found since the push
+            const unsigned uc = static_cast<unsigned>(code);
+            if (!(uc & kLocal)) {
+                // reference node: the exact box test decides entry (gpu_shader.comp:395)
+                const float4* q = A.anodes + 4 * static_cast<size_t>(code);
+                const float4 e0 = q[0], e1 = q[1];
+                if (!ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z))) continue;
+                const float4 c0 = q[2], c1 = q[3];
+                const int flags = __float_as_int(c0.w);
+                if ((flags & 8) && !padded_hit(r.o, invs, dlen, c0, c1, limp)) continue;
+                const int ia = __float_as_int(e0.w), ib = __float_as_int(e1.w);
+                if (ia < 0) {
+                    start = -ia - 1;
+                    count = ib;
+                    const int lr = A.lroot2[code];
+                    if (lr != kNoChild && sp < cap) {
+                        stk[sp * stride] = lr;
+                        stt[sp * stride] = -INFINITY;
+                        ++sp;
+                    }
+                } else if (sp + 2 <= cap) {
+                    const int axis = flags & 3;
+                    const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
+                    const bool fwd = axis_of(r.d, axis) >= 0.0f;
+                    stk[sp * stride] = fwd ? upper : lower;
+                    stt[sp * stride] = -INFINITY;
+                    stk[(sp + 1) * stride] = fwd ? lower : upper;
+                    stt[(sp + 1) * stride] = -INFINITY;
+                    sp += 2;
+                }
+            } else if (uc & kLeaf) {
+                start = static_cast<int>((uc >> 8) & 0x3fffffu);
+                count = static_cast<int>(uc & 0xffu);
+            } else {
+                const float4* q = A.lnodes2 + 4 * static_cast<size_t>(uc & 0x3fffffffu);
+                const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3];
+                float ta, tb;
+                const bool ha = padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta);
+                const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb);
+                const int ca = __float_as_int(a0.w), cb = __float_as_int(a1.w);
+                // near child popped first: order by entry distance
+                const bool a_first = !(tb < ta);
+                if (ha && hb && sp + 2 <= cap) {
+                    stk[sp * stride] = a_first ? cb : ca;
+                    stt[sp * stride] = a_first ? tb : ta;
+                    stk[(sp + 1) * stride] = a_first ? ca : cb;
+                    stt[(sp + 1) * stride] = a_first ? ta : tb;
+                    sp += 2;
+                } else if ((ha || hb) && sp < cap) {
+                    stk[sp * stride] = ha ? ca : cb;
+                    stt[sp * stride] = ha ? ta : tb;
+                    ++sp;
+                }
+            }
+        }
+        if (count == 0) return;  // stack empty
+        for (int i = 0; i < count; ++i) {
+            const GeoRec g = load_rec(A.prims, start + i);
+            if (COUNT) wc.tests++;
+            if (SHADOW) {
+                if (try_shadow(g, r, lim_shadow)) {
+                    shadow = true;
+                    return;
+                }
+            } else {
+                try_closest(g, start + i, r, b);
+            }
+        }
+    }
+}
+
 // One 8x8 tile per wave (lane l: pixel (l&7, l>>3) of the tile).
 __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     const int lane = threadIdx.x & 63;
@@ -859,7 +971,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
         bool unused = false;
         const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
-        if (lane_mode)
+        if (lane_mode && kp.lane_walk == 2)
+            lane_walk2<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, reinterpret_cast<float*>(stk) +
+                                     static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
+        else if (lane_mode)
             lane_accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, blockDim.x, cap, wc);
         else
             accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
@@ -880,7 +995,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         }
         bool shadow = false;
         Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
-        if (lane_mode)
+        if (lane_mode && kp.lane_walk == 2)
+            lane_walk2<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, reinterpret_cast<float*>(stk) +
+                                    static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
+        else if (lane_mode)
             lane_accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, blockDim.x, cap, wc);
         else
             accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
@@ -896,8 +1014,10 @@ template <bool PERSISTENT, bool TIMED>
 __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ anodes,
                                                   const float4* __restrict__ lnodes,
                                                   const float4* __restrict__ prims,
-                                                  const float4* __restrict__ mat, KParams kp) {
-    const AccelPtrs A{anodes, lnodes, prims, kp.N};
+                                                  const float4* __restrict__ mat,
+                                                  const float4* __restrict__ lnodes2,
+                                                  const int* __restrict__ lroot2, KParams kp) {
+    const AccelPtrs A{anodes, lnodes, prims, kp.N, lnodes2, lroot2};
     extern __shared__ int lds_stack[];
     int* stk = lds_stack + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -997,6 +1117,9 @@ struct rt_ctx {
     // launch shape of k_accel (rt_set_launch)
     int waves_per_block = 4, persistent = 0, cu_count = 256;
     int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
+    int lane_walk = 2;        // 1: node-at-pop walk, 2: while-while with child boxes in the parent
+    float4* lnodes2 = nullptr;
+    int* lroot2 = nullptr;
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
@@ -1037,7 +1160,10 @@ void free_scene(rt_ctx* c) {
     hipFree(c->lnodes);
     hipFree(c->prims);
     hipFree(c->prim_idx_dev);
-    c->anodes = c->lnodes = c->prims = nullptr;
+    hipFree(c->lnodes2);
+    hipFree(c->lroot2);
+    c->anodes = c->lnodes = c->prims = c->lnodes2 = nullptr;
+    c->lroot2 = nullptr;
     c->prim_idx_dev = nullptr;
     c->accel_ok = false;
     c->have_scene = false;
@@ -1091,6 +1217,10 @@ int upload_accel(rt_ctx* c) {
     hipFree(c->lnodes);
     hipFree(c->prims);
     hipFree(c->prim_idx_dev);
+    hipFree(c->lnodes2);
+    hipFree(c->lroot2);
+    c->lnodes2 = nullptr;
+    c->lroot2 = nullptr;
     c->anodes = c->lnodes = c->prims = nullptr;
     c->prim_idx_dev = nullptr;
     c->accel_ok = false;
@@ -1124,6 +1254,35 @@ int upload_accel(rt_ctx* c) {
         ln[2 * j] = make_float4(bx.lo[0], bx.lo[1], bx.lo[2], bits_f(A.la[j]));
         ln[2 * j + 1] = make_float4(bx.hi[0], bx.hi[1], bx.hi[2], bits_f(A.lb[j]));
     }
+    // Second local layout (lane_walk2): inner nodes only, each with both child
+    // boxes and child codes (leaf: kLocal|kLeaf|start<<8|count, inner: kLocal|id).
+    std::vector<int> inner_id(M, -1);
+    int n_inner = 0;
+    for (size_t j = 0; j < M; ++j)
+        if (A.la[j] >= 0) inner_id[j] = n_inner++;
+    bool layout2 = true;
+    auto code_of = [&](size_t j) -> int {
+        if (A.la[j] < 0) {
+            const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
+            if (st >= (1u << 22) || cnt > 255u) layout2 = false;
+            return static_cast<int>(kLocal | kLeaf | (st << 8) | cnt);
+        }
+        return static_cast<int>(kLocal | static_cast<unsigned>(inner_id[j]));
+    };
+    std::vector<float4> ln2(4 * static_cast<size_t>(n_inner ? n_inner : 1));
+    for (size_t j = 0; j < M; ++j) {
+        if (A.la[j] < 0) continue;
+        const size_t l = static_cast<size_t>(A.la[j]), r = static_cast<size_t>(A.lb[j] & 0x3fffffff);
+        const rta::Box3 &bl = A.lbox[l], &br = A.lbox[r];
+        float4* q = &ln2[4 * static_cast<size_t>(inner_id[j])];
+        q[0] = make_float4(bl.lo[0], bl.lo[1], bl.lo[2], bits_f(code_of(l)));
+        q[1] = make_float4(bl.hi[0], bl.hi[1], bl.hi[2], bits_f(code_of(r)));
+        q[2] = make_float4(br.lo[0], br.lo[1], br.lo[2], bits_f((A.lb[j] >> 30) & 3));
+        q[3] = make_float4(br.hi[0], br.hi[1], br.hi[2], 0.f);
+    }
+    std::vector<int> lr2(N, kNoChild);
+    for (int k = 0; k < N; ++k)
+        if (A.local_root[k] >= 0) lr2[k] = code_of(static_cast<size_t>(A.local_root[k]));
     std::vector<int> ps(2 * (P ? P : 1));
     for (size_t i = 0; i < P; ++i) {
         ps[i] = A.prim_shape[i];
@@ -1137,6 +1296,13 @@ int upload_accel(rt_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->anodes, an.data(), an.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->lnodes, ln.data(), ln.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->prim_idx_dev, ps.data(), ps.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (layout2) {
+        if (hipMalloc(&c->lnodes2, ln2.size() * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&c->lroot2, lr2.size() * sizeof(int)) != hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        HIP_TRY(hipMemcpyAsync(c->lnodes2, ln2.data(), ln2.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->lroot2, lr2.data(), lr2.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    }
     if (P > 0)
         hipLaunchKernelGGL(k_pack_prims, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->geo_lin, c->prim_idx_dev,
                            c->prim_idx_dev + P, static_cast<int>(P), c->prims);
@@ -1226,9 +1392,12 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                  : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
         k2.lane_from_depth = c->lane_from_depth;
         k2.lane_stack = c->accel.max_stack;
-        const size_t lds = k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 4 : 0;
+        k2.lane_walk = (c->lane_walk == 2 && c->lnodes2) ? 2 : 1;
+        const size_t lds = k2.lane_from_depth < k2.maxBounces
+                               ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 4 * (k2.lane_walk == 2 ? 2 : 1)
+                               : 0;
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, c->anodes, c->lnodes, c->prims, c->mat,
-                           k2);
+                           c->lnodes2, c->lroot2, k2);
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
                            kp);
@@ -1566,6 +1735,13 @@ extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
 extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
     if (!c || lane_from_depth < 0) return RT_ERR_INVALID;
     c->lane_from_depth = lane_from_depth;
+    return RT_OK;
+}
+
+// Diagnostics: per-lane walk form (1 = node-at-pop, 2 = while-while).
+extern "C" int rt_debug_lane_walk(rt_ctx* c, int form) {
+    if (!c || (form != 1 && form != 2)) return RT_ERR_INVALID;
+    c->lane_walk = form;
     return RT_OK;
 }
 

@@ -435,6 +435,11 @@ class ComputeShader:
     def set_walk(self, lane_from_depth):
         self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
 
+    def debug_lane_walk(self, form):
+        fn = self._lib.rt_debug_lane_walk
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(form)), "rt_debug_lane_walk")
+
     def debug_tile_times(self, cap):
         """cap > 0: enable per-tile stamps (diagnostics); then tile_times(cap) reads them."""
         fn = self._lib.rt_debug_tile_times

@@ -20,6 +20,10 @@ import rtamd  # noqa: E402
 WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 1920, 1080, 3)}
 VARIANTS = {
     "accel_wpb4": dict(kernel=3, wpb=4, persistent=False, walk=1),
+    "accel_ww": dict(kernel=3, wpb=4, persistent=False, walk=1, form=2),
+    "accel_ww_w1": dict(kernel=3, wpb=1, persistent=False, walk=1, form=2),
+    "accel_ww_all": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2),
+    "accel_ww_all_w1": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2),
     "accel_wpb1": dict(kernel=3, wpb=1, persistent=False, walk=1),
     "accel_pers4": dict(kernel=3, wpb=4, persistent=True, walk=1),
     "accel_pers1": dict(kernel=3, wpb=1, persistent=True, walk=1),
@@ -55,6 +59,7 @@ for rnd in range(a.rounds):
         ctx.set_kernel(v["kernel"])
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
+        ctx.debug_lane_walk(v.get("form", 1))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         ctx.sync()
         img = out.cpu().numpy()
@@ -74,6 +79,7 @@ if a.times:
         ctx.set_kernel(v["kernel"])
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
+        ctx.debug_lane_walk(v.get("form", 1))
         ctx.debug_tile_times(tiles)
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         t = ctx.tile_times(tiles).astype(np.int64)
