@@ -266,6 +266,78 @@ struct LocalBuilder {
 
 bool shape_bound(const FlatShape& s, Box3& b) { return classify(s, b) == BOUNDED; }
 
+namespace {
+
+struct Cone {
+    double a[3];
+    double theta;  // half angle; > pi/2 = full
+    bool full() const { return theta >= 1.5; }
+};
+
+const double kConeMargin = 2e-3;  // radians beyond float error of N.d and of the cone test
+Cone full_cone() { return Cone{{0, 0, 0}, 10.0}; }
+
+// The INNER-capable normal of a shape: np = N.d must be > 0 for plane, wall
+// and (barycentric) triangle hits; spheres have every direction.
+Cone shape_cone(const FlatShape& s) {
+    if (s.type != RT_WALL && s.type != RT_TRIANGLE) return full_cone();
+    double n[3] = {s.planeNormal.x, s.planeNormal.y, s.planeNormal.z};
+    double l = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (!(l > 1e-20) || !std::isfinite(l)) return full_cone();
+    return Cone{{n[0] / l, n[1] / l, n[2] / l}, 0.0};
+}
+
+Cone merge(const Cone& x, const Cone& y) {
+    if (x.full() || y.full()) return full_cone();
+    double a[3] = {x.a[0] + y.a[0], x.a[1] + y.a[1], x.a[2] + y.a[2]};
+    double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    if (!(l > 1e-6)) return full_cone();
+    for (double& v : a) v /= l;
+    auto ang = [&](const double* b) {
+        double c = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+        return std::acos(std::max(-1.0, std::min(1.0, c)));
+    };
+    Cone c{{a[0], a[1], a[2]}, std::max(ang(x.a) + x.theta, ang(y.a) + y.theta)};
+    return c.full() ? full_cone() : c;
+}
+
+}  // namespace
+
+void build_cones(const FlatShape* shapes, AccelHost& A) {
+    const size_t M = A.lbox.size();
+    A.lcone.assign(4 * M, 0.f);
+    std::vector<Cone> cones(M, full_cone());
+    std::vector<char> done(M, 0);
+    std::function<const Cone&(size_t)> get = [&](size_t j) -> const Cone& {
+        if (done[j]) return cones[j];
+        Cone c;
+        if (A.la[j] < 0) {
+            const int st = -A.la[j] - 1, n = A.lb[j];
+            c = n > 0 ? shape_cone(shapes[A.prim_shape[st]]) : full_cone();
+            for (int i = 1; i < n; ++i) c = merge(c, shape_cone(shapes[A.prim_shape[st + i]]));
+        } else {
+            c = merge(get(static_cast<size_t>(A.la[j])), get(static_cast<size_t>(A.lb[j] & 0x3fffffff)));
+        }
+        cones[j] = c;
+        done[j] = 1;
+        return cones[j];
+    };
+    for (size_t j = 0; j < M; ++j) {
+        const Cone& c = get(j);
+        float* o = &A.lcone[4 * j];
+        const double t = c.theta + kConeMargin;
+        if (c.full() || t >= 1.5707) {
+            o[0] = o[1] = o[2] = 0.f;
+            o[3] = -4.f;
+        } else {
+            o[0] = static_cast<float>(c.a[0]);
+            o[1] = static_cast<float>(c.a[1]);
+            o[2] = static_cast<float>(c.a[2]);
+            o[3] = static_cast<float>(-std::sin(t));
+        }
+    }
+}
+
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
                  int leaf_threshold, int stack_cap, AccelHost& out) {
     (void)I;
@@ -386,6 +458,7 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     };
     visit(N - 1);
     out.max_stack = max_stack;
+    build_cones(shapes, out);
     return max_stack <= stack_cap;
 }
 

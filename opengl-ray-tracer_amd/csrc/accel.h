@@ -44,6 +44,11 @@ struct AccelHost {
     // Local BVH nodes: box; inner: left, right | axis<<30; leaf: -(start+1), count.
     std::vector<Box3> lbox;
     std::vector<int> la, lb;
+    // Back-face cone per local node: every shape below has an INNER-capable
+    // normal within the cone, so a ray with dot(axis, d) < thr*|d| cannot get
+    // an INNER hit there (np = N.d > 0 is required, gpu_shader.comp:206,278,294).
+    // thr = -sin(angle + margin), or -4 (never culls).
+    std::vector<float> lcone;     // 4 per local node: axis.xyz, thr
     int max_stack = 0;            // worst-case wave stack entries
     int always_prims = 0, bounded_prims = 0, local_leaves = 0;
 };
@@ -52,6 +57,9 @@ struct AccelHost {
 // leaf_threshold: leaves with more shapes than this get a local BVH.
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
                  int leaf_threshold, int stack_cap, AccelHost& out);
+
+// Back-face cones of the local nodes (fills A.lcone).
+void build_cones(const FlatShape* shapes, AccelHost& A);
 
 // Conservative bound of every INNER hit point of a shape (barycentric mode).
 // Returns false when no finite bound exists.

@@ -909,11 +909,14 @@ __device__ void lane_walk2(const AccelPtrs& A, const Ray& r, bool active, float 
                 start = static_cast<int>((uc >> 8) & 0x3fffffu);
                 count = static_cast<int>(uc & 0xffu);
             } else {
-                const float4* q = A.lnodes2 + 4 * static_cast<size_t>(uc & 0x3fffffffu);
-                const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3];
+                const float4* q = A.lnodes2 + 6 * static_cast<size_t>(uc & 0x3fffffffu);
+                const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
                 float ta, tb;
-                const bool ha = padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta);
-                const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb);
+                // box test, then the back-face cone: no INNER-capable normal below
+                const bool ha = padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta) &&
+                                !(dot(mk(ka.x, ka.y, ka.z), r.d) < ka.w * dlen);
+                const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
+                                !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
                 const int ca = __float_as_int(a0.w), cb = __float_as_int(a1.w);
                 // near child popped first: order by entry distance
                 const bool a_first = !(tb < ta);
@@ -1120,6 +1123,7 @@ struct rt_ctx {
     int lane_walk = 2;        // 1: node-at-pop walk, 2: while-while with child boxes in the parent
     float4* lnodes2 = nullptr;
     int* lroot2 = nullptr;
+    int cone_cull = 1;
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
@@ -1269,16 +1273,19 @@ int upload_accel(rt_ctx* c) {
         }
         return static_cast<int>(kLocal | static_cast<unsigned>(inner_id[j]));
     };
-    std::vector<float4> ln2(4 * static_cast<size_t>(n_inner ? n_inner : 1));
+    std::vector<float4> ln2(6 * static_cast<size_t>(n_inner ? n_inner : 1));
     for (size_t j = 0; j < M; ++j) {
         if (A.la[j] < 0) continue;
         const size_t l = static_cast<size_t>(A.la[j]), r = static_cast<size_t>(A.lb[j] & 0x3fffffff);
         const rta::Box3 &bl = A.lbox[l], &br = A.lbox[r];
-        float4* q = &ln2[4 * static_cast<size_t>(inner_id[j])];
+        float4* q = &ln2[6 * static_cast<size_t>(inner_id[j])];
         q[0] = make_float4(bl.lo[0], bl.lo[1], bl.lo[2], bits_f(code_of(l)));
         q[1] = make_float4(bl.hi[0], bl.hi[1], bl.hi[2], bits_f(code_of(r)));
         q[2] = make_float4(br.lo[0], br.lo[1], br.lo[2], bits_f((A.lb[j] >> 30) & 3));
         q[3] = make_float4(br.hi[0], br.hi[1], br.hi[2], 0.f);
+        const float *cl = &A.lcone[4 * l], *cr = &A.lcone[4 * r];
+        q[4] = make_float4(cl[0], cl[1], cl[2], c->cone_cull ? cl[3] : -4.f);
+        q[5] = make_float4(cr[0], cr[1], cr[2], c->cone_cull ? cr[3] : -4.f);
     }
     std::vector<int> lr2(N, kNoChild);
     for (int k = 0; k < N; ++k)
@@ -1736,6 +1743,13 @@ extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
     if (!c || lane_from_depth < 0) return RT_ERR_INVALID;
     c->lane_from_depth = lane_from_depth;
     return RT_OK;
+}
+
+// Diagnostics: back-face cone culling on/off (takes effect at the next upload).
+extern "C" int rt_debug_cone_cull(rt_ctx* c, int on) {
+    if (!c) return RT_ERR_INVALID;
+    c->cone_cull = on ? 1 : 0;
+    return c->have_scene ? upload_accel(c) : RT_OK;
 }
 
 // Diagnostics: per-lane walk form (1 = node-at-pop, 2 = while-while).

@@ -144,6 +144,8 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                 } else {
                     const int j = -code - 1;
                     if (!padded(ro, invs, dlen, A.lbox[j], limp)) continue;
+                    const float* k = &A.lcone[4 * j];  // back-face cone (accel.h)
+                    if (dot(mk(k[0], k[1], k[2]), rd) < k[3] * dlen) continue;
                     if (A.la[j] < 0) {
                         scan(-A.la[j] - 1, A.lb[j]);
                     } else {
