@@ -864,46 +864,52 @@ __device__ void lane_walk2(const AccelPtrs& A, const Ray& r, bool active, float 
     const V inv = inv_dir(r.d);
     const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
     const float dlen = len(r.d);
-    int sp = 1;
-    stk[0] = A.N - 1;
-    stt[0] = -INFINITY;
+    int sp = 0;
+    int cur = A.N - 1;  // node in hand (kept in registers while descending)
+    bool have = true;
     for (;;) {
         int start = 0, count = 0;
-        while (sp > 0 && count == 0) {
-            --sp;
-            const int code = stk[sp * stride];
-            const float te = stt[sp * stride];
+        while (count == 0) {
+            if (!have) {
+                if (sp == 0) break;
+                --sp;
+                const float te = stt[sp * stride];
+                const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+                if (te * dlen > limp) continue;  // a nearer hit was found since the push
+                cur = stk[sp * stride];
+                have = true;
+            }
             if (COUNT) wc.nodes++;
             const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
-            if (te * dlen > limp) continue;  // a nearer hit was found since the push
-            const unsigned uc = static_cast<unsigned>(code);
+            const unsigned uc = static_cast<unsigned>(cur);
+            have = false;
             if (!(uc & kLocal)) {
                 // reference node: the exact box test decides entry (gpu_shader.comp:395)
-                const float4* q = A.anodes + 4 * static_cast<size_t>(code);
-                const float4 e0 = q[0], e1 = q[1];
+                const float4* q = A.anodes + 4 * static_cast<size_t>(cur);
+                const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
                 if (!ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z))) continue;
-                const float4 c0 = q[2], c1 = q[3];
                 const int flags = __float_as_int(c0.w);
                 if ((flags & 8) && !padded_hit(r.o, invs, dlen, c0, c1, limp)) continue;
                 const int ia = __float_as_int(e0.w), ib = __float_as_int(e1.w);
                 if (ia < 0) {
                     start = -ia - 1;
                     count = ib;
-                    const int lr = A.lroot2[code];
-                    if (lr != kNoChild && sp < cap) {
-                        stk[sp * stride] = lr;
-                        stt[sp * stride] = -INFINITY;
-                        ++sp;
+                    const int lr = A.lroot2[cur];
+                    if (lr != kNoChild) {
+                        cur = lr;
+                        have = true;
                     }
-                } else if (sp + 2 <= cap) {
+                } else {
                     const int axis = flags & 3;
                     const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
                     const bool fwd = axis_of(r.d, axis) >= 0.0f;
-                    stk[sp * stride] = fwd ? upper : lower;
-                    stt[sp * stride] = -INFINITY;
-                    stk[(sp + 1) * stride] = fwd ? lower : upper;
-                    stt[(sp + 1) * stride] = -INFINITY;
-                    sp += 2;
+                    if (sp < cap) {
+                        stk[sp * stride] = fwd ? upper : lower;
+                        stt[sp * stride] = -INFINITY;
+                        ++sp;
+                    }
+                    cur = fwd ? lower : upper;
+                    have = true;
                 }
             } else if (uc & kLeaf) {
                 start = static_cast<int>((uc >> 8) & 0x3fffffu);
@@ -918,22 +924,22 @@ __device__ void lane_walk2(const AccelPtrs& A, const Ray& r, bool active, float 
                 const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
                                 !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
                 const int ca = __float_as_int(a0.w), cb = __float_as_int(a1.w);
-                // near child popped first: order by entry distance
-                const bool a_first = !(tb < ta);
-                if (ha && hb && sp + 2 <= cap) {
-                    stk[sp * stride] = a_first ? cb : ca;
-                    stt[sp * stride] = a_first ? tb : ta;
-                    stk[(sp + 1) * stride] = a_first ? ca : cb;
-                    stt[(sp + 1) * stride] = a_first ? ta : tb;
-                    sp += 2;
-                } else if ((ha || hb) && sp < cap) {
-                    stk[sp * stride] = ha ? ca : cb;
-                    stt[sp * stride] = ha ? ta : tb;
-                    ++sp;
+                if (ha && hb) {
+                    const bool a_first = !(tb < ta);  // nearer entry first
+                    if (sp < cap) {
+                        stk[sp * stride] = a_first ? cb : ca;
+                        stt[sp * stride] = a_first ? tb : ta;
+                        ++sp;
+                    }
+                    cur = a_first ? ca : cb;
+                    have = true;
+                } else if (ha || hb) {
+                    cur = ha ? ca : cb;
+                    have = true;
                 }
             }
         }
-        if (count == 0) return;  // stack empty
+        if (count == 0) return;  // walk finished
         for (int i = 0; i < count; ++i) {
             const GeoRec g = load_rec(A.prims, start + i);
             if (COUNT) wc.tests++;
