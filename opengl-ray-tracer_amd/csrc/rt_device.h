@@ -90,6 +90,7 @@ struct KParams {
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane
     int lane_stack;                          // per-lane LDS stack entries
     int lane_walk;                           // 1: node-at-pop walk, 2: while-while (lnodes2)
+    int tile_stride;                         // dispatch order -> image tile bijection
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).

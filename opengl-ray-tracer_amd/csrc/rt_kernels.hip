@@ -1040,7 +1040,12 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
         WalkCount wc{0u, 0u};
-        accel_tile<TIMED>(A, mat, kp, tile, stk, kp.lane_stack, wc);
+        // Scatter the dispatch order over the image: expensive tiles cluster in
+        // space, and tiles dispatched together share CUs (a bijection: stride
+        // coprime with the tile count).
+        const int img_tile = static_cast<int>((static_cast<unsigned long long>(tile) * kp.tile_stride) %
+                                              static_cast<unsigned long long>(kp.tiles));
+        accel_tile<TIMED>(A, mat, kp, img_tile, stk, kp.lane_stack, wc);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1051,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
                 mt = max(mt, __shfl_xor(mt, off));
             }
             if (lane == 0) {
-                unsigned long long* o = kp.tile_times + 6 * static_cast<size_t>(tile);
+                unsigned long long* o = kp.tile_times + 6 * static_cast<size_t>(img_tile);
                 o[0] = t0;
                 o[1] = t1;
                 o[2] = sn;
@@ -1130,6 +1135,7 @@ struct rt_ctx {
     float4* lnodes2 = nullptr;
     int* lroot2 = nullptr;
     int cone_cull = 1;
+    int scatter_tiles = 1;
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
@@ -1403,6 +1409,19 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         }
         auto kfn = c->persistent ? (c->tile_times ? k_accel<true, true> : k_accel<true, false>)
                                  : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
+        k2.tile_stride = 1;
+        if (c->scatter_tiles) {
+            // a prime stride (coprime with the tile count) near 0.38 * tiles
+            static const int primes[] = {7919, 104729, 15485863, 1299709, 611953};
+            for (int pr : primes)
+                if (k2.tiles % pr != 0) {
+                    k2.tile_stride = pr % k2.tiles == 0 ? 1 : pr % k2.tiles;
+                    break;
+                }
+            int g = k2.tile_stride, t = k2.tiles;  // keep it a bijection
+            while (t) { int tmp = g % t; g = t; t = tmp; }
+            if (g != 1) k2.tile_stride = 1;
+        }
         k2.lane_from_depth = c->lane_from_depth;
         k2.lane_stack = c->accel.max_stack;
         k2.lane_walk = (c->lane_walk == 2 && c->lnodes2) ? 2 : 1;
@@ -1756,6 +1775,13 @@ extern "C" int rt_debug_cone_cull(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID;
     c->cone_cull = on ? 1 : 0;
     return c->have_scene ? upload_accel(c) : RT_OK;
+}
+
+// Diagnostics: scattered tile dispatch order on/off.
+extern "C" int rt_debug_scatter(rt_ctx* c, int on) {
+    if (!c) return RT_ERR_INVALID;
+    c->scatter_tiles = on ? 1 : 0;
+    return RT_OK;
 }
 
 // Diagnostics: per-lane walk form (1 = node-at-pop, 2 = while-while).

@@ -445,6 +445,11 @@ class ComputeShader:
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(bool(on))), "rt_debug_cone_cull")
 
+    def debug_scatter(self, on):
+        fn = self._lib.rt_debug_scatter
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(bool(on))), "rt_debug_scatter")
+
     def debug_tile_times(self, cap):
         """cap > 0: enable per-tile stamps (diagnostics); then tile_times(cap) reads them."""
         fn = self._lib.rt_debug_tile_times

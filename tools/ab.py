@@ -24,6 +24,10 @@ VARIANTS = {
     "accel_ww_w1": dict(kernel=3, wpb=1, persistent=False, walk=1, form=2),
     "accel_ww_all": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2),
     "accel_ww_all_w1": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2),
+    "ww_all_noscatter": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2, scatter=0),
+    "ww_all_w1_noscatter": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2, scatter=0),
+    "ww_all_pers": dict(kernel=3, wpb=4, persistent=True, walk=0, form=2),
+    "ww_pers_w1": dict(kernel=3, wpb=1, persistent=True, walk=1, form=2),
     "ww_nocone": dict(kernel=3, wpb=4, persistent=False, walk=1, form=2, cone=0),
     "ww_all_nocone": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2, cone=0),
     "accel_wpb1": dict(kernel=3, wpb=1, persistent=False, walk=1),
@@ -63,6 +67,7 @@ for rnd in range(a.rounds):
         ctx.set_walk(v["walk"])
         ctx.debug_lane_walk(v.get("form", 1))
         ctx.debug_cone_cull(v.get("cone", 1))
+        ctx.debug_scatter(v.get("scatter", 1))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         ctx.sync()
         img = out.cpu().numpy()
@@ -84,6 +89,7 @@ if a.times:
         ctx.set_walk(v["walk"])
         ctx.debug_lane_walk(v.get("form", 1))
         ctx.debug_cone_cull(v.get("cone", 1))
+        ctx.debug_scatter(v.get("scatter", 1))
         ctx.debug_tile_times(tiles)
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         t = ctx.tile_times(tiles).astype(np.int64)
