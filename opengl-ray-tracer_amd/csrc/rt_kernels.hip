@@ -1129,13 +1129,13 @@ struct rt_ctx {
     int img_w = 0, img_h = 0;
     unsigned long long* stats_dev = nullptr;
     // launch shape of k_accel (rt_set_launch)
-    int waves_per_block = 4, persistent = 0, cu_count = 256;
-    int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
+    int waves_per_block = 1, persistent = 0, cu_count = 256;
+    int lane_from_depth = 0;  // bounces >= this use the per-lane walk (0: all, large: none)
     int lane_walk = 2;        // 1: node-at-pop walk, 2: while-while with child boxes in the parent
     float4* lnodes2 = nullptr;
     int* lroot2 = nullptr;
     int cone_cull = 1;
-    int scatter_tiles = 1;
+    int scatter_tiles = 0;
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;

@@ -738,3 +738,35 @@ int orc_trace_rays(const FlatShape* shapes, int S, const FlatNode* nodes, int N,
     }
     return 0;
 }
+
+/* Every ray the BVH branch of main() traces for pixel (x, y): kind 0 =
+ * closest-hit (primary/reflection), 1 = shadow; with the shadow query's
+ * limit (min(light distance, 1e20)). Returns the ray count (<= cap).
+ * Diagnostics for tests/tools only. */
+int orc_pixel_rays(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                   const FlatCamera* cam, const FlatLight* light, const rt_params* p, int x, int y,
+                   float* o, float* d, float* lim, int* kind, int cap) {
+    scene_t sc = {shapes, S, nodes, N, idx, I, cam, light, *p};
+    int n = 0;
+    float fx = (float)x, fy = (float)y;
+    ray_t ray = get_ray(cam, 2.0f * fx / p->resX - 1.0f, 1.0f - 2.0f * fy / p->resY);
+    v3 lpos = fv(light->position);
+    for (int depth = 0; depth < p->maxBounces && n < cap; ++depth) {
+        o[3 * n] = ray.o.x; o[3 * n + 1] = ray.o.y; o[3 * n + 2] = ray.o.z;
+        d[3 * n] = ray.d.x; d[3 * n + 1] = ray.d.y; d[3 * n + 2] = ray.d.z;
+        lim[n] = 1e20f; kind[n] = 0; ++n;
+        hit_t hit = intersect_scene2(&sc, ray, NULL);
+        if (hit.type != INNER || n >= cap) break;
+        ray_t sr;
+        sr.o = add(hit.hit, muls(hit.normal, 1e-3f));
+        sr.d = normalize3(sub(lpos, hit.hit));
+        o[3 * n] = sr.o.x; o[3 * n + 1] = sr.o.y; o[3 * n + 2] = sr.o.z;
+        d[3 * n] = sr.d.x; d[3 * n + 1] = sr.d.y; d[3 * n + 2] = sr.d.z;
+        lim[n] = fming(distance3(lpos, hit.hit), 1e20f); kind[n] = 1; ++n;
+        if (!(hit.mat->specularStrength > 0)) break;
+        v3 rd = reflect3(ray.d, hit.normal);
+        ray.o = add(hit.hit, muls(hit.normal, 1e-3f));
+        ray.d = rd;
+    }
+    return n;
+}

@@ -100,6 +100,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
     out_info[3] = A.max_stack;
     long long tests = 0;
     for (int r = 0; r < R; ++r) {
+        long long nodes_before = 0;
         V ro = mk(o[3 * r], o[3 * r + 1], o[3 * r + 2]), rd = mk(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
         V inv = mk(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
         V invs = mk(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
@@ -130,6 +131,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     }
                 };
                 if (std::getenv("ACDBG")) std::printf("pop %d lim %g best %d %g\n", code, limp, b.shape, b.d);
+                ++nodes_before;
                 if (code >= 0) {
                     const FlatNode& nd = nodes[code];
                     if (!ref_aabb(ro, inv, nd.boundsMin, nd.boundsMax)) continue;
@@ -156,6 +158,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
             }
             if (shadow) out_shadow[r] = hit_shadow ? 1 : 0;
             else { out_shape[r] = b.shape; out_d[r] = b.d; }
+            if (out_info[7] == 12345 && pass == (lim[r] < 1e19f ? 1 : 0)) out_shape[r] = static_cast<int>(nodes_before);
         }
     }
     out_info[4] = static_cast<int>(tests / (R > 0 ? R : 1));
