@@ -525,10 +525,12 @@ struct AccelPtrs {
     int N;
     const float4* __restrict__ lnodes2; // 4 float4 per local inner node: both child boxes + codes
     const int* __restrict__ lroot2;     // per reference node: local root as a child code, or kNoChild
+    const float4* __restrict__ anodes2; // 8 float4 per reference inner node: both children's exact + content boxes
+    const int4* __restrict__ tleaf;     // per reference leaf: plain start, plain count, local root code
 };
 
 // Child codes of the per-lane walk's stack and of lnodes2 entries.
-constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u;
+constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u, kTopLeaf = 0x20000000u;
 constexpr int kNoChild = 0x7fffffff;
 
 struct Best {
@@ -955,6 +957,125 @@ __device__ void lane_walk2(const AccelPtrs& A, const Ray& r, bool active, float 
     }
 }
 
+// Per-lane walk, third form: lane_walk2 plus wide reference nodes. An inner
+// reference node holds both children's exact boxes (the reference's entry
+// test, evaluated at the parent: same boxes, same arithmetic, same result)
+// and their conservative content boxes, so a child the lane does not enter
+// costs no iteration and children are ordered by their entry distance.
+// Codes: reference inner node k; kTopLeaf|k reference leaf; kLocal|j local
+// inner node; kLocal|kLeaf|start<<8|count local leaf.
+__device__ __forceinline__ int top_code(int k, int ia) { return ia < 0 ? static_cast<int>(kTopLeaf | k) : k; }
+
+template <bool SHADOW, bool COUNT = false>
+__device__ void lane_walk3(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
+                           int* stk, float* stt, int stride, int cap, WalkCount& wc) {
+    if (A.N <= 0 || !active) return;
+    const V inv = inv_dir(r.d);
+    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
+    const float dlen = len(r.d);
+    int sp = 0, cur = 0;
+    bool have = false;
+    {
+        // the root has no parent: its own exact box decides (gpu_shader.comp:386-395)
+        const float4* q = A.anodes + 4 * static_cast<size_t>(A.N - 1);
+        const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
+        const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+        if (ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z)) &&
+            (!(__float_as_int(c0.w) & 8) || padded_hit(r.o, invs, dlen, c0, c1, limp))) {
+            cur = top_code(A.N - 1, __float_as_int(e0.w));
+            have = true;
+        }
+    }
+    for (;;) {
+        int start = 0, count = 0;
+        while (count == 0) {
+            if (!have) {
+                if (sp == 0) break;
+                --sp;
+                const float te = stt[sp * stride];
+                const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+                if (te * dlen > limp) continue;  // a nearer hit was found since the push
+                cur = stk[sp * stride];
+                have = true;
+            }
+            if (COUNT) wc.nodes++;
+            const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+            const unsigned uc = static_cast<unsigned>(cur);
+            have = false;
+            if (!(uc & (kLocal | kTopLeaf))) {
+                const float4* q = A.anodes2 + 8 * static_cast<size_t>(uc);
+                const float4 ae0 = q[0], ae1 = q[1], ac0 = q[2], ac1 = q[3];
+                const float4 be0 = q[4], be1 = q[5], bc0 = q[6], bc1 = q[7];
+                float ta = -INFINITY, tb = -INFINITY;
+                bool ha = ray_aabb(r.o, inv, mk(ae0.x, ae0.y, ae0.z), mk(ae1.x, ae1.y, ae1.z));
+                bool hb = ray_aabb(r.o, inv, mk(be0.x, be0.y, be0.z), mk(be1.x, be1.y, be1.z));
+                if (ha && (__float_as_int(ac0.w) & 8)) ha = padded_hit_t(r.o, invs, dlen, ac0, ac1, limp, ta);
+                if (hb && (__float_as_int(bc0.w) & 8)) hb = padded_hit_t(r.o, invs, dlen, bc0, bc1, limp, tb);
+                const int ca = __float_as_int(ae0.w), cb = __float_as_int(ae1.w);
+                if (ha && hb) {
+                    const bool a_first = !(tb < ta);
+                    if (sp < cap) {
+                        stk[sp * stride] = a_first ? cb : ca;
+                        stt[sp * stride] = a_first ? tb : ta;
+                        ++sp;
+                    }
+                    cur = a_first ? ca : cb;
+                    have = true;
+                } else if (ha || hb) {
+                    cur = ha ? ca : cb;
+                    have = true;
+                }
+            } else if (uc & kTopLeaf) {
+                const int4 lf = A.tleaf[uc & 0x1fffffffu];
+                start = lf.x;
+                count = lf.y;
+                if (lf.z != kNoChild) {
+                    cur = lf.z;
+                    have = true;
+                }
+            } else if (uc & kLeaf) {
+                start = static_cast<int>((uc >> 8) & 0x3fffffu);
+                count = static_cast<int>(uc & 0xffu);
+            } else {
+                const float4* q = A.lnodes2 + 6 * static_cast<size_t>(uc & 0x3fffffffu);
+                const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
+                float ta, tb;
+                const bool ha = padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta) &&
+                                !(dot(mk(ka.x, ka.y, ka.z), r.d) < ka.w * dlen);
+                const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
+                                !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
+                const int ca = __float_as_int(a0.w), cb = __float_as_int(a1.w);
+                if (ha && hb) {
+                    const bool a_first = !(tb < ta);
+                    if (sp < cap) {
+                        stk[sp * stride] = a_first ? cb : ca;
+                        stt[sp * stride] = a_first ? tb : ta;
+                        ++sp;
+                    }
+                    cur = a_first ? ca : cb;
+                    have = true;
+                } else if (ha || hb) {
+                    cur = ha ? ca : cb;
+                    have = true;
+                }
+            }
+        }
+        if (count == 0) return;  // walk finished
+        for (int i = 0; i < count; ++i) {
+            const GeoRec g = load_rec(A.prims, start + i);
+            if (COUNT) wc.tests++;
+            if (SHADOW) {
+                if (try_shadow(g, r, lim_shadow)) {
+                    shadow = true;
+                    return;
+                }
+            } else {
+                try_closest(g, start + i, r, b);
+            }
+        }
+    }
+}
+
 // One 8x8 tile per wave (lane l: pixel (l&7, l>>3) of the tile).
 __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     const int lane = threadIdx.x & 63;
@@ -980,7 +1101,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
         bool unused = false;
         const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
-        if (lane_mode && kp.lane_walk == 2)
+        if (lane_mode && kp.lane_walk == 3)
+            lane_walk3<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, reinterpret_cast<float*>(stk) +
+                                     static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
+        else if (lane_mode && kp.lane_walk == 2)
             lane_walk2<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, reinterpret_cast<float*>(stk) +
                                      static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
         else if (lane_mode)
@@ -1004,7 +1128,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         }
         bool shadow = false;
         Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
-        if (lane_mode && kp.lane_walk == 2)
+        if (lane_mode && kp.lane_walk == 3)
+            lane_walk3<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, reinterpret_cast<float*>(stk) +
+                                    static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
+        else if (lane_mode && kp.lane_walk == 2)
             lane_walk2<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, reinterpret_cast<float*>(stk) +
                                     static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
         else if (lane_mode)
@@ -1025,8 +1152,10 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
                                                   const float4* __restrict__ prims,
                                                   const float4* __restrict__ mat,
                                                   const float4* __restrict__ lnodes2,
-                                                  const int* __restrict__ lroot2, KParams kp) {
-    const AccelPtrs A{anodes, lnodes, prims, kp.N, lnodes2, lroot2};
+                                                  const int* __restrict__ lroot2,
+                                                  const float4* __restrict__ anodes2,
+                                                  const int4* __restrict__ tleaf, KParams kp) {
+    const AccelPtrs A{anodes, lnodes, prims, kp.N, lnodes2, lroot2, anodes2, tleaf};
     extern __shared__ int lds_stack[];
     int* stk = lds_stack + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -1131,9 +1260,11 @@ struct rt_ctx {
     // launch shape of k_accel (rt_set_launch)
     int waves_per_block = 1, persistent = 0, cu_count = 256;
     int lane_from_depth = 0;  // bounces >= this use the per-lane walk (0: all, large: none)
-    int lane_walk = 2;        // 1: node-at-pop walk, 2: while-while with child boxes in the parent
+    int lane_walk = 3;        // 1: node-at-pop, 2: while-while + local child boxes, 3: + wide reference nodes
     float4* lnodes2 = nullptr;
     int* lroot2 = nullptr;
+    float4* anodes2 = nullptr;
+    int4* tleaf = nullptr;
     int cone_cull = 1;
     int scatter_tiles = 0;
     int* tile_counter = nullptr;
@@ -1178,8 +1309,11 @@ void free_scene(rt_ctx* c) {
     hipFree(c->prim_idx_dev);
     hipFree(c->lnodes2);
     hipFree(c->lroot2);
-    c->anodes = c->lnodes = c->prims = c->lnodes2 = nullptr;
+    hipFree(c->anodes2);
+    hipFree(c->tleaf);
+    c->anodes = c->lnodes = c->prims = c->lnodes2 = c->anodes2 = nullptr;
     c->lroot2 = nullptr;
+    c->tleaf = nullptr;
     c->prim_idx_dev = nullptr;
     c->accel_ok = false;
     c->have_scene = false;
@@ -1235,8 +1369,11 @@ int upload_accel(rt_ctx* c) {
     hipFree(c->prim_idx_dev);
     hipFree(c->lnodes2);
     hipFree(c->lroot2);
-    c->lnodes2 = nullptr;
+    hipFree(c->anodes2);
+    hipFree(c->tleaf);
+    c->lnodes2 = c->anodes2 = nullptr;
     c->lroot2 = nullptr;
+    c->tleaf = nullptr;
     c->anodes = c->lnodes = c->prims = nullptr;
     c->prim_idx_dev = nullptr;
     c->accel_ok = false;
@@ -1302,6 +1439,32 @@ int upload_accel(rt_ctx* c) {
     std::vector<int> lr2(N, kNoChild);
     for (int k = 0; k < N; ++k)
         if (A.local_root[k] >= 0) lr2[k] = code_of(static_cast<size_t>(A.local_root[k]));
+    // Wide reference nodes (lane_walk3): both children's exact + content boxes.
+    std::vector<float4> an2(8 * static_cast<size_t>(N));
+    std::vector<int4> tl(static_cast<size_t>(N), make_int4(0, 0, kNoChild, 0));
+    bool wide_ok = N < (1 << 29);
+    for (int k = 0; k < N && wide_ok; ++k) {
+        const FlatNode& n = c->host_nodes[k];
+        if (n.leftChild == -1) {
+            tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr2[k], 0);
+            continue;
+        }
+        const int ch[2] = {n.leftChild, n.rightChild};
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const FlatNode& cn = c->host_nodes[ch[s2]];
+            const rta::Box3& cb = A.content[ch[s2]];
+            const int code = cn.leftChild == -1 ? static_cast<int>(kTopLeaf | static_cast<unsigned>(ch[s2])) : ch[s2];
+            float4* q = &an2[8 * static_cast<size_t>(k) + 4 * s2];
+            q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, bits_f(s2 == 0 ? code : 0));
+            q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, 0.f);
+            q[2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[ch[s2]] & 8));
+            q[3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
+        }
+        // child B's code lives in q[1].w of child A (the layout read by lane_walk3)
+        const FlatNode& cnb = c->host_nodes[ch[1]];
+        an2[8 * static_cast<size_t>(k) + 1].w =
+            bits_f(cnb.leftChild == -1 ? static_cast<int>(kTopLeaf | static_cast<unsigned>(ch[1])) : ch[1]);
+    }
     std::vector<int> ps(2 * (P ? P : 1));
     for (size_t i = 0; i < P; ++i) {
         ps[i] = A.prim_shape[i];
@@ -1315,6 +1478,13 @@ int upload_accel(rt_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->anodes, an.data(), an.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->lnodes, ln.data(), ln.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->prim_idx_dev, ps.data(), ps.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    if (layout2 && wide_ok) {
+        if (hipMalloc(&c->anodes2, an2.size() * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&c->tleaf, tl.size() * sizeof(int4)) != hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        HIP_TRY(hipMemcpyAsync(c->anodes2, an2.data(), an2.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->tleaf, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    }
     if (layout2) {
         if (hipMalloc(&c->lnodes2, ln2.size() * sizeof(float4)) != hipSuccess ||
             hipMalloc(&c->lroot2, lr2.size() * sizeof(int)) != hipSuccess)
@@ -1424,12 +1594,12 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         }
         k2.lane_from_depth = c->lane_from_depth;
         k2.lane_stack = c->accel.max_stack;
-        k2.lane_walk = (c->lane_walk == 2 && c->lnodes2) ? 2 : 1;
+        k2.lane_walk = c->lnodes2 ? ((c->lane_walk == 3 && c->anodes2) ? 3 : (c->lane_walk >= 2 ? 2 : 1)) : 1;
         const size_t lds = k2.lane_from_depth < k2.maxBounces
-                               ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 4 * (k2.lane_walk == 2 ? 2 : 1)
+                               ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 4 * (k2.lane_walk >= 2 ? 2 : 1)
                                : 0;
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, c->anodes, c->lnodes, c->prims, c->mat,
-                           c->lnodes2, c->lroot2, k2);
+                           c->lnodes2, c->lroot2, c->anodes2, c->tleaf, k2);
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
                            kp);
@@ -1786,7 +1956,7 @@ extern "C" int rt_debug_scatter(rt_ctx* c, int on) {
 
 // Diagnostics: per-lane walk form (1 = node-at-pop, 2 = while-while).
 extern "C" int rt_debug_lane_walk(rt_ctx* c, int form) {
-    if (!c || (form != 1 && form != 2)) return RT_ERR_INVALID;
+    if (!c || form < 1 || form > 3) return RT_ERR_INVALID;
     c->lane_walk = form;
     return RT_OK;
 }
