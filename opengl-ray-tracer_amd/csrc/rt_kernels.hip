@@ -1076,6 +1076,124 @@ __device__ void lane_walk3(const AccelPtrs& A, const Ray& r, bool active, float 
     }
 }
 
+// Packet form of lane_walk3: one wave-uniform walk with a 64-bit lane mask
+// per stack entry (VGPR-resident stack, scalar node loads), using the wide
+// reference nodes and the local child-box nodes with back-face cones. The
+// node in hand stays in scalar registers while descending; children are
+// tested at the parent for every lane of the mask.
+template <bool SHADOW, bool COUNT = false>
+__device__ void packet_walk3(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
+                             bool& shadow, WalkCount& wc) {
+    unsigned long long m = __ballot(active);
+    if (A.N <= 0 || m == 0) return;
+    const V inv = inv_dir(r.d);
+    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
+    const float dlen = len(r.d);
+    WaveStack st{0, 0, 0, 0};
+    int cur = 0;
+    {
+        const float4* q = A.anodes + 4 * static_cast<size_t>(A.N - 1);
+        const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
+        const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+        const bool h = active && ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z)) &&
+                       (!(__float_as_int(c0.w) & 8) || padded_hit(r.o, invs, dlen, c0, c1, limp));
+        m = __ballot(h);
+        cur = top_code(A.N - 1, __float_as_int(e0.w));
+    }
+    unsigned long long done = 0;
+    for (;;) {
+        if (m == 0) {
+            if (st.sp == 0) return;
+            st.pop(cur, m);
+            cur = uni(cur);
+            if (SHADOW) m &= ~done;
+            continue;
+        }
+        if (COUNT && lane_in(m)) wc.nodes++;
+        const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
+        const unsigned uc = static_cast<unsigned>(cur);
+        bool ha = false, hb = false;
+        float ta = -INFINITY, tb = -INFINITY;
+        int ca = 0, cb = 0, start = 0, count = 0;
+        unsigned long long leaf_m = 0;
+        if (!(uc & (kLocal | kTopLeaf))) {
+            const float4* q = A.anodes2 + 8 * static_cast<size_t>(uc);
+            const float4 ae0 = q[0], ae1 = q[1], ac0 = q[2], ac1 = q[3];
+            const float4 be0 = q[4], be1 = q[5], bc0 = q[6], bc1 = q[7];
+            const bool in = lane_in(m);
+            ha = in && ray_aabb(r.o, inv, mk(ae0.x, ae0.y, ae0.z), mk(ae1.x, ae1.y, ae1.z));
+            hb = in && ray_aabb(r.o, inv, mk(be0.x, be0.y, be0.z), mk(be1.x, be1.y, be1.z));
+            if (ha && (__float_as_int(ac0.w) & 8)) ha = padded_hit_t(r.o, invs, dlen, ac0, ac1, limp, ta);
+            if (hb && (__float_as_int(bc0.w) & 8)) hb = padded_hit_t(r.o, invs, dlen, bc0, bc1, limp, tb);
+            ca = uni(__float_as_int(ae0.w));
+            cb = uni(__float_as_int(ae1.w));
+        } else if (uc & kTopLeaf) {
+            const int4 lf = A.tleaf[uc & 0x1fffffffu];
+            start = uni(lf.x);
+            count = uni(lf.y);
+            leaf_m = m;
+            const int lr = uni(lf.z);
+            ca = lr;
+            ha = (lr != kNoChild) && lane_in(m);  // local root: entered with the leaf
+        } else if (uc & kLeaf) {
+            start = static_cast<int>((uc >> 8) & 0x3fffffu);
+            count = static_cast<int>(uc & 0xffu);
+            leaf_m = m;
+        } else {
+            const float4* q = A.lnodes2 + 6 * static_cast<size_t>(uc & 0x3fffffffu);
+            const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
+            const bool in = lane_in(m);
+            ha = in && padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta) &&
+                 !(dot(mk(ka.x, ka.y, ka.z), r.d) < ka.w * dlen);
+            hb = in && padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
+                 !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
+            ca = uni(__float_as_int(a0.w));
+            cb = uni(__float_as_int(a1.w));
+        }
+        if (count > 0) {
+            bool live = lane_in(leaf_m);
+            for (int i = 0; i < count; ++i) {
+                const GeoRec g = load_rec(A.prims, start + i);
+                if (live) {
+                    if (COUNT) wc.tests++;
+                    if (SHADOW) {
+                        if (try_shadow(g, r, lim_shadow)) {
+                            shadow = true;
+                            live = false;
+                        }
+                    } else {
+                        try_closest(g, start + i, r, b);
+                    }
+                }
+                if (SHADOW && __ballot(live) == 0) break;
+            }
+            if (SHADOW) {
+                done = __ballot(shadow);
+                if (ha && shadow) ha = false;
+            }
+        }
+        const unsigned long long ma = __ballot(ha), mb = __ballot(hb);
+        if (ma && mb) {
+            // near first for the wave: the child the first lane of both masks enters sooner
+            const int rep = __builtin_ctzll(ma & mb ? (ma & mb) : ma);
+            const float ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ta), rep));
+            const float rb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tb), rep));
+            const bool a_first = !(rb < ra);
+            if (st.sp < kMaxStack) st.push(a_first ? cb : ca, a_first ? mb : ma);
+            cur = a_first ? ca : cb;
+            m = a_first ? ma : mb;
+        } else if (ma) {
+            cur = ca;
+            m = ma;
+        } else if (mb) {
+            cur = cb;
+            m = mb;
+        } else {
+            m = 0;
+        }
+    }
+}
+
 // One 8x8 tile per wave (lane l: pixel (l&7, l>>3) of the tile).
 __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     const int lane = threadIdx.x & 63;
@@ -1109,6 +1227,8 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
                                      static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
         else if (lane_mode)
             lane_accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, blockDim.x, cap, wc);
+        else if (kp.lane_walk == 3)
+            packet_walk3<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
         else
             accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
         if (alive && best.slot < 0) {
@@ -1136,6 +1256,8 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
                                     static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
         else if (lane_mode)
             lane_accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, blockDim.x, cap, wc);
+        else if (kp.lane_walk == 3)
+            packet_walk3<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         else
             accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);

@@ -27,6 +27,8 @@ VARIANTS = {
     "default": dict(kernel=0, wpb=1, persistent=False, walk=0, form=3, scatter=0),
     "w3_hybrid": dict(kernel=3, wpb=1, persistent=False, walk=1, form=3, scatter=0),
     "w2_all": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2, scatter=0),
+    "w3_packet": dict(kernel=3, wpb=4, persistent=False, walk=99, form=3, scatter=0),
+    "w3_hybrid4": dict(kernel=3, wpb=4, persistent=False, walk=1, form=3, scatter=0),
     "ww_all_noscatter": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2, scatter=0),
     "ww_all_w1_noscatter": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2, scatter=0),
     "ww_all_pers": dict(kernel=3, wpb=4, persistent=True, walk=0, form=2),
