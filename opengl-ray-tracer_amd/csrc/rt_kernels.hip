@@ -1381,7 +1381,7 @@ struct rt_ctx {
     unsigned long long* stats_dev = nullptr;
     // launch shape of k_accel (rt_set_launch)
     int waves_per_block = 1, persistent = 0, cu_count = 256;
-    int lane_from_depth = 0;  // bounces >= this use the per-lane walk (0: all, large: none)
+    int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
     int lane_walk = 3;        // 1: node-at-pop, 2: while-while + local child boxes, 3: + wide reference nodes
     float4* lnodes2 = nullptr;
     int* lroot2 = nullptr;

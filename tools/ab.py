@@ -24,7 +24,8 @@ VARIANTS = {
     "accel_ww_w1": dict(kernel=3, wpb=1, persistent=False, walk=1, form=2),
     "accel_ww_all": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2),
     "accel_ww_all_w1": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2),
-    "default": dict(kernel=0, wpb=1, persistent=False, walk=0, form=3, scatter=0),
+    "default": dict(kernel=0, wpb=1, persistent=False, walk=1, form=3, scatter=0),
+    "w3_all": dict(kernel=3, wpb=1, persistent=False, walk=0, form=3, scatter=0),
     "w3_hybrid": dict(kernel=3, wpb=1, persistent=False, walk=1, form=3, scatter=0),
     "w2_all": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2, scatter=0),
     "w3_packet": dict(kernel=3, wpb=4, persistent=False, walk=99, form=3, scatter=0),
