@@ -351,7 +351,12 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 
     std::vector<Box3> sbox(S);
     std::vector<int> scls(S);
-    for (int i = 0; i < S; ++i) scls[i] = classify(shapes[i], sbox[i]);
+    for (int i = 0; i < S; ++i) {
+        scls[i] = classify(shapes[i], sbox[i]);
+        if (scls[i] == BOUNDED)
+            for (int a = 0; a < 3; ++a)
+                out.scene_mag = std::max({out.scene_mag, std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
+    }
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).

@@ -50,6 +50,11 @@ struct AccelHost {
     // thr = -sin(angle + margin), or -4 (never culls).
     std::vector<float> lcone;     // 4 per local node: axis.xyz, thr
     int max_stack = 0;            // worst-case wave stack entries
+    // Largest |coordinate| of any bounded shape box. The padding is relative to
+    // the scene's coordinates; ray origins far outside (a camera more than 100x
+    // the scene's magnitude away) would need more, so the renderer then skips
+    // the accelerator for that frame (rt_kernels.hip, launch()).
+    float scene_mag = 0.f;
     int always_prims = 0, bounded_prims = 0, local_leaves = 0;
 };
 

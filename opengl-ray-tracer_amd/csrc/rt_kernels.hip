@@ -1671,7 +1671,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     dim3 grid((kp.width + kTileW - 1) / kTileW, (kp.out_rows + kTileH - 1) / kTileH);
     if (grid.y > 65535u) return RT_ERR_INVALID;
     int kind = c->kernel;
-    const bool accel_usable = c->accel_ok && kp.useBVH && !kp.useMT;
+    const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
+    const bool accel_usable = c->accel_ok && kp.useBVH && !kp.useMT && cmag <= 100.f * (c->accel.scene_mag + 1.f);
     if (kind == RT_KERNEL_AUTO) kind = accel_usable ? RT_KERNEL_ACCEL : RT_KERNEL_PACKET;
     if (kind == RT_KERNEL_ACCEL && !accel_usable) kind = RT_KERNEL_PACKET;  // same image either way
     const size_t lds = static_cast<size_t>(kp.max_stack) * kBlock * sizeof(int);

@@ -327,3 +327,33 @@ def test_accel_ties_resolve_like_the_reference(ctx):
     for k in KERNELS:
         img = gpu_rows(ctx, fs2, W, H, p, y0=900, rows=40, kernel=k)
         check(img, ref, f"ties kernel {k}")
+
+
+def test_far_camera_falls_back_exactly(ctx):
+    """A camera far outside the scene's magnitude skips the accelerator (its
+    padding is relative to the scene); the frame still matches the oracle."""
+    W, H = 64, 48
+    fs = rtamd.generate(2, 0, W, H)
+    cam = fs.camera.copy()
+    cam["Position"] = cam["Position"] - cam["Front"] * np.float32(60000.0)
+    fs2 = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, cam, fs.light)
+    p = oracle.params(W, H, 2)
+    ref, _ = oracle.render(fs2, W, H, p)
+    img = gpu_rows(ctx, fs2, W, H, p, kernel=rtamd.KERNEL_AUTO)
+    assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_PACKET
+    check(img, ref, "far camera")
+
+
+@pytest.mark.parametrize("walk", [0, 1, 99])
+def test_walk_policies_identical(ctx, walk):
+    """Packet / per-lane / hybrid walks render the same frame (config 5 rows)."""
+    W, H = 1920, 1080
+    fs = rtamd.generate(5, 0, W, H)
+    p = oracle.params(W, H, 3)
+    ref, _ = oracle.render(fs, W, H, p, y0=480, out_rows=16)
+    ctx.set_walk(walk)
+    try:
+        img = gpu_rows(ctx, fs, W, H, p, y0=480, rows=16, kernel=rtamd.KERNEL_ACCEL)
+    finally:
+        ctx.set_walk(1)
+    check(img, ref, f"walk {walk}")
