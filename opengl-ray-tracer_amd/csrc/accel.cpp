@@ -60,10 +60,20 @@ struct BoxAcc {
 
 // Relative padding: float error of every quantity the reference test computes
 // is ~1e-7 of the coordinates' magnitude (1e-3 of it for the barycentric
-// solve on the thinnest triangle admitted, 3e-4 for a grazing sphere root at
-// 1000 units); 1e-3 of (size + magnitude) covers all of them with room.
+// solve on the thinnest triangle admitted); 1e-3 of (size + magnitude) covers
+// them with room, for ray origins up to AccelHost::origin_lim.
+//
+// A plane-based hit point computed from a ray with origin o lies within
+// ~4u(|D| + |o|) of the plane (u = 2^-24) and its projection inside the shape,
+// wherever the rounding puts it along a grazing ray, so those bounds hold for
+// any such origin. The sphere root does not: D = bb^2 - 4*aa*cc cancels, and
+// the computed point lies within sqrt(r^2 + k*L^2) of the centre, L = |o - c|
+// (measured: k <= 4.4e-7, from L = 10 to 1e4). Spheres get that extra margin
+// with kSphereErr = 4e-6 and the largest L an accelerated origin can have.
 constexpr double kPadRel = 1e-3;
-constexpr double kMinSin2 = 1e-3;  // thinnest triangle bounded (sin^2 of its corner angle)
+constexpr double kMinSin2 = 1e-3;     // thinnest triangle bounded (sin^2 of its corner angle)
+constexpr double kSphereErr = 4e-6;   // k of the sphere-root error above, with room
+constexpr double kOriginRel = 4.0;    // origin_lim = kOriginRel * (scene magnitude + 1)
 
 Box3 finish(const BoxAcc& acc) { return acc.padded(kPadRel * (acc.extent() + acc.mag() + 1.0) + 1e-6); }
 
@@ -92,15 +102,18 @@ float area(const Box3& b) {
 enum { UNBOUNDED = 0, BOUNDED = 1, NEVER = 2 };
 
 // 0: no finite bound; 1: bounded; 2: the reference test never returns INNER.
-int classify(const FlatShape& s, Box3& out) {
+// origin_lim: largest |coordinate| of a ray origin the bound must hold for.
+int classify(const FlatShape& s, Box3& out, double origin_lim) {
     BoxAcc acc;
     switch (s.type) {
         case RT_SPHERE: {
             D3 c = d3(s.sphereCenter);
             double r = std::fabs(static_cast<double>(s.sphereRadius));
             if (!finite3(c) || !std::isfinite(r)) return UNBOUNDED;
-            acc.add(c - D3{r, r, r});
-            acc.add(c + D3{r, r, r});
+            const double L = std::sqrt(3.0) * origin_lim + std::sqrt(dot(c, c));
+            const double R = std::sqrt(r * r + kSphereErr * L * L);
+            acc.add(c - D3{R, R, R});
+            acc.add(c + D3{R, R, R});
             out = finish(acc);
             return BOUNDED;
         }
@@ -264,7 +277,6 @@ struct LocalBuilder {
 
 }  // namespace
 
-bool shape_bound(const FlatShape& s, Box3& b) { return classify(s, b) == BOUNDED; }
 
 namespace {
 
@@ -352,11 +364,14 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     std::vector<Box3> sbox(S);
     std::vector<int> scls(S);
     for (int i = 0; i < S; ++i) {
-        scls[i] = classify(shapes[i], sbox[i]);
+        scls[i] = classify(shapes[i], sbox[i], 0.0);
         if (scls[i] == BOUNDED)
             for (int a = 0; a < 3; ++a)
                 out.scene_mag = std::max({out.scene_mag, std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
     }
+    out.origin_lim = static_cast<float>(kOriginRel * (out.scene_mag + 1.0));
+    for (int i = 0; i < S; ++i)
+        if (shapes[i].type == RT_SPHERE) scls[i] = classify(shapes[i], sbox[i], out.origin_lim);
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).

@@ -50,11 +50,12 @@ struct AccelHost {
     // thr = -sin(angle + margin), or -4 (never culls).
     std::vector<float> lcone;     // 4 per local node: axis.xyz, thr
     int max_stack = 0;            // worst-case wave stack entries
-    // Largest |coordinate| of any bounded shape box. The padding is relative to
-    // the scene's coordinates; ray origins far outside (a camera more than 100x
-    // the scene's magnitude away) would need more, so the renderer then skips
-    // the accelerator for that frame (rt_kernels.hip, launch()).
-    float scene_mag = 0.f;
+    // Largest |coordinate| of any bounded shape box, and the largest |coordinate|
+    // of a ray origin the bounds are built for (kOriginRel * (scene_mag + 1)).
+    // Rays from farther away take the always-enter mode of the padded tests
+    // (accel_math.h); a camera farther away skips the accelerator for the
+    // frame (rt_kernels.hip, launch()).
+    float scene_mag = 0.f, origin_lim = 0.f;
     int always_prims = 0, bounded_prims = 0, local_leaves = 0;
 };
 
@@ -65,9 +66,5 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 
 // Back-face cones of the local nodes (fills A.lcone).
 void build_cones(const FlatShape* shapes, AccelHost& A);
-
-// Conservative bound of every INNER hit point of a shape (barycentric mode).
-// Returns false when no finite bound exists.
-bool shape_bound(const FlatShape& s, Box3& b);
 
 }  // namespace rta

@@ -89,8 +89,6 @@ struct KParams {
     int tiles_x, tiles;                      // 8x8 tiles per row, total
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane
     int lane_stack;                          // per-lane LDS stack entries
-    int lane_walk;                           // 1: node-at-pop walk, 2: while-while (lnodes2)
-    int tile_stride;                         // dispatch order -> image tile bijection
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).
@@ -226,6 +224,22 @@ __device__ __forceinline__ bool ray_aabb(V o, V inv, V bmin, V bmax) {
 }
 
 __device__ __forceinline__ V inv_dir(V d) { return mk(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+
+// ray_aabb with IEEE min/max (v_min3/v_max3). GLSL min/max differ from them
+// only on NaN operands (and the sign of an equal zero, which no comparison
+// sees), so the result is the same whenever no slab value can be NaN: finite
+// origin, finite non-zero reciprocals and NaN-free bounds (aabb_fast_ok).
+__device__ __forceinline__ bool ray_aabb_fast(V o, V inv, V bmin, V bmax) {
+    V t0 = mulv(bmin - o, inv), t1 = mulv(bmax - o, inv);
+    float tmin = fmaxf(fmaxf(fminf(t0.x, t1.x), fminf(t0.y, t1.y)), fminf(t0.z, t1.z));
+    float tmax = fminf(fminf(fmaxf(t0.x, t1.x), fmaxf(t0.y, t1.y)), fmaxf(t0.z, t1.z));
+    return tmax >= tmin && tmax > 0.0f;
+}
+__device__ __forceinline__ bool aabb_fast_ok(V o, V inv) {
+    const float big = 3.0e38f;
+    return fabsf(o.x) < big && fabsf(o.y) < big && fabsf(o.z) < big && fabsf(inv.x) < big &&
+           fabsf(inv.y) < big && fabsf(inv.z) < big && inv.x != 0.0f && inv.y != 0.0f && inv.z != 0.0f;
+}
 
 __device__ __forceinline__ GeoRec load_rec(const float4* __restrict__ base, int j) {
     GeoRec g;

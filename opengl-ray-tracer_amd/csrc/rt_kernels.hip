@@ -32,6 +32,7 @@
 
 #include "../../include/rt_api.h"
 #include "accel.h"
+#include "accel_math.h"
 #include "rt_device.h"
 
 using namespace rtd;
@@ -519,17 +520,17 @@ __global__ __launch_bounds__(kBlock) void k_packet(const float4* __restrict__ ge
 // k_packet.
 
 struct AccelPtrs {
-    const float4* __restrict__ anodes;  // 4 float4 per reference node
-    const float4* __restrict__ lnodes;  // 2 float4 per local node
+    const float4* __restrict__ anodes;  // 4 float4 per reference node (the root's entry test)
     const float4* __restrict__ prims;   // 5 float4 per prim, f[17] = rank
-    int N;
-    const float4* __restrict__ lnodes2; // 4 float4 per local inner node: both child boxes + codes
-    const int* __restrict__ lroot2;     // per reference node: local root as a child code, or kNoChild
-    const float4* __restrict__ anodes2; // 8 float4 per reference inner node: both children's exact + content boxes
+    const float4* __restrict__ lnodes;  // 6 float4 per local inner node: both child boxes + codes, cones
+    const float4* __restrict__ wnodes;  // 8 float4 per reference inner node: both children's exact + content boxes
     const int4* __restrict__ tleaf;     // per reference leaf: plain start, plain count, local root code
+    int N;
+    float origin_lim;                   // AccelHost::origin_lim
+    int boxes_finite;                   // no reference node box holds a NaN (ray_aabb_fast)
 };
 
-// Child codes of the per-lane walk's stack and of lnodes2 entries.
+// Child codes of the walks' stacks and of lnodes / wnodes entries.
 constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u, kTopLeaf = 0x20000000u;
 constexpr int kNoChild = 0x7fffffff;
 
@@ -539,8 +540,6 @@ struct Best {
     V p;
     int slot;
 };
-
-constexpr float kPruneRel = 1.002f;  // distance margin for skipping a box (accel.h)
 
 __device__ __forceinline__ bool lex_better(float d, int seq, const Best& b) {
     return d < b.d || (d == b.d && seq < b.seq);
@@ -636,428 +635,147 @@ __device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float 
     return true;
 }
 
-// Conservative slab test on a padded box: NaN-free (zero direction components
-// use a huge finite reciprocal), accepts iff the ray's forward part meets the
-// box no farther than `limp` (in distance units, dlen = |dir|).
-__device__ __forceinline__ bool padded_hit(V o, V invs, float dlen, float4 lo, float4 hi, float limp) {
-    float tx0 = (lo.x - o.x) * invs.x, tx1 = (hi.x - o.x) * invs.x;
-    float ty0 = (lo.y - o.y) * invs.y, ty1 = (hi.y - o.y) * invs.y;
-    float tz0 = (lo.z - o.z) * invs.z, tz1 = (hi.z - o.z) * invs.z;
-    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-    float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-    return tmax >= fmaxf(tmin, 0.0f) && tmin * dlen <= limp;
-}
-
-__device__ __forceinline__ bool padded_hit_t(V o, V invs, float dlen, float4 lo, float4 hi, float limp,
-                                             float& tentry) {
-    float tx0 = (lo.x - o.x) * invs.x, tx1 = (hi.x - o.x) * invs.x;
-    float ty0 = (lo.y - o.y) * invs.y, ty1 = (hi.y - o.y) * invs.y;
-    float tz0 = (lo.z - o.z) * invs.z, tz1 = (hi.z - o.z) * invs.z;
-    float tmin = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fminf(tz0, tz1));
-    float tmax = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fmaxf(tz0, tz1));
-    tentry = tmin;
-    return tmax >= fmaxf(tmin, 0.0f) && tmin * dlen <= limp;
-}
-
-__device__ __forceinline__ float safe_inv(float d) { return d == 0.0f ? copysignf(1e30f, d) : 1.0f / d; }
-
-__device__ __forceinline__ float axis_of(V v, int a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
-
-// Direction component of the first lane of `m` along `axis` (wave-uniform).
-__device__ __forceinline__ float rep_dir(V d, int axis, unsigned long long m) {
-    const int lane = __builtin_ctzll(m);
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(axis_of(d, axis)), lane));
-}
-
-// Diagnostics (TIMED k_accel only): per-lane node pops and primitive tests.
+// Diagnostics (TIMED k_accel only): per-lane node steps and primitive tests.
 struct WalkCount {
     unsigned nodes, tests;
 };
 
-template <bool SHADOW, bool COUNT = false>
-__device__ void accel_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
-                           bool& shadow, WalkCount& wc) {
-    const unsigned long long m0 = __ballot(active);
-    if (A.N <= 0 || m0 == 0) return;
-    const V inv = inv_dir(r.d);  // exact reciprocal: the reference box test
-    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
-    const float dlen = len(r.d);
-    WaveStack st{0, 0, 0, 0};
-    st.push(A.N - 1, m0);
-    unsigned long long done = 0;
-    while (st.sp > 0) {
-        int code;
-        unsigned long long m;
-        st.pop(code, m);
-        if (SHADOW) m &= ~done;
-        if (m == 0) continue;
-        code = uni(code);
-        if (COUNT && lane_in(m)) wc.nodes++;
-        const float lim = SHADOW ? lim_shadow : b.d;
-        const float limp = lim * kPruneRel + 1e-6f;
-        if (code >= 0) {
-            // reference node: exact box (which leaves the lane enters), then
-            // the conservative content box (distance pruning) when bounded
-            const float4* q = A.anodes + 4 * static_cast<size_t>(code);
-            const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
-            const int flags = uni(__float_as_int(c0.w));
-            bool hb = lane_in(m) && ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z));
-            if (flags & 8) hb = hb && padded_hit(r.o, invs, dlen, c0, c1, limp);
-            const unsigned long long mh = __ballot(hb);
-            if (mh == 0) continue;
-            const int ia = uni(__float_as_int(e0.w)), ib = uni(__float_as_int(e1.w));
-            if (ia < 0) {
-                const int start = -ia - 1;
-                bool live = hb;
-                for (int i = 0; i < ib; ++i) {
-                    const GeoRec g = load_rec(A.prims, start + i);
-                    if (live) {
-                        if (COUNT) wc.tests++;
-                        if (SHADOW) {
-                            if (try_shadow(g, r, lim_shadow)) {
-                                shadow = true;
-                                live = false;
-                            }
-                        } else {
-                            try_closest(g, start + i, r, b);
-                        }
-                    }
-                    if (SHADOW && __ballot(live) == 0) break;
-                }
-                const int lroot = uni(__float_as_int(c1.w));
-                unsigned long long ml = mh;
-                if (SHADOW) {
-                    done = __ballot(shadow);
-                    ml &= ~done;
-                }
-                if (lroot >= 0 && ml) st.push(-(lroot + 1), ml);
-            } else {
-                const int axis = flags & 3;
-                const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
-                const bool fwd = rep_dir(r.d, axis, mh) >= 0.0f;
-                st.push(fwd ? upper : lower, mh);  // far first, near popped next
-                st.push(fwd ? lower : upper, mh);
-            }
-        } else {
-            const int j = -code - 1;
-            const float4* q = A.lnodes + 2 * static_cast<size_t>(j);
-            const float4 lo = q[0], hi = q[1];
-            const bool hb = lane_in(m) && padded_hit(r.o, invs, dlen, lo, hi, limp);
-            const unsigned long long mh = __ballot(hb);
-            if (mh == 0) continue;
-            const int la = uni(__float_as_int(lo.w)), lb = uni(__float_as_int(hi.w));
-            if (la < 0) {
-                const int start = -la - 1;
-                bool live = hb;
-                for (int i = 0; i < lb; ++i) {
-                    const GeoRec g = load_rec(A.prims, start + i);
-                    if (live) {
-                        if (COUNT) wc.tests++;
-                        if (SHADOW) {
-                            if (try_shadow(g, r, lim_shadow)) {
-                                shadow = true;
-                                live = false;
-                            }
-                        } else {
-                            try_closest(g, start + i, r, b);
-                        }
-                    }
-                    if (SHADOW && __ballot(live) == 0) break;
-                }
-                if (SHADOW) {
-                    done = __ballot(shadow);
-                    if ((m0 & ~done) == 0) break;
-                }
-            } else {
-                const int axis = (lb >> 30) & 3, right = lb & 0x3fffffff;
-                const bool fwd = rep_dir(r.d, axis, mh) >= 0.0f;
-                st.push(-((fwd ? right : la) + 1), mh);  // local codes are negative
-                st.push(-((fwd ? la : right) + 1), mh);
-            }
-        }
-    }
-}
-
-// Per-lane variant of accel_walk: every lane walks its own stack (in LDS,
-// entry s of a lane at stk[s * stride]) with per-lane node loads. For
-// incoherent rays (reflections off curved surfaces) the packet walk visits
-// the union of all lanes' nodes; here a wave costs its longest lane. Same
-// visited-set / pruning / tie rules as accel_walk, so the same result.
-template <bool SHADOW, bool COUNT = false>
-__device__ void lane_accel_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
-                                bool& shadow, int* stk, int stride, int cap, WalkCount& wc) {
-    if (A.N <= 0 || !active) return;
-    const V inv = inv_dir(r.d);
-    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
-    const float dlen = len(r.d);
-    int sp = 0;
-    stk[0] = A.N - 1;
-    sp = 1;
-    while (sp > 0) {
-        const int code = stk[--sp * stride];
-        if (COUNT) wc.nodes++;
-        const float lim = SHADOW ? lim_shadow : b.d;
-        const float limp = lim * kPruneRel + 1e-6f;
-        int start = 0, count = 0;
-        if (code >= 0) {
-            const float4* q = A.anodes + 4 * static_cast<size_t>(code);
-            const float4 e0 = q[0], e1 = q[1];
-            if (!ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z))) continue;
-            const float4 c0 = q[2], c1 = q[3];
-            const int flags = __float_as_int(c0.w);
-            if ((flags & 8) && !padded_hit(r.o, invs, dlen, c0, c1, limp)) continue;
-            const int ia = __float_as_int(e0.w), ib = __float_as_int(e1.w);
-            if (ia < 0) {
-                start = -ia - 1;
-                count = ib;
-                const int lroot = __float_as_int(c1.w);
-                if (lroot >= 0 && sp < cap) stk[sp++ * stride] = -(lroot + 1);
-            } else {
-                const int axis = flags & 3;
-                const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
-                const bool fwd = axis_of(r.d, axis) >= 0.0f;
-                if (sp + 2 > cap) continue;  // unreachable: the host bounds the stack
-                stk[sp++ * stride] = fwd ? upper : lower;
-                stk[sp++ * stride] = fwd ? lower : upper;
-                continue;
-            }
-        } else {
-            const float4* q = A.lnodes + 2 * static_cast<size_t>(-code - 1);
-            const float4 lo = q[0], hi = q[1];
-            if (!padded_hit(r.o, invs, dlen, lo, hi, limp)) continue;
-            const int la = __float_as_int(lo.w), lb = __float_as_int(hi.w);
-            if (la < 0) {
-                start = -la - 1;
-                count = lb;
-            } else {
-                const int axis = (lb >> 30) & 3, right = lb & 0x3fffffff;
-                const bool fwd = axis_of(r.d, axis) >= 0.0f;
-                if (sp + 2 > cap) continue;
-                stk[sp++ * stride] = -((fwd ? right : la) + 1);
-                stk[sp++ * stride] = -((fwd ? la : right) + 1);
-                continue;
-            }
-        }
-        for (int i = 0; i < count; ++i) {
-            const GeoRec g = load_rec(A.prims, start + i);
-            if (COUNT) wc.tests++;
-            if (SHADOW) {
-                if (try_shadow(g, r, lim_shadow)) {
-                    shadow = true;
-                    return;
-                }
-            } else {
-                try_closest(g, start + i, r, b);
-            }
-        }
-    }
-}
-
-// Per-lane walk, second form ("while-while"): local BVH nodes hold both
-// child boxes, so a culled child costs no iteration, and far children carry
-// their entry distance on the stack (re-checked against the best hit when
-// popped). Each lane first walks until it holds a leaf, then all lanes test
-// their leaves together, so a lane's leaf scan no longer stalls the others'
-// node steps. Stack: code + entry distance per entry, in LDS.
-template <bool SHADOW, bool COUNT = false>
-__device__ void lane_walk2(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
-                           int* stk, float* stt, int stride, int cap, WalkCount& wc) {
-    if (A.N <= 0 || !active) return;
-    const V inv = inv_dir(r.d);
-    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
-    const float dlen = len(r.d);
-    int sp = 0;
-    int cur = A.N - 1;  // node in hand (kept in registers while descending)
-    bool have = true;
-    for (;;) {
-        int start = 0, count = 0;
-        while (count == 0) {
-            if (!have) {
-                if (sp == 0) break;
-                --sp;
-                const float te = stt[sp * stride];
-                const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
-                if (te * dlen > limp) continue;  // a nearer hit was found since the push
-                cur = stk[sp * stride];
-                have = true;
-            }
-            if (COUNT) wc.nodes++;
-            const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
-            const unsigned uc = static_cast<unsigned>(cur);
-            have = false;
-            if (!(uc & kLocal)) {
-                // reference node: the exact box test decides entry (gpu_shader.comp:395)
-                const float4* q = A.anodes + 4 * static_cast<size_t>(cur);
-                const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
-                if (!ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z))) continue;
-                const int flags = __float_as_int(c0.w);
-                if ((flags & 8) && !padded_hit(r.o, invs, dlen, c0, c1, limp)) continue;
-                const int ia = __float_as_int(e0.w), ib = __float_as_int(e1.w);
-                if (ia < 0) {
-                    start = -ia - 1;
-                    count = ib;
-                    const int lr = A.lroot2[cur];
-                    if (lr != kNoChild) {
-                        cur = lr;
-                        have = true;
-                    }
-                } else {
-                    const int axis = flags & 3;
-                    const int lower = (flags & 4) ? ib : ia, upper = (flags & 4) ? ia : ib;
-                    const bool fwd = axis_of(r.d, axis) >= 0.0f;
-                    if (sp < cap) {
-                        stk[sp * stride] = fwd ? upper : lower;
-                        stt[sp * stride] = -INFINITY;
-                        ++sp;
-                    }
-                    cur = fwd ? lower : upper;
-                    have = true;
-                }
-            } else if (uc & kLeaf) {
-                start = static_cast<int>((uc >> 8) & 0x3fffffu);
-                count = static_cast<int>(uc & 0xffu);
-            } else {
-                const float4* q = A.lnodes2 + 6 * static_cast<size_t>(uc & 0x3fffffffu);
-                const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
-                float ta, tb;
-                // box test, then the back-face cone: no INNER-capable normal below
-                const bool ha = padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta) &&
-                                !(dot(mk(ka.x, ka.y, ka.z), r.d) < ka.w * dlen);
-                const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
-                                !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
-                const int ca = __float_as_int(a0.w), cb = __float_as_int(a1.w);
-                if (ha && hb) {
-                    const bool a_first = !(tb < ta);  // nearer entry first
-                    if (sp < cap) {
-                        stk[sp * stride] = a_first ? cb : ca;
-                        stt[sp * stride] = a_first ? tb : ta;
-                        ++sp;
-                    }
-                    cur = a_first ? ca : cb;
-                    have = true;
-                } else if (ha || hb) {
-                    cur = ha ? ca : cb;
-                    have = true;
-                }
-            }
-        }
-        if (count == 0) return;  // walk finished
-        for (int i = 0; i < count; ++i) {
-            const GeoRec g = load_rec(A.prims, start + i);
-            if (COUNT) wc.tests++;
-            if (SHADOW) {
-                if (try_shadow(g, r, lim_shadow)) {
-                    shadow = true;
-                    return;
-                }
-            } else {
-                try_closest(g, start + i, r, b);
-            }
-        }
-    }
-}
-
-// Per-lane walk, third form: lane_walk2 plus wide reference nodes. An inner
-// reference node holds both children's exact boxes (the reference's entry
-// test, evaluated at the parent: same boxes, same arithmetic, same result)
-// and their conservative content boxes, so a child the lane does not enter
-// costs no iteration and children are ordered by their entry distance.
-// Codes: reference inner node k; kTopLeaf|k reference leaf; kLocal|j local
-// inner node; kLocal|kLeaf|start<<8|count local leaf.
+// Codes of the walk: a reference inner node k; kTopLeaf|k a reference leaf;
+// kLocal|j a local inner node; kLocal|kLeaf|start<<8|count a local leaf.
 __device__ __forceinline__ int top_code(int k, int ia) { return ia < 0 ? static_cast<int>(kTopLeaf | k) : k; }
 
+__device__ __forceinline__ rta::RayC ray_c(const Ray& r, float origin_lim) {
+    return rta::ray_consts(r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, origin_lim);
+}
+
+__device__ __forceinline__ bool box_enter(const rta::RayC& c, float4 lo, float4 hi, float tl, float& te) {
+    return rta::box_enter(c, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, tl, te);
+}
+
+__device__ __forceinline__ bool cone_ok(const rta::RayC& c, float4 k) {
+    return !rta::cone_culls(c, k.x, k.y, k.z, k.w);
+}
+
+// The root has no parent: its own exact box decides entry (gpu_shader.comp:386-395),
+// then its content box.
+__device__ __forceinline__ bool enter_root(const AccelPtrs& A, const Ray& r, const V& inv, const rta::RayC& c,
+                                           float tl, int& code) {
+    const float4* q = A.anodes + 4 * static_cast<size_t>(A.N - 1);
+    const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
+    float te;
+    code = top_code(A.N - 1, __float_as_int(e0.w));
+    return ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z)) &&
+           (!(__float_as_int(c0.w) & 8) || box_enter(c, c0, c1, tl, te));
+}
+
+// Both children of a node in hand: which the lane enters and at what parameter.
+// Reference inner node: the children's exact boxes with the GLSL test (the
+// reference's own entry decision, evaluated at the parent), then their content
+// boxes. Local inner node: padded child boxes and back-face cones.
+struct Kids {
+    int ca, cb;
+    float ta, tb;
+    bool ha, hb;
+};
+
+__device__ __forceinline__ Kids ref_kids(const AccelPtrs& A, unsigned uc, const Ray& r, const V& inv,
+                                         const rta::RayC& c, float tl, bool in, bool fast) {
+    const float4* q = A.wnodes + 8 * static_cast<size_t>(uc);
+    const float4 ae0 = q[0], ae1 = q[1], ac0 = q[2], ac1 = q[3];
+    const float4 be0 = q[4], be1 = q[5], bc0 = q[6], bc1 = q[7];
+    Kids k;
+    bool ea, eb;
+    if (fast) {
+        ea = ray_aabb_fast(r.o, inv, mk(ae0.x, ae0.y, ae0.z), mk(ae1.x, ae1.y, ae1.z));
+        eb = ray_aabb_fast(r.o, inv, mk(be0.x, be0.y, be0.z), mk(be1.x, be1.y, be1.z));
+    } else {
+        ea = ray_aabb(r.o, inv, mk(ae0.x, ae0.y, ae0.z), mk(ae1.x, ae1.y, ae1.z));
+        eb = ray_aabb(r.o, inv, mk(be0.x, be0.y, be0.z), mk(be1.x, be1.y, be1.z));
+    }
+    // content boxes evaluated unconditionally (no branch between the loads and their use)
+    float ta, tb;
+    const bool pa = box_enter(c, ac0, ac1, tl, ta), pb = box_enter(c, bc0, bc1, tl, tb);
+    const bool fa = (__float_as_int(ac0.w) & 8) != 0, fb = (__float_as_int(bc0.w) & 8) != 0;
+    k.ha = in & ea & (pa | !fa);
+    k.hb = in & eb & (pb | !fb);
+    k.ta = fa ? ta : 0.f;
+    k.tb = fb ? tb : 0.f;
+    k.ca = __float_as_int(ae0.w);
+    k.cb = __float_as_int(ae1.w);
+    return k;
+}
+
+__device__ __forceinline__ Kids local_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
+    const float4* q = A.lnodes + 6 * static_cast<size_t>(uc & 0x3fffffffu);
+    const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
+    Kids k;
+    const bool ba = box_enter(c, a0, a1, tl, k.ta), bb = box_enter(c, b0, b1, tl, k.tb);
+    k.ha = in & ba & cone_ok(c, ka);
+    k.hb = in & bb & cone_ok(c, kb);
+    k.ca = __float_as_int(a0.w);
+    k.cb = __float_as_int(a1.w);
+    return k;
+}
+
+// Per-lane walk ("while-while"): each lane walks its own stack in LDS (code +
+// entry parameter per entry). A lane descends until it holds a leaf, keeping
+// the nearer child in registers and stacking the farther one; the wave then
+// tests all lanes' leaves together. A stacked entry is dropped on pop when a
+// nearer hit has been found since it was pushed.
 template <bool SHADOW, bool COUNT = false>
-__device__ void lane_walk3(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
-                           int* stk, float* stt, int stride, int cap, WalkCount& wc) {
+__device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
+                          int* stk, float* stt, int stride, int cap, WalkCount& wc) {
     if (A.N <= 0 || !active) return;
     const V inv = inv_dir(r.d);
-    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
-    const float dlen = len(r.d);
+    const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
+    const rta::RayC c = ray_c(r, A.origin_lim);
+    float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
     int sp = 0, cur = 0;
-    bool have = false;
-    {
-        // the root has no parent: its own exact box decides (gpu_shader.comp:386-395)
-        const float4* q = A.anodes + 4 * static_cast<size_t>(A.N - 1);
-        const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
-        const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
-        if (ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z)) &&
-            (!(__float_as_int(c0.w) & 8) || padded_hit(r.o, invs, dlen, c0, c1, limp))) {
-            cur = top_code(A.N - 1, __float_as_int(e0.w));
-            have = true;
-        }
-    }
+    bool have = enter_root(A, r, inv, c, tl, cur);
     for (;;) {
         int start = 0, count = 0;
         while (count == 0) {
             if (!have) {
                 if (sp == 0) break;
                 --sp;
-                const float te = stt[sp * stride];
-                const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
-                if (te * dlen > limp) continue;  // a nearer hit was found since the push
+                if (stt[sp * stride] > tl) continue;  // a nearer hit was found since the push
                 cur = stk[sp * stride];
                 have = true;
             }
             if (COUNT) wc.nodes++;
-            const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
             const unsigned uc = static_cast<unsigned>(cur);
             have = false;
-            if (!(uc & (kLocal | kTopLeaf))) {
-                const float4* q = A.anodes2 + 8 * static_cast<size_t>(uc);
-                const float4 ae0 = q[0], ae1 = q[1], ac0 = q[2], ac1 = q[3];
-                const float4 be0 = q[4], be1 = q[5], bc0 = q[6], bc1 = q[7];
-                float ta = -INFINITY, tb = -INFINITY;
-                bool ha = ray_aabb(r.o, inv, mk(ae0.x, ae0.y, ae0.z), mk(ae1.x, ae1.y, ae1.z));
-                bool hb = ray_aabb(r.o, inv, mk(be0.x, be0.y, be0.z), mk(be1.x, be1.y, be1.z));
-                if (ha && (__float_as_int(ac0.w) & 8)) ha = padded_hit_t(r.o, invs, dlen, ac0, ac1, limp, ta);
-                if (hb && (__float_as_int(bc0.w) & 8)) hb = padded_hit_t(r.o, invs, dlen, bc0, bc1, limp, tb);
-                const int ca = __float_as_int(ae0.w), cb = __float_as_int(ae1.w);
-                if (ha && hb) {
-                    const bool a_first = !(tb < ta);
-                    if (sp < cap) {
-                        stk[sp * stride] = a_first ? cb : ca;
-                        stt[sp * stride] = a_first ? tb : ta;
-                        ++sp;
-                    }
-                    cur = a_first ? ca : cb;
-                    have = true;
-                } else if (ha || hb) {
-                    cur = ha ? ca : cb;
-                    have = true;
-                }
-            } else if (uc & kTopLeaf) {
+            Kids k;
+            if (uc & kTopLeaf) {
                 const int4 lf = A.tleaf[uc & 0x1fffffffu];
                 start = lf.x;
                 count = lf.y;
                 if (lf.z != kNoChild) {
-                    cur = lf.z;
+                    cur = lf.z;  // local root: entered with the leaf
                     have = true;
                 }
+                continue;
             } else if (uc & kLeaf) {
                 start = static_cast<int>((uc >> 8) & 0x3fffffu);
                 count = static_cast<int>(uc & 0xffu);
+                continue;
+            } else if (uc & kLocal) {
+                k = local_kids(A, uc, c, tl, true);
             } else {
-                const float4* q = A.lnodes2 + 6 * static_cast<size_t>(uc & 0x3fffffffu);
-                const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
-                float ta, tb;
-                const bool ha = padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta) &&
-                                !(dot(mk(ka.x, ka.y, ka.z), r.d) < ka.w * dlen);
-                const bool hb = padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
-                                !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
-                const int ca = __float_as_int(a0.w), cb = __float_as_int(a1.w);
-                if (ha && hb) {
-                    const bool a_first = !(tb < ta);
-                    if (sp < cap) {
-                        stk[sp * stride] = a_first ? cb : ca;
-                        stt[sp * stride] = a_first ? tb : ta;
-                        ++sp;
-                    }
-                    cur = a_first ? ca : cb;
-                    have = true;
-                } else if (ha || hb) {
-                    cur = ha ? ca : cb;
-                    have = true;
+                k = ref_kids(A, uc, r, inv, c, tl, true, fast);
+            }
+            if (k.ha && k.hb) {
+                const bool a_first = !(k.tb < k.ta);  // nearer entry first
+                if (sp < cap) {
+                    stk[sp * stride] = a_first ? k.cb : k.ca;
+                    stt[sp * stride] = a_first ? k.tb : k.ta;
+                    ++sp;
                 }
+                cur = a_first ? k.ca : k.cb;
+                have = true;
+            } else if (k.ha || k.hb) {
+                cur = k.ha ? k.ca : k.cb;
+                have = true;
             }
         }
         if (count == 0) return;  // walk finished
@@ -1073,32 +791,30 @@ __device__ void lane_walk3(const AccelPtrs& A, const Ray& r, bool active, float 
                 try_closest(g, start + i, r, b);
             }
         }
+        if (!SHADOW) tl = rta::t_limit(b.d, c.rdl);
     }
 }
 
-// Packet form of lane_walk3: one wave-uniform walk with a 64-bit lane mask
-// per stack entry (VGPR-resident stack, scalar node loads), using the wide
-// reference nodes and the local child-box nodes with back-face cones. The
-// node in hand stays in scalar registers while descending; children are
-// tested at the parent for every lane of the mask.
+// Packet walk: one wave-uniform walk with a 64-bit lane mask per stack entry
+// (VGPR-resident stack, scalar node loads). The reference's walk order does
+// not depend on the ray, so one walk with masks reproduces every lane's own;
+// the order among children follows the first lane that enters both.
 template <bool SHADOW, bool COUNT = false>
-__device__ void packet_walk3(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
-                             bool& shadow, WalkCount& wc) {
+__device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
+                            bool& shadow, WalkCount& wc) {
     unsigned long long m = __ballot(active);
     if (A.N <= 0 || m == 0) return;
     const V inv = inv_dir(r.d);
-    const V invs = mk(safe_inv(r.d.x), safe_inv(r.d.y), safe_inv(r.d.z));
-    const float dlen = len(r.d);
+    const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
+    const rta::RayC c = ray_c(r, A.origin_lim);
+    float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
     WaveStack st{0, 0, 0, 0};
     int cur = 0;
     {
-        const float4* q = A.anodes + 4 * static_cast<size_t>(A.N - 1);
-        const float4 e0 = q[0], e1 = q[1], c0 = q[2], c1 = q[3];
-        const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
-        const bool h = active && ray_aabb(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z)) &&
-                       (!(__float_as_int(c0.w) & 8) || padded_hit(r.o, invs, dlen, c0, c1, limp));
+        int code = 0;
+        const bool h = enter_root(A, r, inv, c, tl, code) && active;  // code is the same in every lane
         m = __ballot(h);
-        cur = top_code(A.N - 1, __float_as_int(e0.w));
+        cur = uni(code);
     }
     unsigned long long done = 0;
     for (;;) {
@@ -1110,48 +826,29 @@ __device__ void packet_walk3(const AccelPtrs& A, const Ray& r, bool active, floa
             continue;
         }
         if (COUNT && lane_in(m)) wc.nodes++;
-        const float limp = (SHADOW ? lim_shadow : b.d) * kPruneRel + 1e-6f;
         const unsigned uc = static_cast<unsigned>(cur);
-        bool ha = false, hb = false;
-        float ta = -INFINITY, tb = -INFINITY;
-        int ca = 0, cb = 0, start = 0, count = 0;
-        unsigned long long leaf_m = 0;
-        if (!(uc & (kLocal | kTopLeaf))) {
-            const float4* q = A.anodes2 + 8 * static_cast<size_t>(uc);
-            const float4 ae0 = q[0], ae1 = q[1], ac0 = q[2], ac1 = q[3];
-            const float4 be0 = q[4], be1 = q[5], bc0 = q[6], bc1 = q[7];
-            const bool in = lane_in(m);
-            ha = in && ray_aabb(r.o, inv, mk(ae0.x, ae0.y, ae0.z), mk(ae1.x, ae1.y, ae1.z));
-            hb = in && ray_aabb(r.o, inv, mk(be0.x, be0.y, be0.z), mk(be1.x, be1.y, be1.z));
-            if (ha && (__float_as_int(ac0.w) & 8)) ha = padded_hit_t(r.o, invs, dlen, ac0, ac1, limp, ta);
-            if (hb && (__float_as_int(bc0.w) & 8)) hb = padded_hit_t(r.o, invs, dlen, bc0, bc1, limp, tb);
-            ca = uni(__float_as_int(ae0.w));
-            cb = uni(__float_as_int(ae1.w));
-        } else if (uc & kTopLeaf) {
+        Kids k{0, 0, 0.f, 0.f, false, false};
+        int start = 0, count = 0;
+        if (uc & kTopLeaf) {
             const int4 lf = A.tleaf[uc & 0x1fffffffu];
             start = uni(lf.x);
             count = uni(lf.y);
-            leaf_m = m;
-            const int lr = uni(lf.z);
-            ca = lr;
-            ha = (lr != kNoChild) && lane_in(m);  // local root: entered with the leaf
+            k.ca = uni(lf.z);
+            k.ha = (k.ca != kNoChild) && lane_in(m);  // local root: entered with the leaf
         } else if (uc & kLeaf) {
             start = static_cast<int>((uc >> 8) & 0x3fffffu);
             count = static_cast<int>(uc & 0xffu);
-            leaf_m = m;
+        } else if (uc & kLocal) {
+            k = local_kids(A, uc, c, tl, lane_in(m));
+            k.ca = uni(k.ca);
+            k.cb = uni(k.cb);
         } else {
-            const float4* q = A.lnodes2 + 6 * static_cast<size_t>(uc & 0x3fffffffu);
-            const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
-            const bool in = lane_in(m);
-            ha = in && padded_hit_t(r.o, invs, dlen, a0, a1, limp, ta) &&
-                 !(dot(mk(ka.x, ka.y, ka.z), r.d) < ka.w * dlen);
-            hb = in && padded_hit_t(r.o, invs, dlen, b0, b1, limp, tb) &&
-                 !(dot(mk(kb.x, kb.y, kb.z), r.d) < kb.w * dlen);
-            ca = uni(__float_as_int(a0.w));
-            cb = uni(__float_as_int(a1.w));
+            k = ref_kids(A, uc, r, inv, c, tl, lane_in(m), fast);
+            k.ca = uni(k.ca);
+            k.cb = uni(k.cb);
         }
         if (count > 0) {
-            bool live = lane_in(leaf_m);
+            bool live = lane_in(m);
             for (int i = 0; i < count; ++i) {
                 const GeoRec g = load_rec(A.prims, start + i);
                 if (live) {
@@ -1169,24 +866,26 @@ __device__ void packet_walk3(const AccelPtrs& A, const Ray& r, bool active, floa
             }
             if (SHADOW) {
                 done = __ballot(shadow);
-                if (ha && shadow) ha = false;
+                if (k.ha && shadow) k.ha = false;
+            } else {
+                tl = rta::t_limit(b.d, c.rdl);
             }
         }
-        const unsigned long long ma = __ballot(ha), mb = __ballot(hb);
+        const unsigned long long ma = __ballot(k.ha), mb = __ballot(k.hb);
         if (ma && mb) {
             // near first for the wave: the child the first lane of both masks enters sooner
             const int rep = __builtin_ctzll(ma & mb ? (ma & mb) : ma);
-            const float ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ta), rep));
-            const float rb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tb), rep));
+            const float ra = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(k.ta), rep));
+            const float rb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(k.tb), rep));
             const bool a_first = !(rb < ra);
-            if (st.sp < kMaxStack) st.push(a_first ? cb : ca, a_first ? mb : ma);
-            cur = a_first ? ca : cb;
+            if (st.sp < kMaxStack) st.push(a_first ? k.cb : k.ca, a_first ? mb : ma);
+            cur = a_first ? k.ca : k.cb;
             m = a_first ? ma : mb;
         } else if (ma) {
-            cur = ca;
+            cur = k.ca;
             m = ma;
         } else if (mb) {
-            cur = cb;
+            cur = k.cb;
             m = mb;
         } else {
             m = 0;
@@ -1214,23 +913,16 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     Ray ray = primary_ray(kp, pc.x, pc.y);
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
     bool alive = pc.active;
+    float* stt = reinterpret_cast<float*>(stk) + static_cast<size_t>(cap) * blockDim.x;
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
         bool unused = false;
         const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
-        if (lane_mode && kp.lane_walk == 3)
-            lane_walk3<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, reinterpret_cast<float*>(stk) +
-                                     static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
-        else if (lane_mode && kp.lane_walk == 2)
-            lane_walk2<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, reinterpret_cast<float*>(stk) +
-                                     static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
-        else if (lane_mode)
-            lane_accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, blockDim.x, cap, wc);
-        else if (kp.lane_walk == 3)
-            packet_walk3<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+        if (lane_mode)
+            lane_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
         else
-            accel_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+            packet_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
         if (alive && best.slot < 0) {
             acc = acc + mulv(att, bg);
             alive = false;
@@ -1248,18 +940,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         }
         bool shadow = false;
         Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
-        if (lane_mode && kp.lane_walk == 3)
-            lane_walk3<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, reinterpret_cast<float*>(stk) +
-                                    static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
-        else if (lane_mode && kp.lane_walk == 2)
-            lane_walk2<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, reinterpret_cast<float*>(stk) +
-                                    static_cast<size_t>(cap) * blockDim.x, blockDim.x, cap, wc);
-        else if (lane_mode)
-            lane_accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, blockDim.x, cap, wc);
-        else if (kp.lane_walk == 3)
-            packet_walk3<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+        if (lane_mode)
+            lane_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
         else
-            accel_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+            packet_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
     }
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
@@ -1267,17 +951,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 
 // PERSISTENT: each wave pulls tiles from one device counter until none is
 // left (every wave reaches the exit); otherwise one tile per wave. TIMED
-// writes each tile's start/end wall clock (diagnostics only).
+// writes each tile's start/end wall clock and walk counts (diagnostics only).
 template <bool PERSISTENT, bool TIMED>
-__global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ anodes,
-                                                  const float4* __restrict__ lnodes,
-                                                  const float4* __restrict__ prims,
-                                                  const float4* __restrict__ mat,
-                                                  const float4* __restrict__ lnodes2,
-                                                  const int* __restrict__ lroot2,
-                                                  const float4* __restrict__ anodes2,
-                                                  const int4* __restrict__ tleaf, KParams kp) {
-    const AccelPtrs A{anodes, lnodes, prims, kp.N, lnodes2, lroot2, anodes2, tleaf};
+__global__ __launch_bounds__(kBlock) void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
     int* stk = lds_stack + threadIdx.x;
     const int lane = threadIdx.x & 63;
@@ -1291,12 +967,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
         WalkCount wc{0u, 0u};
-        // Scatter the dispatch order over the image: expensive tiles cluster in
-        // space, and tiles dispatched together share CUs (a bijection: stride
-        // coprime with the tile count).
-        const int img_tile = static_cast<int>((static_cast<unsigned long long>(tile) * kp.tile_stride) %
-                                              static_cast<unsigned long long>(kp.tiles));
-        accel_tile<TIMED>(A, mat, kp, img_tile, stk, kp.lane_stack, wc);
+        accel_tile<TIMED>(A, mat, kp, tile, stk, kp.lane_stack, wc);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1307,7 +978,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(const float4* __restrict__ ano
                 mt = max(mt, __shfl_xor(mt, off));
             }
             if (lane == 0) {
-                unsigned long long* o = kp.tile_times + 6 * static_cast<size_t>(img_tile);
+                unsigned long long* o = kp.tile_times + 6 * static_cast<size_t>(tile);
                 o[0] = t0;
                 o[1] = t1;
                 o[2] = sn;
@@ -1363,10 +1034,12 @@ struct rt_ctx {
     size_t staging_idx_cap = 0;
     std::vector<int> host_idx;
     std::vector<FlatShape> host_shapes;
-    // exact-result accelerator (accel.h)
-    float4 *anodes = nullptr, *lnodes = nullptr, *prims = nullptr;
+    // exact-result accelerator (accel.h); device copies in the layouts of AccelPtrs
+    float4 *anodes = nullptr, *lnodes = nullptr, *wnodes = nullptr, *prims = nullptr;
+    int4* tleaf = nullptr;
     int* prim_idx_dev = nullptr;
     bool accel_ok = false;
+    int boxes_finite = 0;
     rta::AccelHost accel;
     // frame constants
     FlatCamera cam{};
@@ -1382,13 +1055,7 @@ struct rt_ctx {
     // launch shape of k_accel (rt_set_launch)
     int waves_per_block = 1, persistent = 0, cu_count = 256;
     int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
-    int lane_walk = 3;        // 1: node-at-pop, 2: while-while + local child boxes, 3: + wide reference nodes
-    float4* lnodes2 = nullptr;
-    int* lroot2 = nullptr;
-    float4* anodes2 = nullptr;
-    int4* tleaf = nullptr;
     int cone_cull = 1;
-    int scatter_tiles = 0;
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
@@ -1419,25 +1086,26 @@ int ensure_staging(T*& p, size_t& cap, size_t n) {
     return RT_OK;
 }
 
+void free_accel(rt_ctx* c) {
+    hipFree(c->anodes);
+    hipFree(c->lnodes);
+    hipFree(c->wnodes);
+    hipFree(c->tleaf);
+    hipFree(c->prims);
+    hipFree(c->prim_idx_dev);
+    c->anodes = c->lnodes = c->wnodes = c->prims = nullptr;
+    c->tleaf = nullptr;
+    c->prim_idx_dev = nullptr;
+    c->accel_ok = false;
+}
+
 void free_scene(rt_ctx* c) {
     hipFree(c->geo_lin);
     hipFree(c->geo_leaf);
     hipFree(c->mat);
     hipFree(c->nodes);
     c->geo_lin = c->geo_leaf = c->mat = c->nodes = nullptr;
-    hipFree(c->anodes);
-    hipFree(c->lnodes);
-    hipFree(c->prims);
-    hipFree(c->prim_idx_dev);
-    hipFree(c->lnodes2);
-    hipFree(c->lroot2);
-    hipFree(c->anodes2);
-    hipFree(c->tleaf);
-    c->anodes = c->lnodes = c->prims = c->lnodes2 = c->anodes2 = nullptr;
-    c->lroot2 = nullptr;
-    c->tleaf = nullptr;
-    c->prim_idx_dev = nullptr;
-    c->accel_ok = false;
+    free_accel(c);
     c->have_scene = false;
 }
 
@@ -1485,108 +1153,86 @@ inline float bits_f(int v) {
 // expects geo_lin to be packed (k_pack_prims copies from it). On failure the
 // context keeps rendering with k_packet.
 int upload_accel(rt_ctx* c) {
-    hipFree(c->anodes);
-    hipFree(c->lnodes);
-    hipFree(c->prims);
-    hipFree(c->prim_idx_dev);
-    hipFree(c->lnodes2);
-    hipFree(c->lroot2);
-    hipFree(c->anodes2);
-    hipFree(c->tleaf);
-    c->lnodes2 = c->anodes2 = nullptr;
-    c->lroot2 = nullptr;
-    c->tleaf = nullptr;
-    c->anodes = c->lnodes = c->prims = nullptr;
-    c->prim_idx_dev = nullptr;
-    c->accel_ok = false;
+    free_accel(c);
     const int N = c->N;
     if (N == 0) return RT_OK;
     rta::AccelHost& A = c->accel;
     if (!rta::build_accel(c->host_shapes.data(), c->S, c->host_nodes.data(), N, c->host_idx.data(), c->I,
                           kLeafScan, kMaxStack, A))
         return RT_OK;
+    if (N >= (1 << 29)) return RT_OK;  // codes carry the node index in 29 bits
+    c->boxes_finite = 1;
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& n = c->host_nodes[k];
+        for (float v : {n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, n.boundsMax.x, n.boundsMax.y, n.boundsMax.z})
+            if (std::isnan(v)) c->boxes_finite = 0;
+    }
+    // anodes: every reference node's exact box and content box (the root's entry test).
     std::vector<float4> an(4 * static_cast<size_t>(N));
     for (int k = 0; k < N; ++k) {
         const FlatNode& n = c->host_nodes[k];
-        int a, b;
-        if (n.leftChild == -1) {
-            a = -(A.plain_start[k] + 1);
-            b = A.plain_count[k];
-        } else {
-            a = n.leftChild;
-            b = n.rightChild;
-        }
         const rta::Box3& cb = A.content[k];
-        an[4 * k + 0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(a));
-        an[4 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(b));
+        an[4 * k + 0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(n.leftChild));
+        an[4 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(n.rightChild));
         an[4 * k + 2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[k]));
-        an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], bits_f(A.local_root[k]));
+        an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
     }
+    // lnodes: local inner nodes only, each with both child boxes, child codes
+    // (leaf: kLocal|kLeaf|start<<8|count, inner: kLocal|id) and back-face cones.
     const size_t M = A.lbox.size(), P = A.prim_shape.size();
-    std::vector<float4> ln(2 * (M ? M : 1));
-    for (size_t j = 0; j < M; ++j) {
-        const rta::Box3& bx = A.lbox[j];
-        ln[2 * j] = make_float4(bx.lo[0], bx.lo[1], bx.lo[2], bits_f(A.la[j]));
-        ln[2 * j + 1] = make_float4(bx.hi[0], bx.hi[1], bx.hi[2], bits_f(A.lb[j]));
-    }
-    // Second local layout (lane_walk2): inner nodes only, each with both child
-    // boxes and child codes (leaf: kLocal|kLeaf|start<<8|count, inner: kLocal|id).
     std::vector<int> inner_id(M, -1);
     int n_inner = 0;
     for (size_t j = 0; j < M; ++j)
         if (A.la[j] >= 0) inner_id[j] = n_inner++;
-    bool layout2 = true;
+    bool codes_ok = true;
     auto code_of = [&](size_t j) -> int {
         if (A.la[j] < 0) {
             const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
-            if (st >= (1u << 22) || cnt > 255u) layout2 = false;
+            if (st >= (1u << 22) || cnt > 255u) codes_ok = false;
             return static_cast<int>(kLocal | kLeaf | (st << 8) | cnt);
         }
         return static_cast<int>(kLocal | static_cast<unsigned>(inner_id[j]));
     };
-    std::vector<float4> ln2(6 * static_cast<size_t>(n_inner ? n_inner : 1));
+    std::vector<float4> ln(6 * static_cast<size_t>(n_inner ? n_inner : 1));
     for (size_t j = 0; j < M; ++j) {
         if (A.la[j] < 0) continue;
         const size_t l = static_cast<size_t>(A.la[j]), r = static_cast<size_t>(A.lb[j] & 0x3fffffff);
         const rta::Box3 &bl = A.lbox[l], &br = A.lbox[r];
-        float4* q = &ln2[6 * static_cast<size_t>(inner_id[j])];
+        float4* q = &ln[6 * static_cast<size_t>(inner_id[j])];
         q[0] = make_float4(bl.lo[0], bl.lo[1], bl.lo[2], bits_f(code_of(l)));
         q[1] = make_float4(bl.hi[0], bl.hi[1], bl.hi[2], bits_f(code_of(r)));
-        q[2] = make_float4(br.lo[0], br.lo[1], br.lo[2], bits_f((A.lb[j] >> 30) & 3));
+        q[2] = make_float4(br.lo[0], br.lo[1], br.lo[2], 0.f);
         q[3] = make_float4(br.hi[0], br.hi[1], br.hi[2], 0.f);
         const float *cl = &A.lcone[4 * l], *cr = &A.lcone[4 * r];
         q[4] = make_float4(cl[0], cl[1], cl[2], c->cone_cull ? cl[3] : -4.f);
         q[5] = make_float4(cr[0], cr[1], cr[2], c->cone_cull ? cr[3] : -4.f);
     }
-    std::vector<int> lr2(N, kNoChild);
-    for (int k = 0; k < N; ++k)
-        if (A.local_root[k] >= 0) lr2[k] = code_of(static_cast<size_t>(A.local_root[k]));
-    // Wide reference nodes (lane_walk3): both children's exact + content boxes.
-    std::vector<float4> an2(8 * static_cast<size_t>(N));
+    // wnodes: per reference inner node both children's exact + content boxes;
+    // tleaf: per reference leaf its plain range and local root code.
+    std::vector<float4> wn(8 * static_cast<size_t>(N));
     std::vector<int4> tl(static_cast<size_t>(N), make_int4(0, 0, kNoChild, 0));
-    bool wide_ok = N < (1 << 29);
-    for (int k = 0; k < N && wide_ok; ++k) {
+    auto top_code_of = [&](int k) {
+        return c->host_nodes[k].leftChild == -1 ? static_cast<int>(kTopLeaf | static_cast<unsigned>(k)) : k;
+    };
+    for (int k = 0; k < N; ++k) {
         const FlatNode& n = c->host_nodes[k];
         if (n.leftChild == -1) {
-            tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr2[k], 0);
+            const int lr = A.local_root[k] >= 0 ? code_of(static_cast<size_t>(A.local_root[k])) : kNoChild;
+            tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr, 0);
             continue;
         }
         const int ch[2] = {n.leftChild, n.rightChild};
         for (int s2 = 0; s2 < 2; ++s2) {
             const FlatNode& cn = c->host_nodes[ch[s2]];
             const rta::Box3& cb = A.content[ch[s2]];
-            const int code = cn.leftChild == -1 ? static_cast<int>(kTopLeaf | static_cast<unsigned>(ch[s2])) : ch[s2];
-            float4* q = &an2[8 * static_cast<size_t>(k) + 4 * s2];
-            q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, bits_f(s2 == 0 ? code : 0));
-            q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, 0.f);
+            float4* q = &wn[8 * static_cast<size_t>(k) + 4 * s2];
+            q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, s2 == 0 ? bits_f(top_code_of(ch[0])) : 0.f);
+            q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, s2 == 0 ? bits_f(top_code_of(ch[1])) : 0.f);
             q[2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[ch[s2]] & 8));
             q[3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
         }
-        // child B's code lives in q[1].w of child A (the layout read by lane_walk3)
-        const FlatNode& cnb = c->host_nodes[ch[1]];
-        an2[8 * static_cast<size_t>(k) + 1].w =
-            bits_f(cnb.leftChild == -1 ? static_cast<int>(kTopLeaf | static_cast<unsigned>(ch[1])) : ch[1]);
     }
+    if (!codes_ok) return RT_OK;
     std::vector<int> ps(2 * (P ? P : 1));
     for (size_t i = 0; i < P; ++i) {
         ps[i] = A.prim_shape[i];
@@ -1594,26 +1240,16 @@ int upload_accel(rt_ctx* c) {
     }
     if (hipMalloc(&c->anodes, an.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->lnodes, ln.size() * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->wnodes, wn.size() * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->tleaf, tl.size() * sizeof(int4)) != hipSuccess ||
         hipMalloc(&c->prims, 5 * (P ? P : 1) * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->prim_idx_dev, ps.size() * sizeof(int)) != hipSuccess)
         return RT_ERR_NO_MEMORY;
     HIP_TRY(hipMemcpyAsync(c->anodes, an.data(), an.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->lnodes, ln.data(), ln.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->tleaf, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->prim_idx_dev, ps.data(), ps.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    if (layout2 && wide_ok) {
-        if (hipMalloc(&c->anodes2, an2.size() * sizeof(float4)) != hipSuccess ||
-            hipMalloc(&c->tleaf, tl.size() * sizeof(int4)) != hipSuccess)
-            return RT_ERR_NO_MEMORY;
-        HIP_TRY(hipMemcpyAsync(c->anodes2, an2.data(), an2.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->tleaf, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
-    }
-    if (layout2) {
-        if (hipMalloc(&c->lnodes2, ln2.size() * sizeof(float4)) != hipSuccess ||
-            hipMalloc(&c->lroot2, lr2.size() * sizeof(int)) != hipSuccess)
-            return RT_ERR_NO_MEMORY;
-        HIP_TRY(hipMemcpyAsync(c->lnodes2, ln2.data(), ln2.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->lroot2, lr2.data(), lr2.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    }
     if (P > 0)
         hipLaunchKernelGGL(k_pack_prims, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->geo_lin, c->prim_idx_dev,
                            c->prim_idx_dev + P, static_cast<int>(P), c->prims);
@@ -1672,7 +1308,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     if (grid.y > 65535u) return RT_ERR_INVALID;
     int kind = c->kernel;
     const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
-    const bool accel_usable = c->accel_ok && kp.useBVH && !kp.useMT && cmag <= 100.f * (c->accel.scene_mag + 1.f);
+    const bool accel_usable = c->accel_ok && kp.useBVH && !kp.useMT && cmag <= c->accel.origin_lim;
     if (kind == RT_KERNEL_AUTO) kind = accel_usable ? RT_KERNEL_ACCEL : RT_KERNEL_PACKET;
     if (kind == RT_KERNEL_ACCEL && !accel_usable) kind = RT_KERNEL_PACKET;  // same image either way
     const size_t lds = static_cast<size_t>(kp.max_stack) * kBlock * sizeof(int);
@@ -1702,27 +1338,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         }
         auto kfn = c->persistent ? (c->tile_times ? k_accel<true, true> : k_accel<true, false>)
                                  : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
-        k2.tile_stride = 1;
-        if (c->scatter_tiles) {
-            // a prime stride (coprime with the tile count) near 0.38 * tiles
-            static const int primes[] = {7919, 104729, 15485863, 1299709, 611953};
-            for (int pr : primes)
-                if (k2.tiles % pr != 0) {
-                    k2.tile_stride = pr % k2.tiles == 0 ? 1 : pr % k2.tiles;
-                    break;
-                }
-            int g = k2.tile_stride, t = k2.tiles;  // keep it a bijection
-            while (t) { int tmp = g % t; g = t; t = tmp; }
-            if (g != 1) k2.tile_stride = 1;
-        }
         k2.lane_from_depth = c->lane_from_depth;
         k2.lane_stack = c->accel.max_stack;
-        k2.lane_walk = c->lnodes2 ? ((c->lane_walk == 3 && c->anodes2) ? 3 : (c->lane_walk >= 2 ? 2 : 1)) : 1;
-        const size_t lds = k2.lane_from_depth < k2.maxBounces
-                               ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 4 * (k2.lane_walk >= 2 ? 2 : 1)
-                               : 0;
-        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, c->anodes, c->lnodes, c->prims, c->mat,
-                           c->lnodes2, c->lroot2, c->anodes2, c->tleaf, k2);
+        const size_t lds =
+            k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 2 * sizeof(int) : 0;
+        const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, kp.N, c->accel.origin_lim,
+                          c->boxes_finite};
+        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
                            kp);
@@ -2068,20 +1690,6 @@ extern "C" int rt_debug_cone_cull(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID;
     c->cone_cull = on ? 1 : 0;
     return c->have_scene ? upload_accel(c) : RT_OK;
-}
-
-// Diagnostics: scattered tile dispatch order on/off.
-extern "C" int rt_debug_scatter(rt_ctx* c, int on) {
-    if (!c) return RT_ERR_INVALID;
-    c->scatter_tiles = on ? 1 : 0;
-    return RT_OK;
-}
-
-// Diagnostics: per-lane walk form (1 = node-at-pop, 2 = while-while).
-extern "C" int rt_debug_lane_walk(rt_ctx* c, int form) {
-    if (!c || form < 1 || form > 3) return RT_ERR_INVALID;
-    c->lane_walk = form;
-    return RT_OK;
 }
 
 extern "C" int rt_set_launch(rt_ctx* c, int waves_per_block, int persistent) {

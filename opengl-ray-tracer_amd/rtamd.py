@@ -338,8 +338,9 @@ class ComputeShader:
     """The GPU operator: ComputeShader("gpu_shader.comp") + its SSBOs + uniforms
     (src/computeShader.hpp, src/main.cpp:238-370) on one HIP device."""
 
-    def __init__(self, device=0):
-        self._lib = rt_lib()
+    def __init__(self, device=0, lib_path=None):
+        # lib_path: another build of librtamd.so (A/B of two builds in one process, tools/ab.py)
+        self._lib = rt_lib() if lib_path is None else _bind(C.CDLL(os.path.abspath(lib_path)), RT_SYMBOLS)
         h = C.c_void_p()
         self._chk(self._lib.rt_create(C.byref(h), device), "rt_create")
         self._h = h
@@ -435,20 +436,10 @@ class ComputeShader:
     def set_walk(self, lane_from_depth):
         self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
 
-    def debug_lane_walk(self, form):
-        fn = self._lib.rt_debug_lane_walk
-        fn.argtypes = [_P, _I]
-        self._chk(fn(self._h, int(form)), "rt_debug_lane_walk")
-
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(bool(on))), "rt_debug_cone_cull")
-
-    def debug_scatter(self, on):
-        fn = self._lib.rt_debug_scatter
-        fn.argtypes = [_P, _I]
-        self._chk(fn(self._h, int(bool(on))), "rt_debug_scatter")
 
     def debug_tile_times(self, cap):
         """cap > 0: enable per-tile stamps (diagnostics); then tile_times(cap) reads them."""

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "../../opengl-ray-tracer_amd/csrc/accel.h"
+#include "../../opengl-ray-tracer_amd/csrc/accel_math.h"
 
 namespace {
 struct V { float x, y, z; };
@@ -72,15 +73,10 @@ bool ref_aabb(V o, V inv, const rt_vec3& lo, const rt_vec3& hi) {
     return tmax >= tmin && tmax > 0.0f;
 }
 
-float safe_inv(float d) { return d == 0.0f ? std::copysign(1e30f, d) : 1.0f / d; }
-
-bool padded(V o, V invs, float dlen, const rta::Box3& b, float limp) {
-    float tx0 = (b.lo[0] - o.x) * invs.x, tx1 = (b.hi[0] - o.x) * invs.x;
-    float ty0 = (b.lo[1] - o.y) * invs.y, ty1 = (b.hi[1] - o.y) * invs.y;
-    float tz0 = (b.lo[2] - o.z) * invs.z, tz1 = (b.hi[2] - o.z) * invs.z;
-    float tmin = std::fmax(std::fmax(std::fmin(tx0, tx1), std::fmin(ty0, ty1)), std::fmin(tz0, tz1));
-    float tmax = std::fmin(std::fmin(std::fmax(tx0, tx1), std::fmax(ty0, ty1)), std::fmax(tz0, tz1));
-    return tmax >= std::fmax(tmin, 0.0f) && tmin * dlen <= limp;
+// The device walk's conservative tests (accel_math.h), same float operations.
+bool padded(const rta::RayC& c, const rta::Box3& b, float l) {
+    float te;
+    return rta::box_enter(c, b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2], rta::t_limit(l, c.rdl), te);
 }
 }  // namespace
 
@@ -103,8 +99,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
         long long nodes_before = 0;
         V ro = mk(o[3 * r], o[3 * r + 1], o[3 * r + 2]), rd = mk(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
         V inv = mk(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
-        V invs = mk(safe_inv(rd.x), safe_inv(rd.y), safe_inv(rd.z));
-        float dlen = std::sqrt(dot(rd, rd));
+        const rta::RayC rc = rta::ray_consts(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, A.origin_lim);
         for (int pass = 0; pass < 2; ++pass) {
             const bool shadow = pass == 1;
             Best b{1e20f, 0x7fffffff, mk(0, 0, 0), -1};
@@ -114,8 +109,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
             while (!st.empty() && !(shadow && hit_shadow)) {
                 int code = st.back();
                 st.pop_back();
-                float l = shadow ? lim[r] : b.d;
-                float limp = l * 1.002f + 1e-6f;
+                const float l = shadow ? lim[r] : b.d;
                 auto scan = [&](int start, int cnt) {
                     for (int i = 0; i < cnt && !(shadow && hit_shadow); ++i) {
                         const int si = A.prim_shape[start + i], seq = A.prim_seq[start + i];
@@ -130,12 +124,12 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         }
                     }
                 };
-                if (std::getenv("ACDBG")) std::printf("pop %d lim %g best %d %g\n", code, limp, b.shape, b.d);
+                if (std::getenv("ACDBG")) std::printf("pop %d lim %g best %d %g\n", code, l, b.shape, b.d);
                 ++nodes_before;
                 if (code >= 0) {
                     const FlatNode& nd = nodes[code];
                     if (!ref_aabb(ro, inv, nd.boundsMin, nd.boundsMax)) continue;
-                    if ((A.flags[code] & 8) && !padded(ro, invs, dlen, A.content[code], limp)) continue;
+                    if ((A.flags[code] & 8) && !padded(rc, A.content[code], l)) continue;
                     if (nd.leftChild == -1) {
                         scan(A.plain_start[code], A.plain_count[code]);
                         if (A.local_root[code] >= 0) st.push_back(-(A.local_root[code] + 1));
@@ -145,9 +139,9 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     }
                 } else {
                     const int j = -code - 1;
-                    if (!padded(ro, invs, dlen, A.lbox[j], limp)) continue;
+                    if (!padded(rc, A.lbox[j], l)) continue;
                     const float* k = &A.lcone[4 * j];  // back-face cone (accel.h)
-                    if (dot(mk(k[0], k[1], k[2]), rd) < k[3] * dlen) continue;
+                    if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
                     if (A.la[j] < 0) {
                         scan(-A.la[j] - 1, A.lb[j]);
                     } else {

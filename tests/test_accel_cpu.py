@@ -79,7 +79,7 @@ def random_rays(rng, R, box=30.0):
     return o, d
 
 
-@pytest.mark.parametrize("cfg", [2, 3, 5])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 5])
 def test_accel_matches_reference_walk(check_lib, cfg):
     W, H = 96, 54
     fs = rtamd.generate(cfg, 0, W, H)
@@ -115,3 +115,66 @@ def test_accel_ties(check_lib):
     fs2 = rtamd.FlatScene(shapes, nodes, idx, fs.camera, fs.light)
     o, d = camera_rays(fs2, 96, 54)
     compare(check_lib, fs2, o, d, np.full(len(o), 50.0))
+
+
+def test_accel_axis_aligned_tiny_and_far_rays(check_lib):
+    """The fused slab test's edge cases (accel_math.h): zero and tiny direction
+    components (clamped reciprocal), origins far outside the scene and
+    non-unit directions (both take the always-enter mode)."""
+    fs = rtamd.generate(3, 0, 96, 54)
+    rng = np.random.default_rng(11)
+    R = 3000
+    o = rng.uniform(-20, 20, (R, 3))
+    d = np.zeros((R, 3))
+    d[np.arange(R), rng.integers(0, 3, R)] = rng.choice([-1.0, 1.0], R)
+    tiny = rng.choice([0.0, 1e-30, -1e-25, 1e-20, -1e-19, 1e-12, 3e-8], (R, 3))
+    d2 = np.where(d == 0, tiny, d)
+    # far origins aimed back at the scene, and scaled (non-unit) directions
+    t = rng.uniform(-5, 5, (R, 3))
+    far = rng.normal(size=(R, 3))
+    far = far / np.linalg.norm(far, axis=1, keepdims=True) * rng.choice([1e4, 1e6, 1e8], (R, 1))
+    d3 = (t - far) / np.linalg.norm(t - far, axis=1, keepdims=True)
+    o4, d4 = random_rays(rng, R)
+    d4 = d4 * rng.choice([0.3, 3.0], (R, 1))
+    O = np.concatenate([o, o, far, o4])
+    D = np.concatenate([d, d2, d3, d4])
+    lim = rng.uniform(1, 80, len(O))
+    compare(check_lib, fs, O, D, lim)
+
+
+def test_accel_sphere_silhouettes_from_afar(check_lib):
+    """Rays grazing sphere silhouettes from origins up to the accelerator's
+    origin bound: the reference's sphere root cancels (D = bb^2 - 4 aa cc), so
+    its hit points stray outside the sphere by ~sqrt(k) * |o - c|; the sphere
+    boxes carry that margin (accel.cpp, kSphereErr). Small spheres far from the
+    scene centre make the stray larger than the relative padding alone."""
+    fs = rtamd.generate(3, 0, 96, 54)
+    rng = np.random.default_rng(5)
+    n = 300
+    sph = np.zeros(n, fs.shapes.dtype)
+    sph["type"] = 0
+    sph["sphereCenter"] = rng.uniform(-50, 50, (n, 3))
+    sph["sphereRadius"] = rng.uniform(0.005, 0.05, n)
+    sph["material"] = fs.shapes["material"][0]
+    shapes = np.concatenate([fs.shapes, sph])
+    # one reference leaf holding everything: every sphere sits under local boxes
+    nodes = np.zeros(1, rtamd.NODE_DTYPE)
+    nodes["boundsMin"], nodes["boundsMax"] = -1e3, 1e3
+    nodes["leftChild"] = nodes["rightChild"] = -1
+    nodes["numShapes"] = len(shapes)
+    idx = np.arange(len(shapes), dtype=np.int32)
+    fs2 = rtamd.FlatScene(shapes, nodes, idx, fs.camera, fs.light)
+    R = 8000
+    k = rng.integers(0, n, R)
+    c = sph["sphereCenter"][k].astype(np.float64)
+    r = sph["sphereRadius"][k].astype(np.float64)
+    u = rng.normal(size=(R, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    o = np.clip(c + u * rng.uniform(50, 300, (R, 1)), -220, 220)  # origin_lim = 4 * (55 + 1) = 224
+    w = np.cross(o - c, rng.normal(size=(R, 3)))
+    w /= np.linalg.norm(w, axis=1, keepdims=True)
+    tgt = c + w * (r + rng.uniform(-0.01, 0.2, R))[:, None]  # near or just outside the silhouette
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    lim = rng.uniform(1, 400, R)
+    compare(check_lib, fs2, o, d, lim)

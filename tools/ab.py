@@ -19,30 +19,14 @@ import rtamd  # noqa: E402
 
 WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 1920, 1080, 3)}
 VARIANTS = {
-    "accel_wpb4": dict(kernel=3, wpb=4, persistent=False, walk=1),
-    "accel_ww": dict(kernel=3, wpb=4, persistent=False, walk=1, form=2),
-    "accel_ww_w1": dict(kernel=3, wpb=1, persistent=False, walk=1, form=2),
-    "accel_ww_all": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2),
-    "accel_ww_all_w1": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2),
-    "default": dict(kernel=0, wpb=1, persistent=False, walk=1, form=3, scatter=0),
-    "w3_all": dict(kernel=3, wpb=1, persistent=False, walk=0, form=3, scatter=0),
-    "w3_hybrid": dict(kernel=3, wpb=1, persistent=False, walk=1, form=3, scatter=0),
-    "w2_all": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2, scatter=0),
-    "w3_packet": dict(kernel=3, wpb=4, persistent=False, walk=99, form=3, scatter=0),
-    "w3_hybrid4": dict(kernel=3, wpb=4, persistent=False, walk=1, form=3, scatter=0),
-    "ww_all_noscatter": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2, scatter=0),
-    "ww_all_w1_noscatter": dict(kernel=3, wpb=1, persistent=False, walk=0, form=2, scatter=0),
-    "ww_all_pers": dict(kernel=3, wpb=4, persistent=True, walk=0, form=2),
-    "ww_pers_w1": dict(kernel=3, wpb=1, persistent=True, walk=1, form=2),
-    "ww_nocone": dict(kernel=3, wpb=4, persistent=False, walk=1, form=2, cone=0),
-    "ww_all_nocone": dict(kernel=3, wpb=4, persistent=False, walk=0, form=2, cone=0),
-    "accel_wpb1": dict(kernel=3, wpb=1, persistent=False, walk=1),
-    "accel_pers4": dict(kernel=3, wpb=4, persistent=True, walk=1),
-    "accel_pers1": dict(kernel=3, wpb=1, persistent=True, walk=1),
-    "accel_packetwalk": dict(kernel=3, wpb=4, persistent=False, walk=99),
-    "accel_lanewalk": dict(kernel=3, wpb=4, persistent=False, walk=0),
-    "accel_lanewalk_w1": dict(kernel=3, wpb=1, persistent=False, walk=0),
-    "accel_walk2": dict(kernel=3, wpb=4, persistent=False, walk=2),
+    "default": dict(kernel=0, wpb=1, persistent=False, walk=1),
+    "hybrid_w2": dict(kernel=3, wpb=2, persistent=False, walk=1),
+    "hybrid_w4": dict(kernel=3, wpb=4, persistent=False, walk=1),
+    "lane_all": dict(kernel=3, wpb=1, persistent=False, walk=0),
+    "packet_all": dict(kernel=3, wpb=1, persistent=False, walk=99),
+    "lane_from2": dict(kernel=3, wpb=1, persistent=False, walk=2),
+    "persistent": dict(kernel=3, wpb=1, persistent=True, walk=1),
+    "nocone": dict(kernel=3, wpb=1, persistent=False, walk=1, cone=0),
     "packet": dict(kernel=2, wpb=4, persistent=False, walk=1),
 }
 
@@ -50,30 +34,41 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--frames", type=int, default=20)
-ap.add_argument("--variants", default="accel_packetwalk,accel_wpb4,accel_lanewalk,accel_lanewalk_w1,accel_walk2,accel_pers4")
+ap.add_argument("--variants", default="default,lane_all,packet_all,hybrid_w2")
 ap.add_argument("--bounces", type=int, default=0, help="override maxBounces")
 ap.add_argument("--times", action="store_true", help="per-tile wall-clock distribution")
+ap.add_argument("--lib2", default=None, help="second librtamd.so build: variants NAME@2 run on it")
 a = ap.parse_args()
 cfg, W, H, mb = WL[a.config]
 mb = a.bounces or mb
 fs = rtamd.generate(cfg, 0, W, H)
-ctx = rtamd.ComputeShader(0)
-ctx.upload(fs)
-ctx.set_params(W, H, mb, True)
+ctxs = {}
+for key, path in (("", None), ("@2", a.lib2)):
+    if key and not path:
+        continue
+    cx = rtamd.ComputeShader(0, lib_path=path)
+    cx.upload(fs)
+    cx.set_params(W, H, mb, True)
+    ctxs[key] = cx
 out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
 torch.cuda.synchronize()
 names = a.variants.split(",")
+
+
+def pick(n):
+    base, _, tag = n.partition("@")
+    return ctxs["@" + tag if tag else ""], VARIANTS[base]
+
+
 res = {n: [] for n in names}
 ref = None
 for rnd in range(a.rounds):
     for n in names:
-        v = VARIANTS[n]
+        ctx, v = pick(n)
         ctx.set_kernel(v["kernel"])
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
-        ctx.debug_lane_walk(v.get("form", 1))
         ctx.debug_cone_cull(v.get("cone", 1))
-        ctx.debug_scatter(v.get("scatter", 1))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         ctx.sync()
         img = out.cpu().numpy()
@@ -89,13 +84,11 @@ print(json.dumps({"config": a.config, "maxBounces": mb, "variants": summary}))
 if a.times:
     tiles = ((W + 7) // 8) * ((H + 7) // 8)
     for n in names:
-        v = VARIANTS[n]
+        ctx, v = pick(n)
         ctx.set_kernel(v["kernel"])
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
-        ctx.debug_lane_walk(v.get("form", 1))
         ctx.debug_cone_cull(v.get("cone", 1))
-        ctx.debug_scatter(v.get("scatter", 1))
         ctx.debug_tile_times(tiles)
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         t = ctx.tile_times(tiles).astype(np.int64)
@@ -118,3 +111,10 @@ if a.times:
         med = np.argsort(dur)[len(dur) // 2]
         print("  median tile:", (round(float(dur[med]), 1), int(t[med, 2]), int(t[med, 4]), int(t[med, 3]), int(t[med, 5])))
         print("  totals: nodes", int(t[:, 2].sum()), "tests", int(t[:, 3].sum()))
+        # concurrency profile: tiles in flight over the kernel's span, in 20 slices
+        span = float(end.max())
+        edges = np.linspace(0.0, span, 21)
+        live = [int(((start < b) & (end > a_)).sum()) for a_, b in zip(edges[:-1], edges[1:])]
+        print("  tiles in flight per 5% of span:", live)
+        print("  tiles finishing after 50/75/90% of span:",
+              [int((end > f * span).sum()) for f in (0.5, 0.75, 0.9)])
