@@ -905,9 +905,32 @@ __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
     return pc;
 }
 
+// Diagnostics (TIMED k_accel): one record of kTileRec u64 per tile:
+//   [0] start, [1] end (100 MHz wall clock), [2] node steps and [3] tests
+//   summed over the wave's lanes, [4], [5] their per-lane maxima,
+//   [6 + s] wave clock ticks and [14 + s] node steps summed over lanes of walk
+//   slot s = 2 * bounce + (0 closest, 1 shadow), bounce < 4, [22] active lanes
+//   at bounce 0.
+constexpr int kTileRec = 24;
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, const WalkCount& before,
+                                         const WalkCount& after, unsigned long long ticks) {
+    if (!rec || slot >= 8) return;
+    const unsigned long long n = wave_sum(after.nodes - before.nodes);
+    if ((threadIdx.x & 63) == 0) {
+        rec[6 + slot] = ticks;
+        rec[14 + slot] = n;
+    }
+}
+
 template <bool COUNT>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
-                           int* stk, int cap, WalkCount& wc) {
+                           int* stk, int cap, WalkCount& wc, unsigned long long* rec) {
     const PixelCoord pc = tile_pixel(kp, tile);
     const V bg = background(kp, pc.y);
     Ray ray = primary_ray(kp, pc.x, pc.y);
@@ -919,10 +942,13 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
         bool unused = false;
         const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
+        WalkCount w0 = wc;
+        unsigned long long c0 = COUNT ? clock64() : 0;
         if (lane_mode)
             lane_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
         else
             packet_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+        if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
         if (alive && best.slot < 0) {
             acc = acc + mulv(att, bg);
             alive = false;
@@ -940,10 +966,13 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         }
         bool shadow = false;
         Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
+        w0 = wc;
+        c0 = COUNT ? clock64() : 0;
         if (lane_mode)
             lane_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
         else
             packet_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+        if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
     }
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
@@ -967,7 +996,8 @@ __global__ __launch_bounds__(kBlock) void k_accel(AccelPtrs A, const float4* __r
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
         WalkCount wc{0u, 0u};
-        accel_tile<TIMED>(A, mat, kp, tile, stk, kp.lane_stack, wc);
+        unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
+        accel_tile<TIMED>(A, mat, kp, tile, stk, kp.lane_stack, wc, rec);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -978,7 +1008,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(AccelPtrs A, const float4* __r
                 mt = max(mt, __shfl_xor(mt, off));
             }
             if (lane == 0) {
-                unsigned long long* o = kp.tile_times + 6 * static_cast<size_t>(tile);
+                unsigned long long* o = rec;
                 o[0] = t0;
                 o[1] = t1;
                 o[2] = sn;
@@ -1330,6 +1360,9 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         k2.tiles = k2.tiles_x * ((kp.out_rows + 7) / 8);
         k2.tile_counter = c->tile_counter;
         k2.tile_times = c->tile_times;
+        if (c->tile_times)
+            HIP_TRY(hipMemsetAsync(c->tile_times, 0, kTileRec * c->tile_times_cap * sizeof(unsigned long long),
+                                   c->stream));
         const int wpb = c->waves_per_block;
         int blocks = (k2.tiles + wpb - 1) / wpb;
         if (c->persistent) {
@@ -1699,24 +1732,23 @@ extern "C" int rt_set_launch(rt_ctx* c, int waves_per_block, int persistent) {
     return RT_OK;
 }
 
-// Diagnostics (not part of rt_api.h): enable per-tile wall-clock stamps for
-// k_accel (cap tiles; 0 disables) and read them back (6 x u64 per tile:
-// start, end in 100 MHz s_memrealtime ticks; node pops and primitive tests
-// summed over the wave's lanes, then their per-lane maxima). Synchronous.
+// Diagnostics (not part of rt_api.h): enable per-tile records for k_accel
+// (cap tiles; 0 disables) and read them back (kTileRec u64 per tile, layout
+// at kTileRec). Synchronous.
 extern "C" int rt_debug_tile_times(rt_ctx* c, int cap, unsigned long long* out) {
     if (!c || cap < 0) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (out && c->tile_times && cap > 0) {
         const size_t n = std::min(static_cast<size_t>(cap), c->tile_times_cap);
-        HIP_TRY(hipMemcpy(out, c->tile_times, n * 6 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(out, c->tile_times, n * kTileRec * sizeof(unsigned long long), hipMemcpyDeviceToHost));
         return static_cast<int>(n);
     }
     hipFree(c->tile_times);
     c->tile_times = nullptr;
     c->tile_times_cap = 0;
     if (cap > 0) {
-        if (hipMalloc(&c->tile_times, static_cast<size_t>(cap) * 6 * sizeof(unsigned long long)) != hipSuccess)
+        if (hipMalloc(&c->tile_times, static_cast<size_t>(cap) * kTileRec * sizeof(unsigned long long)) != hipSuccess)
             return RT_ERR_NO_MEMORY;
         c->tile_times_cap = cap;
     }

@@ -448,7 +448,8 @@ class ComputeShader:
         self._chk(fn(self._h, int(cap), None), "rt_debug_tile_times")
 
     def tile_times(self, cap):
-        buf = np.zeros((cap, 6), np.uint64)
+        """[n, 24] per-tile records of k_accel (layout: kTileRec in rt_kernels.hip)."""
+        buf = np.zeros((cap, 24), np.uint64)
         fn = self._lib.rt_debug_tile_times
         fn.argtypes = [_P, _I, _P]
         n = fn(self._h, int(cap), _ptr(buf))

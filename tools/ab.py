@@ -111,10 +111,11 @@ if a.times:
         med = np.argsort(dur)[len(dur) // 2]
         print("  median tile:", (round(float(dur[med]), 1), int(t[med, 2]), int(t[med, 4]), int(t[med, 3]), int(t[med, 5])))
         print("  totals: nodes", int(t[:, 2].sum()), "tests", int(t[:, 3].sum()))
-        # concurrency profile: tiles in flight over the kernel's span, in 20 slices
-        span = float(end.max())
-        edges = np.linspace(0.0, span, 21)
-        live = [int(((start < b) & (end > a_)).sum()) for a_, b in zip(edges[:-1], edges[1:])]
-        print("  tiles in flight per 5% of span:", live)
-        print("  tiles finishing after 50/75/90% of span:",
-              [int((end > f * span).sum()) for f in (0.5, 0.75, 0.9)])
+        cyc, nod = t[:, 6:14].sum(axis=0), t[:, 14:22].sum(axis=0)
+        tot = cyc.sum()
+        for sl in range(min(2 * mb, 8)):
+            print(f"  bounce {sl // 2} {'shadow ' if sl % 2 else 'closest'}: wave-Mcycles {cyc[sl] / 1e6:8.1f}"
+                  f" ({100.0 * cyc[sl] / max(tot, 1):4.1f}%) lane node steps {nod[sl] / 1e6:7.2f} M")
+        slow = np.argsort(dur)[::-1][:32]
+        print("  slowest 32 tiles, share of wave cycles per walk:",
+              (t[slow, 6:6 + 2 * mb].sum(axis=0) / max(t[slow, 6:6 + 2 * mb].sum(), 1)).round(3).tolist())
