@@ -350,6 +350,89 @@ void build_cones(const FlatShape* shapes, AccelHost& A) {
     }
 }
 
+namespace {
+
+// Inner height of binary local node j: the stack entries a binary walk pushes
+// below it on its deepest path (0 for a leaf).
+int inner_height(const AccelHost& A, int j, std::vector<int>& memo) {
+    if (j < 0 || A.la[j] < 0) return 0;
+    if (memo[j] >= 0) return memo[j];
+    const int h = 1 + std::max(inner_height(A, A.la[j], memo), inner_height(A, A.lb[j] & 0x3fffffff, memo));
+    memo[j] = h;
+    return h;
+}
+
+// Collapses the binary local tree below binary inner node j into wide nodes:
+// a wide node takes j's children, then repeatedly replaces its largest inner
+// child (surface area) by that child's two children, up to kWide. A lane walk
+// pushes every entered child but the nearest, so a wide node of k children
+// adds k - 1 entries to the stack below it; `budget` bounds that sum along
+// every path (the expansion stops early where the budget requires). Returns
+// the wide id; `pend` = the bound reached.
+int make_wide(AccelHost& A, int j, int budget, std::vector<int>& memo, int& pend) {
+    auto inner = [&](int b) { return b >= 0 && A.la[b] >= 0; };
+    std::vector<int> slots{A.la[j], A.lb[j] & 0x3fffffff};
+    auto need = [&](const std::vector<int>& sl) {
+        int m = 0;
+        for (int b : sl) m = std::max(m, inner_height(A, b, memo));
+        return static_cast<int>(sl.size()) - 1 + m;
+    };
+    for (;;) {
+        if (static_cast<int>(slots.size()) >= kWide) break;
+        int pick = -1;
+        float best = -1.f;
+        for (int s2 = 0; s2 < static_cast<int>(slots.size()); ++s2)
+            if (inner(slots[s2]) && area(A.lbox[slots[s2]]) > best) {
+                best = area(A.lbox[slots[s2]]);
+                pick = s2;
+            }
+        if (pick < 0) break;
+        std::vector<int> next = slots;
+        const int b = next[pick];
+        next[pick] = A.la[b];
+        next.push_back(A.lb[b] & 0x3fffffff);
+        if (need(next) > budget) break;  // deeper expansion would exceed the stack budget
+        slots = next;
+    }
+    const int w = static_cast<int>(A.wchild.size()) / kWide;
+    A.wchild.resize(A.wchild.size() + kWide, -1);
+    A.wsub.resize(A.wsub.size() + kWide, -1);
+    const int own = static_cast<int>(slots.size()) - 1;
+    int below = 0;
+    for (int s2 = 0; s2 < static_cast<int>(slots.size()); ++s2) {
+        A.wchild[kWide * w + s2] = slots[s2];
+        if (inner(slots[s2])) {
+            int p = 0;
+            const int sub = make_wide(A, slots[s2], budget - own, memo, p);
+            A.wsub[kWide * w + s2] = sub;
+            below = std::max(below, p);
+        }
+    }
+    pend = own + below;
+    return w;
+}
+
+}  // namespace
+
+// Wide collapse of every local tree within the lane stack budget `cap`;
+// returns the stack bound of the lane walk over them.
+static int build_wide(AccelHost& A, const std::vector<int>& ref_depth, int cap) {
+    A.wchild.clear();
+    A.wsub.clear();
+    A.wroot.assign(A.local_root.size(), -1);
+    std::vector<int> memo(A.lbox.size(), -1);
+    int need = 0;
+    for (size_t k = 0; k < A.local_root.size(); ++k) {
+        const int r = A.local_root[k];
+        if (r < 0 || A.la[r] < 0) continue;
+        const int budget = std::max(cap - ref_depth[k] - 2, inner_height(A, r, memo));
+        int pend = 0;
+        A.wroot[k] = make_wide(A, r, budget, memo, pend);
+        need = std::max(need, ref_depth[k] + pend + 2);
+    }
+    return need;
+}
+
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
                  int leaf_threshold, int stack_cap, AccelHost& out) {
     (void)I;
@@ -441,7 +524,6 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
             if (budget < 1) return false;
             out.local_root[k] = lb.build(0, static_cast<int>(lb.items.size()), 0, budget);
             out.bounded_prims += static_cast<int>(lb.items.size());
-            max_stack = std::max(max_stack, depth[k] + lb.max_depth_seen + 2);
         }
         max_stack = std::max(max_stack, depth[k] + 1);
     }
@@ -477,8 +559,9 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
         out.flags[k] = axis | (swap << 2) | (bounded ? 8 : 0);
     };
     visit(N - 1);
-    out.max_stack = max_stack;
     build_cones(shapes, out);
+    max_stack = std::max(max_stack, build_wide(out, depth, kLaneStack));
+    out.max_stack = max_stack;
     return max_stack <= stack_cap;
 }
 

@@ -49,6 +49,11 @@ struct AccelHost {
     // an INNER hit there (np = N.d > 0 is required, gpu_shader.comp:206,278,294).
     // thr = -sin(angle + margin), or -4 (never culls).
     std::vector<float> lcone;     // 4 per local node: axis.xyz, thr
+    // 4-wide collapse of the local trees (build_wide): each wide node holds up
+    // to kWide binary nodes (their boxes and cones are tested at the wide node),
+    // wchild = binary node index or -1, wsub = wide node of an inner child or -1.
+    // wroot = wide node of each reference leaf's local root (-1: none, or a leaf).
+    std::vector<int> wchild, wsub, wroot;
     int max_stack = 0;            // worst-case wave stack entries
     // Largest |coordinate| of any bounded shape box, and the largest |coordinate|
     // of a ray origin the bounds are built for (kOriginRel * (scene_mag + 1)).
@@ -66,5 +71,11 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 
 // Back-face cones of the local nodes (fills A.lcone).
 void build_cones(const FlatShape* shapes, AccelHost& A);
+
+constexpr int kWide = 4;
+// Stack entries the lane walk keeps per lane in LDS (6 B each: code + bf16
+// entry parameter): 26 x 64 lanes x 6 B fits 16 waves per CU in 160 KB. The
+// wide collapse stays within it wherever the binary tree allows.
+constexpr int kLaneStack = 26;
 
 }  // namespace rta

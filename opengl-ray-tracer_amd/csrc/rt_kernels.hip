@@ -705,17 +705,60 @@ __device__ __forceinline__ Kids ref_kids(const AccelPtrs& A, unsigned uc, const 
     return k;
 }
 
-__device__ __forceinline__ Kids local_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
-    const float4* q = A.lnodes + 6 * static_cast<size_t>(uc & 0x3fffffffu);
-    const float4 a0 = q[0], a1 = q[1], b0 = q[2], b1 = q[3], ka = q[4], kb = q[5];
-    Kids k;
-    const bool ba = box_enter(c, a0, a1, tl, k.ta), bb = box_enter(c, b0, b1, tl, k.tb);
-    k.ha = in & ba & cone_ok(c, ka);
-    k.hb = in & bb & cone_ok(c, kb);
-    k.ca = __float_as_int(a0.w);
-    k.cb = __float_as_int(a1.w);
+// A wide local node (accel.h, build_wide): up to four children, stored as
+// 11 float4 (lo.x[4], lo.y[4], lo.z[4], hi.x[4], hi.y[4], hi.z[4], cone
+// axis x[4], y[4], z[4], cone threshold[4], child codes[4]). Returns the
+// children sorted by entry parameter, misses last (key = +inf).
+struct Kids4 {
+    float t[4];
+    int code[4];
+};
+
+__device__ __forceinline__ void cas(Kids4& k, int i, int j) {
+    const bool sw = k.t[j] < k.t[i];
+    const float ti = k.t[i], tj = k.t[j];
+    const int ci = k.code[i], cj = k.code[j];
+    k.t[i] = sw ? tj : ti;
+    k.t[j] = sw ? ti : tj;
+    k.code[i] = sw ? cj : ci;
+    k.code[j] = sw ? ci : cj;
+}
+
+__device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
+    const float4* q = A.lnodes + 11 * static_cast<size_t>(uc & 0x3fffffffu);
+    const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
+    const float4 ax = q[6], ay = q[7], az = q[8], th = q[9], cd = q[10];
+    const float l0[4] = {lx.x, lx.y, lx.z, lx.w}, l1[4] = {ly.x, ly.y, ly.z, ly.w}, l2[4] = {lz.x, lz.y, lz.z, lz.w};
+    const float h0[4] = {hx.x, hx.y, hx.z, hx.w}, h1[4] = {hy.x, hy.y, hy.z, hy.w}, h2[4] = {hz.x, hz.y, hz.z, hz.w};
+    const float a0[4] = {ax.x, ax.y, ax.z, ax.w}, a1[4] = {ay.x, ay.y, ay.z, ay.w}, a2[4] = {az.x, az.y, az.z, az.w};
+    const float tt[4] = {th.x, th.y, th.z, th.w};
+    const int cc[4] = {__float_as_int(cd.x), __float_as_int(cd.y), __float_as_int(cd.z), __float_as_int(cd.w)};
+    Kids4 k;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+        float te;
+        const bool h = rta::box_enter(c, l0[s2], l1[s2], l2[s2], h0[s2], h1[s2], h2[s2], tl, te) &
+                       !rta::cone_culls(c, a0[s2], a1[s2], a2[s2], tt[s2]) & (cc[s2] != kNoChild) & in;
+        k.t[s2] = h ? te : INFINITY;
+        k.code[s2] = cc[s2];
+    }
     return k;
 }
+
+__device__ __forceinline__ void sort4(Kids4& k) {
+    cas(k, 0, 1);
+    cas(k, 2, 3);
+    cas(k, 0, 2);
+    cas(k, 1, 3);
+    cas(k, 1, 2);
+}
+
+// Stacked entry parameters are kept as bf16 rounded toward zero: never above
+// the true value (te >= 0), so the pop-time prune only ever drops less.
+__device__ __forceinline__ unsigned short f_bf16_down(float t) {
+    return static_cast<unsigned short>(__float_as_uint(t) >> 16);
+}
+__device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_float(static_cast<unsigned>(b) << 16); }
 
 // Per-lane walk ("while-while"): each lane walks its own stack in LDS (code +
 // entry parameter per entry). A lane descends until it holds a leaf, keeping
@@ -724,7 +767,7 @@ __device__ __forceinline__ Kids local_kids(const AccelPtrs& A, unsigned uc, cons
 // nearer hit has been found since it was pushed.
 template <bool SHADOW, bool COUNT = false>
 __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
-                          int* stk, float* stt, int stride, int cap, WalkCount& wc) {
+                          int* stk, unsigned short* stt, int stride, int cap, WalkCount& wc) {
     if (A.N <= 0 || !active) return;
     const V inv = inv_dir(r.d);
     const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
@@ -738,7 +781,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
             if (!have) {
                 if (sp == 0) break;
                 --sp;
-                if (stt[sp * stride] > tl) continue;  // a nearer hit was found since the push
+                if (bf16_f(stt[sp * stride]) > tl) continue;  // a nearer hit was found since the push
                 cur = stk[sp * stride];
                 have = true;
             }
@@ -760,7 +803,21 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 count = static_cast<int>(uc & 0xffu);
                 continue;
             } else if (uc & kLocal) {
-                k = local_kids(A, uc, c, tl, true);
+                Kids4 w = wide_kids(A, uc, c, tl, true);
+                sort4(w);
+#pragma unroll
+                for (int s2 = 3; s2 >= 1; --s2) {
+                    if (w.t[s2] < INFINITY && sp < cap) {
+                        stk[sp * stride] = w.code[s2];
+                        stt[sp * stride] = f_bf16_down(w.t[s2]);
+                        ++sp;
+                    }
+                }
+                if (w.t[0] < INFINITY) {
+                    cur = w.code[0];
+                    have = true;
+                }
+                continue;
             } else {
                 k = ref_kids(A, uc, r, inv, c, tl, true, fast);
             }
@@ -768,7 +825,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 const bool a_first = !(k.tb < k.ta);  // nearer entry first
                 if (sp < cap) {
                     stk[sp * stride] = a_first ? k.cb : k.ca;
-                    stt[sp * stride] = a_first ? k.tb : k.ta;
+                    stt[sp * stride] = f_bf16_down(a_first ? k.tb : k.ta);
                     ++sp;
                 }
                 cur = a_first ? k.ca : k.cb;
@@ -839,9 +896,39 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
             start = static_cast<int>((uc >> 8) & 0x3fffffu);
             count = static_cast<int>(uc & 0xffu);
         } else if (uc & kLocal) {
-            k = local_kids(A, uc, c, tl, lane_in(m));
-            k.ca = uni(k.ca);
-            k.cb = uni(k.cb);
+            // wide node: children ordered by the entry parameters of the first lane
+            // that enters any of them; the rest pushed far to near
+            const Kids4 w = wide_kids(A, uc, c, tl, lane_in(m));
+            unsigned long long wm[4];
+            float key[4];
+            int code[4];
+            unsigned long long any = 0;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                wm[s2] = __ballot(w.t[s2] < INFINITY);
+                any |= wm[s2];
+            }
+            const int rep = any ? __builtin_ctzll(any) : 0;
+#pragma unroll
+            for (int s2 = 0; s2 < 4; ++s2) {
+                key[s2] = wm[s2] ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.t[s2]), rep)) : INFINITY;
+                code[s2] = uni(w.code[s2]);
+                if (wm[s2] && !(key[s2] < INFINITY)) key[s2] = 3.0e38f;  // the representative lane misses it
+            }
+#define RT_CAS3(i, j)                                                                   \
+    if (key[j] < key[i]) {                                                              \
+        const float t_ = key[i]; key[i] = key[j]; key[j] = t_;                          \
+        const int c_ = code[i]; code[i] = code[j]; code[j] = c_;                        \
+        const unsigned long long m_ = wm[i]; wm[i] = wm[j]; wm[j] = m_;                 \
+    }
+            RT_CAS3(0, 1) RT_CAS3(2, 3) RT_CAS3(0, 2) RT_CAS3(1, 3) RT_CAS3(1, 2)
+#undef RT_CAS3
+#pragma unroll
+            for (int s2 = 3; s2 >= 1; --s2)
+                if (wm[s2] && st.sp < kMaxStack) st.push(code[s2], wm[s2]);
+            cur = code[0];
+            m = wm[0];
+            continue;
         } else {
             k = ref_kids(A, uc, r, inv, c, tl, lane_in(m), fast);
             k.ca = uni(k.ca);
@@ -930,13 +1017,12 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
 
 template <bool COUNT>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
-                           int* stk, int cap, WalkCount& wc, unsigned long long* rec) {
+                           int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
     const PixelCoord pc = tile_pixel(kp, tile);
     const V bg = background(kp, pc.y);
     Ray ray = primary_ray(kp, pc.x, pc.y);
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
     bool alive = pc.active;
-    float* stt = reinterpret_cast<float*>(stk) + static_cast<size_t>(cap) * blockDim.x;
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
@@ -981,10 +1067,18 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 // PERSISTENT: each wave pulls tiles from one device counter until none is
 // left (every wave reaches the exit); otherwise one tile per wave. TIMED
 // writes each tile's start/end wall clock and walk counts (diagnostics only).
+// At most 128 VGPRs: four waves per SIMD, which the LDS stacks also fit
+// (accel.h, kLaneStack).
+#ifndef RT_ACCEL_ATTR
+#define RT_ACCEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
+#endif
 template <bool PERSISTENT, bool TIMED>
-__global__ __launch_bounds__(kBlock) void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
+__global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
+    // per-lane stacks, entry j of lane i at [j * blockDim.x + i]: codes, then bf16 entry parameters
     int* stk = lds_stack + threadIdx.x;
+    unsigned short* stt =
+        reinterpret_cast<unsigned short*>(lds_stack + static_cast<size_t>(kp.lane_stack) * blockDim.x) + threadIdx.x;
     const int lane = threadIdx.x & 63;
     int tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (PERSISTENT) {
@@ -997,7 +1091,7 @@ __global__ __launch_bounds__(kBlock) void k_accel(AccelPtrs A, const float4* __r
         if (TIMED) t0 = wall_clock64();
         WalkCount wc{0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
-        accel_tile<TIMED>(A, mat, kp, tile, stk, kp.lane_stack, wc, rec);
+        accel_tile<TIMED>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1086,6 +1180,7 @@ struct rt_ctx {
     int waves_per_block = 1, persistent = 0, cu_count = 256;
     int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
     int cone_cull = 1;
+    int lane_stack_override = 0;  // diagnostics only (rt_debug_lane_stack): breaks exactness if too small
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
@@ -1207,35 +1302,38 @@ int upload_accel(rt_ctx* c) {
         an[4 * k + 2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[k]));
         an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
     }
-    // lnodes: local inner nodes only, each with both child boxes, child codes
-    // (leaf: kLocal|kLeaf|start<<8|count, inner: kLocal|id) and back-face cones.
-    const size_t M = A.lbox.size(), P = A.prim_shape.size();
-    std::vector<int> inner_id(M, -1);
-    int n_inner = 0;
-    for (size_t j = 0; j < M; ++j)
-        if (A.la[j] >= 0) inner_id[j] = n_inner++;
+    // lnodes: the wide local nodes (accel.h, build_wide), 11 float4 each (wide_kids).
+    const size_t P = A.prim_shape.size();
     bool codes_ok = true;
-    auto code_of = [&](size_t j) -> int {
-        if (A.la[j] < 0) {
-            const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
-            if (st >= (1u << 22) || cnt > 255u) codes_ok = false;
-            return static_cast<int>(kLocal | kLeaf | (st << 8) | cnt);
-        }
-        return static_cast<int>(kLocal | static_cast<unsigned>(inner_id[j]));
+    auto leaf_code = [&](size_t j) -> int {
+        const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
+        if (st >= (1u << 22) || cnt > 255u) codes_ok = false;
+        return static_cast<int>(kLocal | kLeaf | (st << 8) | cnt);
     };
-    std::vector<float4> ln(6 * static_cast<size_t>(n_inner ? n_inner : 1));
-    for (size_t j = 0; j < M; ++j) {
-        if (A.la[j] < 0) continue;
-        const size_t l = static_cast<size_t>(A.la[j]), r = static_cast<size_t>(A.lb[j] & 0x3fffffff);
-        const rta::Box3 &bl = A.lbox[l], &br = A.lbox[r];
-        float4* q = &ln[6 * static_cast<size_t>(inner_id[j])];
-        q[0] = make_float4(bl.lo[0], bl.lo[1], bl.lo[2], bits_f(code_of(l)));
-        q[1] = make_float4(bl.hi[0], bl.hi[1], bl.hi[2], bits_f(code_of(r)));
-        q[2] = make_float4(br.lo[0], br.lo[1], br.lo[2], 0.f);
-        q[3] = make_float4(br.hi[0], br.hi[1], br.hi[2], 0.f);
-        const float *cl = &A.lcone[4 * l], *cr = &A.lcone[4 * r];
-        q[4] = make_float4(cl[0], cl[1], cl[2], c->cone_cull ? cl[3] : -4.f);
-        q[5] = make_float4(cr[0], cr[1], cr[2], c->cone_cull ? cr[3] : -4.f);
+    const size_t nw = A.wchild.size() / rta::kWide;
+    std::vector<float4> ln(11 * (nw ? nw : 1));
+    for (size_t w = 0; w < nw; ++w) {
+        float v[11][4];
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const int j = A.wchild[rta::kWide * w + s2];
+            int code = kNoChild;
+            float box[6] = {0, 0, 0, 0, 0, 0}, cone[4] = {0, 0, 0, -4.f};
+            if (j >= 0) {
+                const rta::Box3& bx = A.lbox[j];
+                for (int a = 0; a < 3; ++a) {
+                    box[a] = bx.lo[a];
+                    box[3 + a] = bx.hi[a];
+                }
+                for (int a = 0; a < 4; ++a) cone[a] = A.lcone[4 * j + a];
+                if (!c->cone_cull) cone[3] = -4.f;
+                code = A.la[j] < 0 ? leaf_code(static_cast<size_t>(j))
+                                   : static_cast<int>(kLocal | static_cast<unsigned>(A.wsub[rta::kWide * w + s2]));
+            }
+            for (int a = 0; a < 6; ++a) v[a][s2] = box[a];
+            for (int a = 0; a < 4; ++a) v[6 + a][s2] = cone[a];
+            v[10][s2] = bits_f(code);
+        }
+        for (int r = 0; r < 11; ++r) ln[11 * w + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
     }
     // wnodes: per reference inner node both children's exact + content boxes;
     // tleaf: per reference leaf its plain range and local root code.
@@ -1247,7 +1345,9 @@ int upload_accel(rt_ctx* c) {
     for (int k = 0; k < N; ++k) {
         const FlatNode& n = c->host_nodes[k];
         if (n.leftChild == -1) {
-            const int lr = A.local_root[k] >= 0 ? code_of(static_cast<size_t>(A.local_root[k])) : kNoChild;
+            const int r = A.local_root[k];
+            const int lr = A.wroot[k] >= 0 ? static_cast<int>(kLocal | static_cast<unsigned>(A.wroot[k]))
+                                           : (r >= 0 ? leaf_code(static_cast<size_t>(r)) : kNoChild);
             tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr, 0);
             continue;
         }
@@ -1372,9 +1472,9 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         auto kfn = c->persistent ? (c->tile_times ? k_accel<true, true> : k_accel<true, false>)
                                  : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
         k2.lane_from_depth = c->lane_from_depth;
-        k2.lane_stack = c->accel.max_stack;
+        k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
         const size_t lds =
-            k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 2 * sizeof(int) : 0;
+            k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6 : 0;
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, kp.N, c->accel.origin_lim,
                           c->boxes_finite};
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
@@ -1723,6 +1823,14 @@ extern "C" int rt_debug_cone_cull(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID;
     c->cone_cull = on ? 1 : 0;
     return c->have_scene ? upload_accel(c) : RT_OK;
+}
+
+// Diagnostics: override the per-lane LDS stack depth of k_accel (0 = computed
+// bound). A value below the bound can drop stack entries: timing studies only.
+extern "C" int rt_debug_lane_stack(rt_ctx* c, int n) {
+    if (!c || n < 0 || n > kMaxStack) return RT_ERR_INVALID;
+    c->lane_stack_override = n;
+    return RT_OK;
 }
 
 extern "C" int rt_set_launch(rt_ctx* c, int waves_per_block, int persistent) {

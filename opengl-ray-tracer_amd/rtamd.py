@@ -436,6 +436,11 @@ class ComputeShader:
     def set_walk(self, lane_from_depth):
         self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
 
+    def debug_lane_stack(self, n):
+        fn = self._lib.rt_debug_lane_stack
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(n)), "rt_debug_lane_stack")
+
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull
         fn.argtypes = [_P, _I]

@@ -132,21 +132,24 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     if ((A.flags[code] & 8) && !padded(rc, A.content[code], l)) continue;
                     if (nd.leftChild == -1) {
                         scan(A.plain_start[code], A.plain_count[code]);
-                        if (A.local_root[code] >= 0) st.push_back(-(A.local_root[code] + 1));
+                        const int lr = A.local_root[code];
+                        if (lr >= 0 && A.wroot[code] >= 0) st.push_back(-(A.wroot[code] + 1));  // wide root
+                        else if (lr >= 0 && padded(rc, A.lbox[lr], l)) scan(-A.la[lr] - 1, A.lb[lr]);
                     } else {
                         st.push_back(nd.leftChild);
                         st.push_back(nd.rightChild);
                     }
                 } else {
-                    const int j = -code - 1;
-                    if (!padded(rc, A.lbox[j], l)) continue;
-                    const float* k = &A.lcone[4 * j];  // back-face cone (accel.h)
-                    if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
-                    if (A.la[j] < 0) {
-                        scan(-A.la[j] - 1, A.lb[j]);
-                    } else {
-                        st.push_back(-(A.la[j] + 1));
-                        st.push_back(-((A.lb[j] & 0x3fffffff) + 1));
+                    // wide local node (accel.h, build_wide): each child's padded
+                    // box and back-face cone, tested at the wide node
+                    const int w = -code - 1;
+                    for (int s2 = 0; s2 < rta::kWide; ++s2) {
+                        const int j = A.wchild[rta::kWide * w + s2];
+                        if (j < 0 || !padded(rc, A.lbox[j], l)) continue;
+                        const float* k = &A.lcone[4 * j];
+                        if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                        if (A.la[j] < 0) scan(-A.la[j] - 1, A.lb[j]);
+                        else st.push_back(-(A.wsub[rta::kWide * w + s2] + 1));
                     }
                 }
             }

