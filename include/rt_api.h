@@ -157,6 +157,15 @@ int rt_set_launch(struct rt_ctx* ctx, int waves_per_block, int persistent);
  * configs 2, 3 and 5). Same image for every value. */
 int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 
+/* Tile dispatch order of the accelerated kernel. RT_SCHED_ROWS: row-major.
+ * RT_SCHED_COST (default): every dispatch records each 8x8 tile's duration,
+ * and the next dispatch with the same tile count starts the tiles in
+ * decreasing order of those durations (longest first), so the frame is not
+ * left waiting on expensive tiles that started late. The order only changes
+ * when pixels are computed, never their values. */
+enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1 };
+int rt_set_schedule(struct rt_ctx* ctx, int mode);
+
 /* Accelerator statistics for the uploaded scene. */
 int rt_accel_info_get(struct rt_ctx* ctx, rt_accel_info* out);
 

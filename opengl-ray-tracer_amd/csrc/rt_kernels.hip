@@ -1000,6 +1000,17 @@ __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
 //   at bounce 0.
 constexpr int kTileRec = 24;
 
+// Cost-ordered dispatch (rt_set_schedule, k_tile_order): 32 half-octave
+// buckets of a tile's work; the render kernel counts them per group of
+// kOrderThreads tiles (one k_tile_order workgroup each).
+constexpr int kOrderBuckets = 32, kOrderThreads = 256;
+
+__device__ __forceinline__ int work_bucket(unsigned c) {
+    if (c < 2u) return 0;
+    const int l = 31 - __builtin_clz(c);  // >= 1
+    return min(kOrderBuckets - 1, 2 * l - 1 + static_cast<int>((c >> (l - 1)) & 1u));
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
@@ -1015,6 +1026,8 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
     }
 }
 
+// Walk counts (node steps, tests) are always kept: they are the cost that
+// orders the next dispatch (rt_set_schedule). COUNT adds the per-walk records.
 template <bool COUNT>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
@@ -1031,9 +1044,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         WalkCount w0 = wc;
         unsigned long long c0 = COUNT ? clock64() : 0;
         if (lane_mode)
-            lane_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
+            lane_walk<false, true>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
         else
-            packet_walk<false, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+            packet_walk<false, true>(A, ray, alive, 0.f, best, unused, wc);
         if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
         if (alive && best.slot < 0) {
             acc = acc + mulv(att, bg);
@@ -1055,9 +1068,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         w0 = wc;
         c0 = COUNT ? clock64() : 0;
         if (lane_mode)
-            lane_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
+            lane_walk<true, true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
         else
-            packet_walk<true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+            packet_walk<true, true>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
         if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
     }
@@ -1089,6 +1102,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
     while (tile < kp.tiles) {
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
+        if (kp.tile_order) tile = kp.tile_order[tile];  // dispatch order -> image tile (a permutation)
         WalkCount wc{0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
         accel_tile<TIMED>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
@@ -1111,6 +1125,14 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 o[5] = mt;
             }
         }
+        if (kp.tile_cost) {
+            const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
+            const unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
+            if (lane == 0) {
+                kp.tile_cost[tile] = wk;
+                atomicAdd(&kp.sched_hist[(tile / kOrderThreads) * kOrderBuckets + work_bucket(wk)], 1u);
+            }
+        }
         if (!PERSISTENT) break;
         int t = 0;
         if (lane == 0) t = atomicAdd(kp.tile_counter, 1);
@@ -1128,6 +1150,62 @@ __global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __re
     float4 last = src[4];
     last.w = __int_as_float(prim_seq[j]);  // f[17]: rank in the reference walk
     dst[4] = last;
+}
+
+// Dispatch order for the next frame (rt_set_schedule): tiles sorted by the
+// work their waves did in the last dispatch (node steps + primitive tests over
+// the 64 lanes; unlike a duration it does not depend on what ran beside the
+// tile), most first, as a counting sort over 32 half-octave buckets. The render
+// kernel counts each group of kOrderThreads tiles' buckets (hist rows); group
+// j's workgroup here places its tiles after every tile of a heavier bucket and
+// after the tiles of the same bucket in groups < j (ranks inside a group by
+// LDS atomics: order inside a bucket is arbitrary). Two histogram sets
+// alternate by frame; this kernel zeroes the rows the next frame counts into.
+__global__ __launch_bounds__(kOrderThreads) void k_tile_order(const unsigned* __restrict__ cost, int n,
+                                                              const unsigned* __restrict__ hist,
+                                                              unsigned* __restrict__ next, int next_words,
+                                                              int* __restrict__ order) {
+    constexpr int kPart = kOrderThreads / kOrderBuckets;  // threads per bucket for the row sums
+    __shared__ unsigned tot[kPart][kOrderBuckets], pre[kPart][kOrderBuckets];
+    __shared__ unsigned start[kOrderBuckets], rank[kOrderBuckets];
+    const int t = threadIdx.x, j = blockIdx.x, groups = gridDim.x;
+    {
+        const int b = t % kOrderBuckets, part = t / kOrderBuckets;
+        unsigned a = 0, p = 0;
+#pragma unroll 8
+        for (int r = part; r < groups; r += kPart) {
+            const unsigned h = hist[r * kOrderBuckets + b];
+            a += h;
+            p += r < j ? h : 0u;
+        }
+        tot[part][b] = a;
+        pre[part][b] = p;
+    }
+    for (int w = j * kOrderThreads + t; w < next_words; w += groups * kOrderThreads) next[w] = 0u;
+    __syncthreads();
+    if (t < 64) {  // one wave: bucket sums, then a suffix scan (buckets from the most work down)
+        unsigned a = 0, p = 0;
+        if (t < kOrderBuckets) {
+#pragma unroll
+            for (int k = 0; k < kPart; ++k) {
+                a += tot[k][t];
+                p += pre[k][t];
+            }
+            rank[t] = 0u;
+        }
+        unsigned x = a;  // inclusive sum over buckets >= t
+        for (int off = 1; off < kOrderBuckets; off <<= 1) {
+            const unsigned y = __shfl_down(x, off);
+            if (t + off < kOrderBuckets) x += y;
+        }
+        if (t < kOrderBuckets) start[t] = x - a + p;
+    }
+    __syncthreads();
+    const int i = j * kOrderThreads + t;
+    if (i < n) {
+        const int b = work_bucket(cost[i]);
+        order[start[b] + atomicAdd(&rank[b], 1u)] = i;
+    }
 }
 
 }  // namespace
@@ -1180,6 +1258,15 @@ struct rt_ctx {
     int waves_per_block = 1, persistent = 0, cu_count = 256;
     int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
     int cone_cull = 1;
+    int* tile_order = nullptr;  // diagnostics (rt_debug_tile_order): fixed dispatch order of the 8x8 tiles
+    int tile_order_n = 0;
+    // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
+    int schedule = RT_SCHED_COST;
+    unsigned* sched_cost = nullptr;
+    int* sched_order = nullptr;
+    unsigned* sched_sets = nullptr;      // 2 sets of per-group bucket histograms, alternating by frame
+    int sched_parity = 0;
+    int sched_cap = 0, sched_valid = 0;  // buffer capacity; tile count the order is for (0: none)
     int lane_stack_override = 0;  // diagnostics only (rt_debug_lane_stack): breaks exactness if too small
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
@@ -1389,6 +1476,10 @@ int upload_accel(rt_ctx* c) {
     return RT_OK;
 }
 
+size_t sched_set_words(int tiles) {
+    return static_cast<size_t>((tiles + kOrderThreads - 1) / kOrderThreads) * kOrderBuckets;
+}
+
 int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
                  size_t pitch, KParams& kp) {
     if (!c->have_scene || !c->have_cam || !c->have_light) return RT_ERR_NO_SCENE;
@@ -1471,6 +1562,31 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         }
         auto kfn = c->persistent ? (c->tile_times ? k_accel<true, true> : k_accel<true, false>)
                                  : (c->tile_times ? k_accel<false, true> : k_accel<false, false>);
+        k2.tile_order = nullptr;
+        k2.tile_cost = nullptr;
+        if (c->tile_order && c->tile_order_n == k2.tiles) {
+            k2.tile_order = c->tile_order;
+        } else if (c->schedule == RT_SCHED_COST) {
+            if (c->sched_cap < k2.tiles) {
+                hipFree(c->sched_cost);
+                hipFree(c->sched_order);
+                hipFree(c->sched_sets);
+                c->sched_cost = nullptr;
+                c->sched_order = nullptr;
+                c->sched_sets = nullptr;
+                c->sched_cap = c->sched_valid = 0;
+                if (hipMalloc(&c->sched_cost, k2.tiles * sizeof(unsigned)) != hipSuccess ||
+                    hipMalloc(&c->sched_order, k2.tiles * sizeof(int)) != hipSuccess ||
+                    hipMalloc(&c->sched_sets, 2 * sched_set_words(k2.tiles) * sizeof(unsigned)) != hipSuccess)
+                    return RT_ERR_NO_MEMORY;
+                HIP_TRY(hipMemsetAsync(c->sched_sets, 0, 2 * sched_set_words(k2.tiles) * sizeof(unsigned), c->stream));
+                c->sched_parity = 0;
+                c->sched_cap = k2.tiles;
+            }
+            k2.sched_hist = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
+            if (c->sched_valid == k2.tiles) k2.tile_order = c->sched_order;
+            k2.tile_cost = c->sched_cost;
+        }
         k2.lane_from_depth = c->lane_from_depth;
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
         const size_t lds =
@@ -1478,6 +1594,16 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, kp.N, c->accel.origin_lim,
                           c->boxes_finite};
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
+        if (k2.tile_cost) {
+            // the next frame's order; stream-ordered after this dispatch, before the next
+            unsigned* set = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
+            unsigned* next = c->sched_sets + (1 - c->sched_parity) * sched_set_words(c->sched_cap);
+            hipLaunchKernelGGL(k_tile_order, dim3((k2.tiles + kOrderThreads - 1) / kOrderThreads), dim3(kOrderThreads),
+                               0, c->stream, c->sched_cost, k2.tiles, set, next,
+                               static_cast<int>(sched_set_words(c->sched_cap)), c->sched_order);
+            c->sched_parity = 1 - c->sched_parity;
+            c->sched_valid = k2.tiles;
+        }
     } else {
         hipLaunchKernelGGL(k_packet, grid, dim3(kBlock), 0, c->stream, c->geo_leaf, c->geo_lin, c->mat, c->nodes,
                            kp);
@@ -1556,6 +1682,10 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->stats_dev);
     hipFree(c->tile_counter);
     hipFree(c->tile_times);
+    hipFree(c->tile_order);
+    hipFree(c->sched_cost);
+    hipFree(c->sched_order);
+    hipFree(c->sched_sets);
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1830,6 +1960,33 @@ extern "C" int rt_debug_cone_cull(rt_ctx* c, int on) {
 extern "C" int rt_debug_lane_stack(rt_ctx* c, int n) {
     if (!c || n < 0 || n > kMaxStack) return RT_ERR_INVALID;
     c->lane_stack_override = n;
+    return RT_OK;
+}
+
+extern "C" int rt_set_schedule(rt_ctx* c, int mode) {
+    if (!c || (mode != RT_SCHED_ROWS && mode != RT_SCHED_COST)) return RT_ERR_INVALID;
+    c->schedule = mode;
+    c->sched_valid = 0;
+    return RT_OK;
+}
+
+// Diagnostics: dispatch order of k_accel's tiles (a permutation of [0, n)),
+// used when n equals the launch's tile count; n = 0 clears it.
+extern "C" int rt_debug_tile_order(rt_ctx* c, const int* order, int n) {
+    if (!c || n < 0 || (n > 0 && !order)) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    hipFree(c->tile_order);
+    c->tile_order = nullptr;
+    c->tile_order_n = 0;
+    if (n == 0) return RT_OK;
+    std::vector<char> seen(n, 0);
+    for (int i = 0; i < n; ++i) {
+        if (order[i] < 0 || order[i] >= n || seen[order[i]]) return RT_ERR_INVALID;
+        seen[order[i]] = 1;
+    }
+    if (hipMalloc(&c->tile_order, n * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
+    HIP_TRY(hipMemcpy(c->tile_order, order, n * sizeof(int), hipMemcpyHostToDevice));
+    c->tile_order_n = n;
     return RT_OK;
 }
 

@@ -70,6 +70,7 @@ LIGHT_DTYPE = np.dtype({
 
 SPHERE, PLANE, WALL, TRIANGLE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_LANE, KERNEL_PACKET, KERNEL_ACCEL = 0, 1, 2, 3
+SCHED_ROWS, SCHED_COST = 0, 1
 
 
 class rt_params(C.Structure):
@@ -186,12 +187,16 @@ RT_SYMBOLS = {
     "rt_accel_info_get": (_I, [_P, _P]),
     "rt_set_launch": (_I, [_P, _I, _I]),
     "rt_set_walk": (_I, [_P, _I]),
+    "rt_set_schedule": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
 
 
-def _bind(lib, table):
+def _bind(lib, table, partial=False):
+    """partial: skip symbols the library lacks (an older build compared by tools/ab.py)."""
     for name, (res, args) in table.items():
+        if partial and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -340,7 +345,7 @@ class ComputeShader:
 
     def __init__(self, device=0, lib_path=None):
         # lib_path: another build of librtamd.so (A/B of two builds in one process, tools/ab.py)
-        self._lib = rt_lib() if lib_path is None else _bind(C.CDLL(os.path.abspath(lib_path)), RT_SYMBOLS)
+        self._lib = rt_lib() if lib_path is None else _bind(C.CDLL(os.path.abspath(lib_path)), RT_SYMBOLS, partial=True)
         h = C.c_void_p()
         self._chk(self._lib.rt_create(C.byref(h), device), "rt_create")
         self._h = h
@@ -436,10 +441,20 @@ class ComputeShader:
     def set_walk(self, lane_from_depth):
         self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
 
+    def set_schedule(self, mode):
+        """SCHED_COST (default): tiles start longest-first by their last duration; SCHED_ROWS: row-major."""
+        self._chk(self._lib.rt_set_schedule(self._h, int(mode)), "rt_set_schedule")
+
     def debug_lane_stack(self, n):
         fn = self._lib.rt_debug_lane_stack
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(n)), "rt_debug_lane_stack")
+
+    def debug_tile_order(self, order):
+        fn = self._lib.rt_debug_tile_order
+        fn.argtypes = [_P, _P, _I]
+        o = np.ascontiguousarray(order if order is not None else [], np.int32)
+        self._chk(fn(self._h, _ptr(o) if o.size else None, int(o.size)), "rt_debug_tile_order")
 
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull

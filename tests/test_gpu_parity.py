@@ -357,3 +357,26 @@ def test_walk_policies_identical(ctx, walk):
     finally:
         ctx.set_walk(1)
     check(img, ref, f"walk {walk}")
+
+
+@pytest.mark.gpu
+def test_cost_schedule_identical_images(ctx):
+    """rt_set_schedule: the cost-ordered dispatch (default) renders the same
+    image as row-major, frame after frame, and across a change of tile count."""
+    fs = rtamd.generate(3, 0, 320, 180)
+    ctx.upload(fs)
+    ctx.set_params(320, 180, 3, True)
+    ctx.set_kernel(rtamd.KERNEL_ACCEL)
+    ctx.set_schedule(rtamd.SCHED_ROWS)
+    ref = ctx.render(320, 180)
+    ctx.set_schedule(rtamd.SCHED_COST)
+    for _ in range(3):
+        assert np.array_equal(ctx.render(320, 180), ref)
+    band = ctx.render(320, 180)[40:120]
+    out = torch.zeros((80, 320, 4), dtype=torch.float32, device="cuda")
+    for _ in range(2):  # alternate tile counts: the order sets must stay consistent
+        ctx.dispatch_rows(320, 180, 40, 80, 1, 80, out.data_ptr(), 320 * 16)
+        ctx.sync()
+        assert np.array_equal(out.cpu().numpy(), band)
+        assert np.array_equal(ctx.render(320, 180), ref)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)

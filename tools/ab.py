@@ -28,6 +28,9 @@ VARIANTS = {
     "persistent": dict(kernel=3, wpb=1, persistent=True, walk=1),
     "nocone": dict(kernel=3, wpb=1, persistent=False, walk=1, cone=0),
     "packet": dict(kernel=2, wpb=4, persistent=False, walk=1),
+    "lpt": dict(kernel=3, wpb=1, persistent=False, walk=1, order="lpt"),
+    "rows": dict(kernel=3, wpb=1, persistent=False, walk=1, sched=0),
+    "lpt_rows": dict(kernel=3, wpb=1, persistent=False, walk=1, order="rows"),
     "stack20": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=20),
     "stack16": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=16),
 }
@@ -55,6 +58,22 @@ for key, path in (("", None), ("@2", a.lib2)):
 out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
 torch.cuda.synchronize()
 names = a.variants.split(",")
+tiles_n = ((W + 7) // 8) * ((H + 7) // 8)
+orders = {}
+if any(VARIANTS[n.partition("@")[0]].get("order") for n in names):
+    # longest-processing-time-first dispatch from one measured frame (diagnostics:
+    # the upper bound of what a cost-ordered dispatch can recover)
+    cx = ctxs[""]
+    cx.set_kernel(3)
+    cx.debug_tile_times(tiles_n)
+    cx.dispatch_rows(W, H, 0, 1, 1, H, torch.empty((H, W, 4), dtype=torch.float32, device="cuda").data_ptr(), W * 16)
+    tt = cx.tile_times(tiles_n).astype(np.int64)
+    cx.debug_tile_times(0)
+    d = tt[:, 1] - tt[:, 0]
+    orders["lpt"] = np.argsort(-d, kind="stable").astype(np.int32)
+    rowcost = d.reshape((H + 7) // 8, -1).sum(axis=1)
+    orders["rows"] = np.concatenate([np.arange(r * ((W + 7) // 8), (r + 1) * ((W + 7) // 8))
+                                     for r in np.argsort(-rowcost, kind="stable")]).astype(np.int32)
 
 
 def pick(n):
@@ -71,6 +90,10 @@ for rnd in range(a.rounds):
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
         ctx.debug_cone_cull(v.get("cone", 1))
+        if hasattr(ctx._lib, "rt_debug_tile_order"):
+            ctx.debug_tile_order(orders.get(v.get("order")))
+        if hasattr(ctx._lib, "rt_set_schedule"):
+            ctx.set_schedule(v.get("sched", 1))
         if hasattr(ctx._lib, "rt_debug_lane_stack"):
             ctx.debug_lane_stack(v.get("stack", 0))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
@@ -93,6 +116,10 @@ if a.times:
         ctx.set_launch(v["wpb"], v["persistent"])
         ctx.set_walk(v["walk"])
         ctx.debug_cone_cull(v.get("cone", 1))
+        if hasattr(ctx._lib, "rt_debug_tile_order"):
+            ctx.debug_tile_order(orders.get(v.get("order")))
+        if hasattr(ctx._lib, "rt_set_schedule"):
+            ctx.set_schedule(v.get("sched", 1))
         if hasattr(ctx._lib, "rt_debug_lane_stack"):
             ctx.debug_lane_stack(v.get("stack", 0))
         ctx.debug_tile_times(tiles)
@@ -125,3 +152,15 @@ if a.times:
         slow = np.argsort(dur)[::-1][:32]
         print("  slowest 32 tiles, share of wave cycles per walk:",
               (t[slow, 6:6 + 2 * mb].sum(axis=0) / max(t[slow, 6:6 + 2 * mb].sum(), 1)).round(3).tolist())
+        # concurrency profile: tiles in flight over the kernel's span, in 20 slices
+        span = float(end.max())
+        edges = np.linspace(0.0, span, 21)
+        live = [int(((start < b) & (end > a_)).sum()) for a_, b in zip(edges[:-1], edges[1:])]
+        print("  tiles in flight per 5% of span:", live)
+        busy = np.zeros(400)
+        grid = np.linspace(0.0, span, 401)
+        for s_, e_ in zip(start, end):
+            i0, i1 = np.searchsorted(grid, [s_, e_])
+            busy[max(i0 - 1, 0):i1] += 1
+        print("  mean tiles resident over span:", round(float(busy.mean()), 1),
+              " time with < 1000 / < 250 resident: %.0f%% / %.0f%%" % (100 * (busy < 1000).mean(), 100 * (busy < 250).mean()))
