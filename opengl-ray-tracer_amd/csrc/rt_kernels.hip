@@ -1539,6 +1539,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         e1 = c->ring1[c->ring_used];
     }
     if (!stats) HIP_TRY(hipEventRecord(e0, c->stream));
+    bool order_after = false;  // e1 already recorded between the render and the order kernel
     if (stats) {
         hipLaunchKernelGGL(k_lane<true>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
                            c->nodes, kp);
@@ -1595,7 +1596,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                           c->boxes_finite};
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
         if (k2.tile_cost) {
-            // the next frame's order; stream-ordered after this dispatch, before the next
+            // the next frame's order; stream-ordered after this dispatch (and after its
+            // end event, so rt_kernel_times is the render kernel alone), before the next
+            if (!stats) HIP_TRY(hipEventRecord(e1, c->stream));
+            order_after = true;
             unsigned* set = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
             unsigned* next = c->sched_sets + (1 - c->sched_parity) * sched_set_words(c->sched_cap);
             hipLaunchKernelGGL(k_tile_order, dim3((k2.tiles + kOrderThreads - 1) / kOrderThreads), dim3(kOrderThreads),
@@ -1611,7 +1615,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     c->last_kind = stats ? RT_KERNEL_LANE : kind;
     HIP_TRY(hipGetLastError());
     if (!stats) {
-        HIP_TRY(hipEventRecord(e1, c->stream));
+        if (!order_after) HIP_TRY(hipEventRecord(e1, c->stream));
         c->last0 = e0;
         c->last1 = e1;
         if (c->ring_used < static_cast<int>(c->ring0.size())) ++c->ring_used;
