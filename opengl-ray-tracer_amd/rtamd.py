@@ -456,6 +456,11 @@ class ComputeShader:
         o = np.ascontiguousarray(order if order is not None else [], np.int32)
         self._chk(fn(self._h, _ptr(o) if o.size else None, int(o.size)), "rt_debug_tile_order")
 
+    def debug_spec(self, mode):
+        fn = self._lib.rt_debug_spec
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(mode)), "rt_debug_spec")
+
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull
         fn.argtypes = [_P, _I]

@@ -30,6 +30,8 @@ VARIANTS = {
     "packet": dict(kernel=2, wpb=4, persistent=False, walk=1),
     "lpt": dict(kernel=3, wpb=1, persistent=False, walk=1, order="lpt"),
     "rows": dict(kernel=3, wpb=1, persistent=False, walk=1, sched=0),
+    "spec_on": dict(kernel=3, wpb=1, persistent=False, walk=1, spec=1),
+    "spec_off": dict(kernel=3, wpb=1, persistent=False, walk=1, spec=0),
     "lpt_rows": dict(kernel=3, wpb=1, persistent=False, walk=1, order="rows"),
     "stack20": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=20),
     "stack16": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=16),
@@ -94,6 +96,8 @@ for rnd in range(a.rounds):
             ctx.debug_tile_order(orders.get(v.get("order")))
         if hasattr(ctx._lib, "rt_set_schedule"):
             ctx.set_schedule(v.get("sched", 1))
+        if hasattr(ctx._lib, "rt_debug_spec"):
+            ctx.debug_spec(v.get("spec", 1))
         if hasattr(ctx._lib, "rt_debug_lane_stack"):
             ctx.debug_lane_stack(v.get("stack", 0))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
@@ -120,6 +124,8 @@ if a.times:
             ctx.debug_tile_order(orders.get(v.get("order")))
         if hasattr(ctx._lib, "rt_set_schedule"):
             ctx.set_schedule(v.get("sched", 1))
+        if hasattr(ctx._lib, "rt_debug_spec"):
+            ctx.debug_spec(v.get("spec", 1))
         if hasattr(ctx._lib, "rt_debug_lane_stack"):
             ctx.debug_lane_stack(v.get("stack", 0))
         ctx.debug_tile_times(tiles)
@@ -138,9 +144,9 @@ if a.times:
         print("  mean tile us by tile-row (every 10th):", per_row[::10].round(1).tolist())
         tx = (W + 7) // 8
         worst = np.argsort(dur)[::-1][:6]
-        print("  slowest tiles (x8, y8, us, nodes sum/max-lane, tests sum/max-lane):",
-              [(int(w % tx) * 8, int(w // tx) * 8, round(float(dur[w]), 1), int(t[w, 2]), int(t[w, 4]), int(t[w, 3]),
-                int(t[w, 5])) for w in worst])
+        print("  slowest tiles (x8, y8, us, nodes sum/max-lane/wave-iters, tests sum/max-lane/wave-iters):",
+              [(int(w % tx) * 8, int(w // tx) * 8, round(float(dur[w]), 1), int(t[w, 2]), int(t[w, 4]), int(t[w, 23]),
+                int(t[w, 3]), int(t[w, 5]), int(t[w, 22])) for w in worst])
         med = np.argsort(dur)[len(dur) // 2]
         print("  median tile:", (round(float(dur[med]), 1), int(t[med, 2]), int(t[med, 4]), int(t[med, 3]), int(t[med, 5])))
         print("  totals: nodes", int(t[:, 2].sum()), "tests", int(t[:, 3].sum()))
