@@ -3,14 +3,21 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--kernel auto]
 
-A step is one frame of the reference's GPU render loop (src/main.cpp:325-370):
-per-frame camera + light upload (SSBO 2/1), the render dispatch, completion,
-and for N > 1 the RCCL fan-in of every rank's rows to rank 0 (one process per
-GPU, launched by torch.distributed.run). Default workload: config 3, the car
-scene (4,022 triangles + 100 spheres, reference BVH with the 2-triangle road),
-1920x1080, maxBounces 3, barycentric, no Fresnel. All N ranks render one frame
-together (interleaved 8-row stripes), so the total work per step is fixed:
-scaling "strong".
+A step is one frame of the reference's GPU render loop (src/main.cpp:325-370)
+per GPU: per-frame camera + light upload (SSBO 2/1), the render dispatch and
+its completion (one process per GPU, launched by torch.distributed.run).
+Default workload: config 3, the car scene (4,022 triangles + 100 spheres,
+reference BVH with the 2-triangle road), 1920x1080, maxBounces 3, barycentric,
+no Fresnel.
+
+Multi-GPU (--mode): frames are independent units, so by default (weak) every
+rank renders its own 1920x1080 frame per step -- frame r of a camera orbit
+around the car, 1 degree per frame, rank 0 = the config's camera -- with no
+collective on the data path: the per-GPU work is fixed as N grows, scaling
+"weak". --mode strong instead splits ONE frame per step across the ranks
+(interleaved 8-row stripes) and gathers it to rank 0 over RCCL: total work
+fixed, scaling "strong" (the frame then ends with its slowest pixel paths,
+DESIGN.md §7).
 
 value = Mrays/s = (closest-hit + shadow rays of the frame, counted on the
 reference walk by the counting kernel) x frames / s, summed over the job.
@@ -56,6 +63,8 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="car road: 0 = 2-triangle quad, 1 = 222 strips")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet", "accel"])
     ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
+                    help="N > 1: weak = one frame per GPU (orbit), strong = one frame split over the GPUs + gather")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
@@ -106,8 +115,19 @@ def main():
     torch.cuda.set_stream(torch.cuda.Stream())
 
     cfg, W, H, mb, desc = WORKLOADS[a.config]
-    fs = rtamd.generate(cfg, a.variant, W, H)
-    sc_stats = rtamd.Scene().generate(cfg, a.variant, W / H).bvh_stats()
+    sc = rtamd.Scene().generate(cfg, a.variant, W / H)
+    sc_stats = sc.bvh_stats()
+    strong = a.mode == "strong" and world > 1
+    if not strong and rank > 0:
+        # frame `rank` of the orbit: the camera turned about the vertical axis through
+        # the look-at point (the origin) by `rank` degrees
+        cam0 = sc.serializeScene().camera
+        p = cam0["Position"][0].astype(np.float64)
+        ang = np.radians(float(rank))
+        pos = (p[0] * np.cos(ang) + p[2] * np.sin(ang), p[1], -p[0] * np.sin(ang) + p[2] * np.cos(ang))
+        sc.set_camera(pos, float(cam0["fov"][0]), float(cam0["aspectRatio"][0]))
+        sc.LookAt((0.0, 0.0, 0.0))
+    fs = sc.serializeScene()
 
     ctx = rtamd.ComputeShader(torch.cuda.current_device())
     ctx.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -115,19 +135,21 @@ def main():
     ctx.set_params(W, H, mb, True, False, False)
     ctx.set_kernel({"auto": 0, "lane": 1, "packet": 2, "accel": 3}[a.kernel])
 
-    plan = tiling.StripePlan(H, world, a.stripe)
-    rows = plan.rows(rank)
+    # strong: this rank's interleaved stripes of the one frame; weak: the rank's whole frame
+    plan = tiling.StripePlan(H, world if strong else 1, a.stripe)
+    prank = rank if strong else 0
+    rows = plan.rows(prank)
     buf = torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev)
 
     # Work of this rank's rows on the reference walk (counting kernel, untimed).
-    st = ctx.collect_stats(W, H, plan.y0(rank), a.stripe, world, rows)
+    st = ctx.collect_stats(W, H, plan.y0(prank), a.stripe, plan.world, rows)
     mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, rows * W), st["hits"]],
                         dtype=torch.float64, device=dev)
     total = mine.clone()
     if world > 1:
         total = total.cpu() if a.backend == "gloo" else total
         dist.all_reduce(total)
-    rays_frame = float(total[0] + total[1])
+    rays_step = float(total[0] + total[1])  # all ranks' rays of one step
     b_alg_rank = float(mine[2])
 
     cam, light = fs.camera, fs.light
@@ -135,8 +157,8 @@ def main():
     def frame():
         ctx.set_camera(cam)   # SSBO 2 (src/main.cpp:328-330)
         ctx.set_light(light)  # SSBO 1 (:332-334)
-        ctx.dispatch_rows(W, H, plan.y0(rank), a.stripe, world, rows, buf.data_ptr(), W * 16)
-        if world > 1:
+        ctx.dispatch_rows(W, H, plan.y0(prank), a.stripe, plan.world, rows, buf.data_ptr(), W * 16)
+        if strong:
             tiling.gather_to_root(buf, plan)
 
     for _ in range(a.warmup):
@@ -165,7 +187,8 @@ def main():
     k_med = float(np.median(kt)) if len(kt) else float("nan")
 
     if rank == 0:
-        fps = a.steps / elapsed
+        frames = a.steps * (1 if strong or world == 1 else world)
+        fps = frames / elapsed
         achieved = b_alg_rank / (k_ms * 1e-3) / 1e9
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -174,14 +197,14 @@ def main():
                 traffic = json.load(f).get(f"config{a.config}_n{world}_{a.kernel}")
         out = {
             "metric": METRIC,
-            "value": rays_frame * fps / 1e6,
+            "value": rays_step * a.steps / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (procedural stand-in meshes, fixed seed; the reference's .obj assets are absent)",
@@ -190,10 +213,11 @@ def main():
                        "width": W, "height": H, "maxBounces": mb, "useBVH": 1, "useFresnel": 0,
                        "triangle_test": "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
                        "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel,
-                       "parallelism": f"row-stripes{a.stripe}x{world}" + ("+rccl-gather" if world > 1 else "")},
+                       "parallelism": (f"row-stripes{a.stripe}x{world}+rccl-gather" if strong else
+                                       f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)")},
             "fps": fps,
             "mrays_primary_per_s": W * H * fps / 1e6,
-            "rays_per_frame": rays_frame,
+            "rays_per_step": rays_step,
             "kernel_ms_mean": k_ms,
             "kernel_ms_median": k_med,
             "roofline": {
