@@ -730,22 +730,50 @@ __device__ __forceinline__ void cas(Kids4& k, int i, int j) {
     k.code[j] = sw ? ci : cj;
 }
 
+// Two children per packed instruction (v_pk_fma_f32, v_pk_mul_f32): the same
+// fma / mul per component as rta::box_enter and rta::cone_culls.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+__device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f2 ly, f2 lz, f2 hx, f2 hy, f2 hz,
+                                          f2 ax, f2 ay, f2 az, f2 th, float& t0, float& t1, bool& h0, bool& h1) {
+    const f2 ix = {c.ix, c.ix}, iy = {c.iy, c.iy}, iz = {c.iz, c.iz};
+    const f2 ox = {-c.ox, -c.ox}, oy = {-c.oy, -c.oy}, oz = {-c.oz, -c.oz};
+    const f2 x0 = fma2(lx, ix, ox), x1 = fma2(hx, ix, ox);
+    const f2 y0 = fma2(ly, iy, oy), y1 = fma2(hy, iy, oy);
+    const f2 z0 = fma2(lz, iz, oz), z1 = fma2(hz, iz, oz);
+    const f2 dz = {c.dz, c.dz}, dy = {c.dy, c.dy}, dx = {c.dx, c.dx};
+    const f2 dn = fma2(ax, dx, fma2(ay, dy, az * dz));
+    const f2 thr = th - (f2){rta::kConeEps, rta::kConeEps};
+    float tn[2], tf[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        tn[k] = fmaxf(fmaxf(fminf(x0[k], x1[k]), fminf(y0[k], y1[k])), fmaxf(fminf(z0[k], z1[k]), 0.0f));
+        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), fminf(fmaxf(z0[k], z1[k]), tl));
+    }
+    t0 = tn[0];
+    t1 = tn[1];
+    h0 = (tn[0] <= tf[0]) & !(dn[0] < thr[0]);
+    h1 = (tn[1] <= tf[1]) & !(dn[1] < thr[1]);
+}
+
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
     const float4* q = A.lnodes + 11 * static_cast<size_t>(uc & 0x3fffffffu);
     const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
     const float4 ax = q[6], ay = q[7], az = q[8], th = q[9], cd = q[10];
-    const float l0[4] = {lx.x, lx.y, lx.z, lx.w}, l1[4] = {ly.x, ly.y, ly.z, ly.w}, l2[4] = {lz.x, lz.y, lz.z, lz.w};
-    const float h0[4] = {hx.x, hx.y, hx.z, hx.w}, h1[4] = {hy.x, hy.y, hy.z, hy.w}, h2[4] = {hz.x, hz.y, hz.z, hz.w};
-    const float a0[4] = {ax.x, ax.y, ax.z, ax.w}, a1[4] = {ay.x, ay.y, ay.z, ay.w}, a2[4] = {az.x, az.y, az.z, az.w};
-    const float tt[4] = {th.x, th.y, th.z, th.w};
     const int cc[4] = {__float_as_int(cd.x), __float_as_int(cd.y), __float_as_int(cd.z), __float_as_int(cd.w)};
+    float t[4];
+    bool h[4];
+    wide_pair(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y}, (f2){hy.x, hy.y},
+              (f2){hz.x, hz.y}, (f2){ax.x, ax.y}, (f2){ay.x, ay.y}, (f2){az.x, az.y}, (f2){th.x, th.y}, t[0], t[1],
+              h[0], h[1]);
+    wide_pair(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w}, (f2){hy.z, hy.w},
+              (f2){hz.z, hz.w}, (f2){ax.z, ax.w}, (f2){ay.z, ay.w}, (f2){az.z, az.w}, (f2){th.z, th.w}, t[2], t[3],
+              h[2], h[3]);
     Kids4 k;
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
-        float te;
-        const bool h = rta::box_enter(c, l0[s2], l1[s2], l2[s2], h0[s2], h1[s2], h2[s2], tl, te) &
-                       !rta::cone_culls(c, a0[s2], a1[s2], a2[s2], tt[s2]) & (cc[s2] != kNoChild) & in;
-        k.t[s2] = h ? te : INFINITY;
+        k.t[s2] = (h[s2] & (cc[s2] != kNoChild) & in) ? t[s2] : INFINITY;
         k.code[s2] = cc[s2];
     }
     return k;
