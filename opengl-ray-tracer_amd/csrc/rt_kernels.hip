@@ -1078,11 +1078,16 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
 template <bool COUNT, bool SPEC>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
-    const PixelCoord pc = tile_pixel(kp, tile);
-    const V bg = background(kp, pc.y);
-    Ray ray = primary_ray(kp, pc.x, pc.y);
+    // Pixel coordinates and the background are recomputed where needed rather than
+    // kept live through the walks (register pressure: they would be spilled).
+    Ray ray;
+    bool alive;
+    {
+        const PixelCoord pc = tile_pixel(kp, tile);
+        ray = primary_ray(kp, pc.x, pc.y);
+        alive = pc.active;
+    }
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
-    bool alive = pc.active;
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
         Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
@@ -1096,17 +1101,15 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
             packet_walk<false, true, COUNT>(A, ray, alive, 0.f, best, unused, wc);
         if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
         if (alive && best.slot < 0) {
-            acc = acc + mulv(att, bg);
+            acc = acc + mulv(att, background(kp, tile_pixel(kp, tile).y));
             alive = false;
         }
-        V hn = mk(0.f, 0.f, 0.f);
-        Mat m{};
+        // The shadow ray; the hit's normal and material are fetched again after the
+        // shadow walk rather than kept live through it (register pressure).
         Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
         float ld = 0.f;
         if (alive) {
-            const GeoRec g = load_rec(A.prims, best.slot);
-            hn = shape_normal(g, best.p);
-            m = load_mat(mat, g.idx);
+            const V hn = shape_normal(load_rec(A.prims, best.slot), best.p);
             sr = Ray{best.p + hn * 1e-3f, normalize(kp.light_pos - best.p)};
             ld = dist(kp.light_pos, best.p);
         }
@@ -1119,8 +1122,13 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         else
             packet_walk<true, true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
-        if (alive) alive = shade_bounce(kp, ray, best.p, hn, m, shadow, acc, att, 1e-3f);
+        if (alive) {
+            const GeoRec g = load_rec(A.prims, best.slot);
+            alive = shade_bounce(kp, ray, best.p, shape_normal(g, best.p), load_mat(mat, g.idx), shadow, acc, att,
+                                 1e-3f);
+        }
     }
+    const PixelCoord pc = tile_pixel(kp, tile);
     if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
 }
 
