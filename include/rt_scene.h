@@ -2,7 +2,7 @@
  * rt_scene.h — C ABI of the host scene library (librtscene.so).
  *
  * The CPU side of the reference's hot path, restated in C++: the shape set
- * (src/shapes/*.hpp), Material/Light/Camera (src/material.hpp, src/light.hpp,
+ * (src/shapes/{sphere,plane,wall,triangle}.hpp), Material/Light/Camera (src/material.hpp, src/light.hpp,
  * src/camera.hpp), the spatial-midpoint BVH builder (split/buildBVH,
  * src/main.cpp:1111-1193, src/BoundingBox.hpp) and the serialisers that fill
  * the Flat* records (serializeShape/serializeBVH/serializeCamera/serializeLight,
@@ -55,6 +55,23 @@ int rts_add_mesh(struct rts_scene* s, const float* vertices, int num_vertices,
 int rts_add_mesh_oriented(struct rts_scene* s, const float* vertices, int num_vertices,
                           const unsigned* indices, int num_indices, const float* origin,
                           const FlatMaterial* mat);
+
+/* Wavefront OBJ ingestion, replacing assimp (src/model.hpp:49-168): vertex
+ * positions and faces (polygons split as a fan from their first corner, as
+ * aiProcess_Triangulate does for convex faces) become one mesh, added like
+ * rts_add_mesh (oriented != 0: like rts_add_mesh_oriented). Returns the number
+ * of triangles added, -1 invalid argument, -2 I/O error, -3 malformed file. */
+int rts_load_obj(struct rts_scene* s, const char* path, const float* origin, const FlatMaterial* mat,
+                 int oriented);
+int rts_parse_obj(struct rts_scene* s, const char* text, long len, const float* origin,
+                  const FlatMaterial* mat, int oriented);
+
+/* Image dump, replacing the screen quad (src/main.cpp:476-501, shaders/shader.frag):
+ * an RGBA32F image (row 0 = NDC y +1, pitch in bytes) written as binary PPM
+ * (rgb clamped to [0,1], 8 bits) or colour PFM (float rgb, exact). 0 or -1
+ * (invalid argument) / -2 (I/O error). */
+enum { RTS_IMAGE_PPM = 0, RTS_IMAGE_PFM = 1 };
+int rts_write_image(const char* path, const float* rgba, int width, int height, long pitch_bytes, int format);
 
 /* Camera() then Position/aspect/fov, and Camera::LookAt (src/camera.hpp:124-163). */
 int rts_set_camera(struct rts_scene* s, const float* position, float fov_deg, float aspect);

@@ -10,10 +10,13 @@
 // the reference's IEEE sequence.
 #include "../../include/rt_scene.h"
 
+#include <cerrno>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 namespace {
@@ -630,6 +633,138 @@ int rts_add_mesh(rts_scene* s, const float* v, int nv, const unsigned* idx, int 
 int rts_add_mesh_oriented(rts_scene* s, const float* v, int nv, const unsigned* idx, int ni,
                           const float* origin, const FlatMaterial* mat) {
     return add_mesh(s, v, nv, idx, ni, origin, mat, true);
+}
+
+// ---------------------------------------------------------------------------
+// Wavefront OBJ ingestion (replaces assimp's loader,
+// src/model.hpp:49-168). Vertex positions ("v x y z [w]") and faces
+// ("f a b c ...", each corner "i", "i/t", "i//n" or "i/t/n"; negative indices
+// count back from the last vertex read) are kept; texture coordinates, normals,
+// groups, objects and materials are ignored, as they do not reach the ray
+// tracer's FlatShape records. A face of k corners becomes the fan
+// (0,1,2), (0,2,3), ..., (0,k-2,k-1), aiProcess_Triangulate's split of a convex
+// polygon. The whole file is one mesh: Mesh::mesh2triangles with `origin`
+// added to every vertex (src/mesh.hpp:163-189), and the normal flip applied
+// only if `oriented` (generateScene1/2 drop it, see add_mesh).
+namespace {
+
+int parse_obj(rts_scene* s, const char* text, size_t len, const float* origin, const FlatMaterial* mat, bool oriented) {
+    std::vector<float> v;
+    std::vector<unsigned> idx;
+    std::vector<long> face;
+    size_t pos = 0;
+    int line_no = 0;
+    while (pos < len) {
+        size_t end = pos;
+        while (end < len && text[end] != '\n') ++end;
+        std::string line(text + pos, end - pos);
+        pos = end + 1;
+        ++line_no;
+        if (!line.empty() && line.back() == '\r') line.pop_back();
+        const char* c = line.c_str();
+        while (*c == ' ' || *c == '\t') ++c;
+        if (c[0] == 'v' && (c[1] == ' ' || c[1] == '\t')) {
+            char* e = nullptr;
+            float xyz[3];
+            const char* q = c + 2;
+            for (int k = 0; k < 3; ++k) {
+                errno = 0;
+                xyz[k] = std::strtof(q, &e);
+                if (e == q || errno == ERANGE) return -3;
+                q = e;
+            }
+            v.insert(v.end(), xyz, xyz + 3);
+        } else if (c[0] == 'f' && (c[1] == ' ' || c[1] == '\t')) {
+            face.clear();
+            const char* q = c + 2;
+            const long nv = static_cast<long>(v.size() / 3);
+            for (;;) {
+                while (*q == ' ' || *q == '\t') ++q;
+                if (!*q) break;
+                char* e = nullptr;
+                const long i = std::strtol(q, &e, 10);
+                if (e == q) return -3;
+                const long r = i > 0 ? i - 1 : nv + i;  // 1-based, or relative to the last vertex
+                if (i == 0 || r < 0 || r >= nv) return -3;
+                face.push_back(r);
+                q = e;
+                while (*q && *q != ' ' && *q != '\t') ++q;  // skip "/t/n"
+            }
+            if (face.size() < 3) return -3;
+            for (size_t k = 1; k + 1 < face.size(); ++k) {
+                idx.push_back(static_cast<unsigned>(face[0]));
+                idx.push_back(static_cast<unsigned>(face[k]));
+                idx.push_back(static_cast<unsigned>(face[k + 1]));
+            }
+        }
+    }
+    if (idx.empty()) return 0;
+    const int first = add_mesh(s, v.data(), static_cast<int>(v.size() / 3), idx.data(), static_cast<int>(idx.size()),
+                               origin, mat, oriented);
+    return first < 0 ? first : static_cast<int>(idx.size() / 3);
+}
+
+}  // namespace
+
+int rts_parse_obj(rts_scene* s, const char* text, long len, const float* origin, const FlatMaterial* mat,
+                  int oriented) {
+    if (!s || (!text && len > 0) || len < 0) return -1;
+    return parse_obj(s, text, static_cast<size_t>(len), origin, mat, oriented != 0);
+}
+
+int rts_load_obj(rts_scene* s, const char* path, const float* origin, const FlatMaterial* mat, int oriented) {
+    if (!s || !path) return -1;
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return -2;
+    std::string text;
+    char buf[1 << 16];
+    size_t n;
+    while ((n = std::fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, n);
+    const bool err = std::ferror(f) != 0;
+    std::fclose(f);
+    if (err) return -2;
+    return parse_obj(s, text.data(), text.size(), origin, mat, oriented != 0);
+}
+
+// ---------------------------------------------------------------------------
+// Image dump (replaces the screen quad, src/main.cpp:476-501,
+// shader.frag, which shows the RGBA32F texture's rgb). Rows are written in
+// image order, row 0 first = NDC y +1, the top of the camera's view.
+// RTS_IMAGE_PPM: binary P6, each channel clamped to [0, 1] and rounded to 8 bits.
+// RTS_IMAGE_PFM: colour PFM ("PF"), the float rgb exactly; PFM stores the
+// bottom row first, so the file's first row is image row h-1.
+int rts_write_image(const char* path, const float* rgba, int w, int h, long pitch_bytes, int format) {
+    if (!path || !rgba || w <= 0 || h <= 0 || pitch_bytes < 16L * w || (format != RTS_IMAGE_PPM && format != RTS_IMAGE_PFM))
+        return -1;
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return -2;
+    bool ok = true;
+    auto row = [&](int y) { return reinterpret_cast<const float*>(reinterpret_cast<const char*>(rgba) + y * pitch_bytes); };
+    if (format == RTS_IMAGE_PPM) {
+        ok = std::fprintf(f, "P6\n%d %d\n255\n", w, h) > 0;
+        std::vector<unsigned char> line(3 * static_cast<size_t>(w));
+        for (int y = 0; y < h && ok; ++y) {
+            const float* r = row(y);
+            for (int x = 0; x < w; ++x)
+                for (int k = 0; k < 3; ++k) {
+                    float c = r[4 * x + k];
+                    c = c > 0.f ? (c < 1.f ? c : 1.f) : 0.f;  // NaN -> 0
+                    line[3 * x + k] = static_cast<unsigned char>(std::lround(c * 255.f));
+                }
+            ok = std::fwrite(line.data(), 1, line.size(), f) == line.size();
+        }
+    } else {
+        ok = std::fprintf(f, "PF\n%d %d\n-1.0\n", w, h) > 0;  // negative scale: little endian
+        std::vector<float> line(3 * static_cast<size_t>(w));
+        for (int y = h - 1; y >= 0 && ok; --y) {
+            const float* r = row(y);
+            for (int x = 0; x < w; ++x)
+                for (int k = 0; k < 3; ++k) line[3 * x + k] = r[4 * x + k];
+            ok = std::fwrite(line.data(), sizeof(float), line.size(), f) == line.size();
+        }
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? 0 : -2;
 }
 
 int rts_set_camera(rts_scene* s, const float* position, float fov_deg, float aspect) {

@@ -168,6 +168,9 @@ SCENE_SYMBOLS = {
     "rts_serialize": (_I, [_P, _P, _P, _P, _P, _P]),
     "rts_bvh_stats": (_I, [_P, _P, _P, _P, _P]),
     "rts_generate": (_I, [_P, _I, _I, C.c_float]),
+    "rts_load_obj": (_I, [_P, C.c_char_p, _P, _P, _I]),
+    "rts_parse_obj": (_I, [_P, C.c_char_p, C.c_long, _P, _P, _I]),
+    "rts_write_image": (_I, [C.c_char_p, _P, _I, _I, C.c_long, _I]),
 }
 
 RT_SYMBOLS = {
@@ -294,6 +297,16 @@ class Scene:
         fn = self._lib.rts_add_mesh_oriented if oriented else self._lib.rts_add_mesh
         return self._chk(fn(self._h, _ptr(v), len(v), _ptr(i), len(i), _f3(origin), self._mat(mat)), "add_mesh")
 
+    def load_obj(self, path, origin=(0, 0, 0), mat=None, oriented=False):
+        """Wavefront OBJ file -> triangles (rts_load_obj); returns the triangle count."""
+        return self._chk(self._lib.rts_load_obj(self._h, os.fsencode(path), _f3(origin), self._mat(mat),
+                                                int(bool(oriented))), "load_obj")
+
+    def parse_obj(self, text, origin=(0, 0, 0), mat=None, oriented=False):
+        b = text.encode() if isinstance(text, str) else bytes(text)
+        return self._chk(self._lib.rts_parse_obj(self._h, b, len(b), _f3(origin), self._mat(mat),
+                                                 int(bool(oriented))), "parse_obj")
+
     def set_camera(self, position, fov=60.0, aspect=1.0):
         self._chk(self._lib.rts_set_camera(self._h, _f3(position), fov, aspect), "set_camera")
 
@@ -330,6 +343,19 @@ class Scene:
         self._chk(self._lib.rts_serialize(self._h, _ptr(shapes), _ptr(nodes), _ptr(idx), _ptr(cam), _ptr(light)),
                   "serializeScene")
         return FlatScene(shapes, nodes, idx, cam, light)
+
+
+IMAGE_PPM, IMAGE_PFM = 0, 1
+
+
+def write_image(path, img, fmt=IMAGE_PPM):
+    """[H, W, 4] float32 image (row 0 = NDC y +1) -> binary PPM (clamped, 8-bit) or PFM (exact)."""
+    a = np.ascontiguousarray(img, np.float32)
+    if a.ndim != 3 or a.shape[2] != 4:
+        raise ValueError("write_image expects [H, W, 4] float32")
+    rc = scene_lib().rts_write_image(os.fsencode(path), _ptr(a), a.shape[1], a.shape[0], a.shape[1] * 16, int(fmt))
+    if rc != 0:
+        raise RTError("rts_write_image", rc)
 
 
 def generate(config, variant=0, width=1920, height=1080) -> FlatScene:

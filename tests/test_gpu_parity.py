@@ -380,3 +380,32 @@ def test_cost_schedule_identical_images(ctx):
         assert np.array_equal(out.cpu().numpy(), band)
         assert np.array_equal(ctx.render(320, 180), ref)
     ctx.set_kernel(rtamd.KERNEL_AUTO)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", [rtamd.KERNEL_ACCEL, rtamd.KERNEL_PACKET])
+def test_obj_scene_parity(ctx, kernel):
+    """A scene read from OBJ text (rts_parse_obj: a subdivided sphere-ish blob
+    of quads and triangles, plus a floor) renders like the oracle."""
+    lines, k = [], 12
+    for i in range(k + 1):
+        th = np.pi * i / k
+        for j in range(2 * k):
+            ph = np.pi * j / k
+            lines.append(f"v {np.sin(th) * np.cos(ph) * 3:.6f} {np.cos(th) * 3:.6f} {np.sin(th) * np.sin(ph) * 3:.6f}")
+    for i in range(k):
+        for j in range(2 * k):
+            a, b = i * 2 * k + j + 1, i * 2 * k + (j + 1) % (2 * k) + 1
+            lines.append(f"f {a} {b} {b + 2 * k} {a + 2 * k}")
+    sc = rtamd.Scene()
+    assert sc.parse_obj("\n".join(lines), origin=(0, 0, -5), oriented=True) == 2 * k * 2 * k
+    sc.add_plane((0, 1, 0), (0, 4, 0))
+    sc.set_camera((6, -4, 10), 60, 4 / 3)
+    sc.LookAt((0, 0, -5))
+    sc.set_light((5, -10, 5), (1, 1, 1), 30)
+    sc.buildBVH(15)
+    fs = sc.serializeScene()
+    W, H = 128, 96
+    p = oracle.params(W, H, 3)
+    ref, _ = oracle.render(fs, W, H, p)
+    check(gpu_rows(ctx, fs, W, H, p, kernel=kernel), ref, f"obj kernel{kernel}")
