@@ -1,6 +1,7 @@
 // accel.cpp — host-side builder of the exact-result accelerator. See accel.h
 // for the contract; the bounds below are what makes skipping a shape safe.
 #include "accel.h"
+#include "accel_bound.h"
 
 #include <algorithm>
 #include <cmath>
@@ -10,72 +11,6 @@
 
 namespace rta {
 namespace {
-
-struct D3 {
-    double x, y, z;
-};
-inline D3 d3(rt_vec3 v) { return D3{v.x, v.y, v.z}; }
-inline D3 operator+(D3 a, D3 b) { return D3{a.x + b.x, a.y + b.y, a.z + b.z}; }
-inline D3 operator-(D3 a, D3 b) { return D3{a.x - b.x, a.y - b.y, a.z - b.z}; }
-inline D3 operator*(D3 a, double s) { return D3{a.x * s, a.y * s, a.z * s}; }
-inline double dot(D3 a, D3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-inline D3 cross(D3 a, D3 b) { return D3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
-inline bool finite3(D3 a) { return std::isfinite(a.x) && std::isfinite(a.y) && std::isfinite(a.z); }
-inline double maxabs(D3 a) { return std::max({std::fabs(a.x), std::fabs(a.y), std::fabs(a.z)}); }
-
-// float normalize exactly as the kernels do it (only used to rebuild the
-// wall basis; the box is then padded, so bit-exactness is not required).
-inline void fnormalize(float v[3]) {
-    float s = 1.0f / std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-    v[0] *= s;
-    v[1] *= s;
-    v[2] *= s;
-}
-
-struct BoxAcc {
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    void add(D3 p) {
-        const double v[3] = {p.x, p.y, p.z};
-        for (int i = 0; i < 3; ++i) {
-            lo[i] = std::min(lo[i], v[i]);
-            hi[i] = std::max(hi[i], v[i]);
-        }
-    }
-    Box3 padded(double pad) const {
-        Box3 b;
-        for (int i = 0; i < 3; ++i) {
-            // round outwards after padding
-            b.lo[i] = std::nextafter(static_cast<float>(lo[i] - pad), -INFINITY);
-            b.hi[i] = std::nextafter(static_cast<float>(hi[i] + pad), INFINITY);
-        }
-        return b;
-    }
-    double extent() const { return std::max({hi[0] - lo[0], hi[1] - lo[1], hi[2] - lo[2]}); }
-    double mag() const {
-        double m = 0;
-        for (int i = 0; i < 3; ++i) m = std::max({m, std::fabs(lo[i]), std::fabs(hi[i])});
-        return m;
-    }
-};
-
-// Relative padding: float error of every quantity the reference test computes
-// is ~1e-7 of the coordinates' magnitude (1e-3 of it for the barycentric
-// solve on the thinnest triangle admitted); 1e-3 of (size + magnitude) covers
-// them with room, for ray origins up to AccelHost::origin_lim.
-//
-// A plane-based hit point computed from a ray with origin o lies within
-// ~4u(|D| + |o|) of the plane (u = 2^-24) and its projection inside the shape,
-// wherever the rounding puts it along a grazing ray, so those bounds hold for
-// any such origin. The sphere root does not: D = bb^2 - 4*aa*cc cancels, and
-// the computed point lies within sqrt(r^2 + k*L^2) of the centre, L = |o - c|
-// (measured: k <= 4.4e-7, from L = 10 to 1e4). Spheres get that extra margin
-// with kSphereErr = 4e-6 and the largest L an accelerated origin can have.
-constexpr double kPadRel = 1e-3;
-constexpr double kMinSin2 = 1e-3;     // thinnest triangle bounded (sin^2 of its corner angle)
-constexpr double kSphereErr = 4e-6;   // k of the sphere-root error above, with room
-constexpr double kOriginRel = 4.0;    // origin_lim = kOriginRel * (scene magnitude + 1)
-
-Box3 finish(const BoxAcc& acc) { return acc.padded(kPadRel * (acc.extent() + acc.mag() + 1.0) + 1e-6); }
 
 Box3 empty_box() {
     Box3 b;
@@ -97,77 +32,6 @@ float area(const Box3& b) {
     float e[3];
     for (int i = 0; i < 3; ++i) e[i] = std::max(0.f, b.hi[i] - b.lo[i]);
     return e[0] * e[1] + e[1] * e[2] + e[2] * e[0];
-}
-
-enum { UNBOUNDED = 0, BOUNDED = 1, NEVER = 2 };
-
-// 0: no finite bound; 1: bounded; 2: the reference test never returns INNER.
-// origin_lim: largest |coordinate| of a ray origin the bound must hold for.
-int classify(const FlatShape& s, Box3& out, double origin_lim) {
-    BoxAcc acc;
-    switch (s.type) {
-        case RT_SPHERE: {
-            D3 c = d3(s.sphereCenter);
-            double r = std::fabs(static_cast<double>(s.sphereRadius));
-            if (!finite3(c) || !std::isfinite(r)) return UNBOUNDED;
-            const double L = std::sqrt(3.0) * origin_lim + std::sqrt(dot(c, c));
-            const double R = std::sqrt(r * r + kSphereErr * L * L);
-            acc.add(c - D3{R, R, R});
-            acc.add(c + D3{R, R, R});
-            out = finish(acc);
-            return BOUNDED;
-        }
-        case RT_WALL: {
-            float n[3] = {s.planeNormal.x, s.planeNormal.y, s.planeNormal.z};
-            // the intersection basis of gpu_shader.comp:305-307
-            float u[3] = {n[1] * 0.f - 1.f * n[2], n[2] * 0.f - 0.f * n[0], n[0] * 1.f - 0.f * n[1]};
-            fnormalize(u);
-            if (std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]) < 1e-5f) {  // NaN stays NaN (:306)
-                float u2[3] = {n[1] * 0.f - 0.f * n[2], n[2] * 1.f - 0.f * n[0], n[0] * 0.f - 1.f * n[1]};
-                std::memcpy(u, u2, sizeof u);
-                fnormalize(u);
-            }
-            D3 N{n[0], n[1], n[2]}, U{u[0], u[1], u[2]};
-            D3 V = cross(N, U);
-            double vl = std::sqrt(dot(V, V));
-            if (!finite3(U) || !(vl > 0) || !std::isfinite(vl)) return UNBOUNDED;  // ±Y: NaN basis, never rejected
-            V = V * (1.0 / vl);
-            D3 st = d3(s.wallStart);
-            double nn = dot(N, N), W = s.wallWidth, H = s.wallHeight, D = s.planeD;
-            if (!finite3(st) || !(nn > 0) || !std::isfinite(W) || !std::isfinite(H) || !std::isfinite(D))
-                return UNBOUNDED;
-            D3 c0 = st - N * ((dot(N, st) + D) / nn);  // start projected on the stored plane
-            acc.add(c0);
-            acc.add(c0 + U * W);
-            acc.add(c0 + V * H);
-            acc.add(c0 + U * W + V * H);
-            out = finish(acc);
-            return BOUNDED;
-        }
-        case RT_TRIANGLE: {
-            D3 p1 = d3(s.triP1), p2 = d3(s.triP2), p3 = d3(s.triP3), N = d3(s.planeNormal);
-            double D = s.planeD;
-            if (!finite3(p1) || !finite3(p2) || !finite3(p3) || !finite3(N) || !std::isfinite(D)) return UNBOUNDED;
-            D3 e1 = p2 - p1, e2 = p3 - p1, cr = cross(e1, e2);
-            double d00 = dot(e1, e1), d11 = dot(e2, e2), c2 = dot(cr, cr);
-            if (!(d00 > 0) || !(d11 > 0) || !(c2 >= kMinSin2 * d00 * d11)) return UNBOUNDED;  // thin: error unbounded
-            D3 nt = cr * (1.0 / std::sqrt(c2));
-            double nl = std::sqrt(dot(N, N));
-            if (std::fabs(nl - 1.0) > 1e-3 || std::fabs(dot(N, nt)) < nl * (1.0 - 1e-4)) return UNBOUNDED;
-            double mag = std::max({maxabs(p1), maxabs(p2), maxabs(p3)}) + 1.0;
-            for (D3 p : {p1, p2, p3})
-                if (std::fabs(dot(N, p) + D) > 1e-4 * mag) return UNBOUNDED;  // stored plane off the vertices
-            acc.add(p1);
-            acc.add(p2);
-            acc.add(p3);
-            out = finish(acc);
-            return BOUNDED;
-        }
-        case RT_PLANE:
-            return UNBOUNDED;
-        default:
-            return NEVER;  // get_intersection has no branch for it (gpu_shader.comp:246-325)
-    }
 }
 
 struct Item {

@@ -25,12 +25,9 @@
 #include <vector>
 
 #include "../../include/rt_flat.h"
+#include "accel_bound.h"
 
 namespace rta {
-
-struct Box3 {
-    float lo[3], hi[3];
-};
 
 struct AccelHost {
     // prims: the shapes in the order the accelerated kernel reads them.

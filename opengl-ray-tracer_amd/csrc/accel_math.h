@@ -21,6 +21,7 @@
 #include <cmath>
 
 #if defined(__HIP__)
+#include <hip/hip_runtime.h>
 #define RTA_HD __host__ __device__ __forceinline__
 #else
 #define RTA_HD inline
