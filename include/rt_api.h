@@ -101,6 +101,32 @@ int rt_update_shapes(struct rt_ctx* ctx, int first, int count, const FlatShape* 
 /* Re-upload of all nodes with the same topology (src/main.cpp:340-345, updateBVH). */
 int rt_update_nodes(struct rt_ctx* ctx, const FlatNode* nodes, int num_nodes);
 
+/* Device-side animation. Replaces the reference's
+ * per-frame CPU path: updateScene + updateBVH + serializeBVH + the two
+ * glBufferSubData calls (src/main.cpp:336-346, 981-992, 1068-1077).
+ *
+ * rt_set_animated marks the shapes the host animates: the reference's
+ * animatedIndices / Shape::animated (src/main.cpp:120, 600-616, 706-708).
+ * ids must be distinct and in [0, num_shapes); count 0 clears the set.
+ * The set holds until the next rt_upload_scene.
+ *
+ * rt_animate uploads their new records: shapes[i] is shape ids[i]. On the
+ * device it then grows every node whose shape set lists an animated shape to
+ * include the shape, exactly as updateBVH does. That means the leaf and every
+ * node above it, growToInclude (src/BoundingBox.hpp:44-95), grow-only.
+ * The accelerator's conservative boxes grow along with the node boxes.
+ * A moved shape whose kind of bound changes triggers a host rebuild of the
+ * accelerator. Examples: a triangle that becomes too thin to bound, or a
+ * sphere whose radius becomes infinite. The frame is identical either way.
+ * The host array may be reused when the call returns. RT_ERR_INVALID if no
+ * set is marked.
+ *
+ * rt_read_nodes copies the current node records to the host, including the
+ * boxes rt_animate grew. num_nodes must match the scene's node count. */
+int rt_set_animated(struct rt_ctx* ctx, const int* ids, int count);
+int rt_animate(struct rt_ctx* ctx, const FlatShape* shapes);
+int rt_read_nodes(struct rt_ctx* ctx, FlatNode* nodes, int num_nodes);
+
 /* SSBO 2 and 1 (src/main.cpp:328-334). */
 int rt_set_camera(struct rt_ctx* ctx, const FlatCamera* camera);
 int rt_set_light(struct rt_ctx* ctx, const FlatLight* light);

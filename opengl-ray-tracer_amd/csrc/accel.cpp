@@ -317,8 +317,7 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
                 out.scene_mag = std::max({out.scene_mag, std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
     }
     out.origin_lim = static_cast<float>(kOriginRel * (out.scene_mag + 1.0));
-    for (int i = 0; i < S; ++i)
-        if (shapes[i].type == RT_SPHERE) scls[i] = classify(shapes[i], sbox[i], out.origin_lim);
+    for (int i = 0; i < S; ++i) scls[i] = classify(shapes[i], sbox[i], out.origin_lim);
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).

@@ -18,6 +18,12 @@
 // the computed point lies within sqrt(r^2 + k*L^2) of the centre, L = |o - c|
 // (measured: k <= 4.4e-7, from L = 10 to 1e4). Spheres get that extra margin
 // with kSphereErr = 4e-6 and the largest L an accelerated origin can have.
+//
+// Origin-relative error: the padded slab test (accel_math.h) errs by about
+// u*|o| in space, and a plane-based hit point by about 4u*|o|; for a small
+// shape far from the largest origin that exceeds the size-relative padding, so
+// every box also gets kOriginErr * origin_lim (~8x the ~5e-7 * origin_lim of
+// both errors together, for |o| up to sqrt(3) * origin_lim).
 #pragma once
 
 #include <math.h>
@@ -35,6 +41,7 @@ constexpr double kPadRel = 1e-3;
 constexpr double kMinSin2 = 1e-3;    // thinnest triangle bounded (sin^2 of its corner angle)
 constexpr double kSphereErr = 4e-6;  // k of the sphere-root error above, with room
 constexpr double kOriginRel = 4.0;   // origin_lim = kOriginRel * (scene magnitude + 1)
+constexpr double kOriginErr = 4e-6;  // padding per unit of origin_lim (origin-relative error above)
 
 enum { UNBOUNDED = 0, BOUNDED = 1, NEVER = 2 };
 
@@ -91,11 +98,14 @@ struct BoxAcc {
     }
 };
 
-RTA_HD Box3 finish(const BoxAcc& acc) { return acc.padded(kPadRel * (acc.extent() + acc.mag() + 1.0) + 1e-6); }
+RTA_HD Box3 finish(const BoxAcc& acc, double origin_lim) {
+    return acc.padded(kPadRel * (acc.extent() + acc.mag() + 1.0) + kOriginErr * origin_lim + 1e-6);
+}
 
 // UNBOUNDED: no finite bound; BOUNDED: `out` is set; NEVER: the reference test
 // never returns INNER. origin_lim: largest |coordinate| of a ray origin the
-// bound must hold for (the sphere margin; 0 for the build's first pass).
+// bound must hold for (0 for the build's first pass, which only measures the
+// scene's magnitude).
 RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
     BoxAcc acc;
     switch (s.type) {
@@ -107,7 +117,7 @@ RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
             const double R = sqrt(r * r + kSphereErr * L * L);
             acc.add(c - D3{R, R, R});
             acc.add(c + D3{R, R, R});
-            out = finish(acc);
+            out = finish(acc, origin_lim);
             return BOUNDED;
         }
         case RT_WALL: {
@@ -134,7 +144,7 @@ RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
             acc.add(c0 + U * W);
             acc.add(c0 + V * H);
             acc.add(c0 + U * W + V * H);
-            out = finish(acc);
+            out = finish(acc, origin_lim);
             return BOUNDED;
         }
         case RT_TRIANGLE: {
@@ -154,7 +164,7 @@ RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
             acc.add(p1);
             acc.add(p2);
             acc.add(p3);
-            out = finish(acc);
+            out = finish(acc, origin_lim);
             return BOUNDED;
         }
         case RT_PLANE:

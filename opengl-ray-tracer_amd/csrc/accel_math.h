@@ -8,8 +8,9 @@
 // the distance limit carries a 0.2 % margin, and the cone thresholds carry
 // 2 mrad. The float error of the fused forms below is orders of magnitude
 // smaller than those margins for every ray they are used on:
-//   * slab: t = fma(lo, inv, -o*inv). Its error is about 6e-8*|o| in space.
-//     That is below the padding when |o| <= origin_lim (AccelHost).
+//   * slab: t = fma(lo, inv, -o*inv). Its error is about 6e-8*|o| in space,
+//     below the kOriginErr*origin_lim part of every box's padding
+//     (accel_bound.h) when |o| <= origin_lim (AccelHost).
 //   * |inv| is clamped to kInvCap. A hit at parameter t on a clamped axis
 //     then still lies inside the slab, because pad*kInvCap >= 1e17 > 2t for
 //     unit-length directions (0.5 <= |d| <= 2) and such origins.

@@ -57,15 +57,8 @@ enum {
 // ---------------------------------------------------------------------------
 // Pack kernels
 
-__global__ void k_pack_shapes(const FlatShape* __restrict__ src, int S, const int* __restrict__ idx, int I,
-                              float4* __restrict__ geo_lin, float4* __restrict__ geo_leaf,
-                              float4* __restrict__ mat) {
-    int j = blockIdx.x * blockDim.x + threadIdx.x;
-    int total = S + I;
-    if (j >= total) return;
-    const bool leaf_slot = j >= S;
-    const int si = leaf_slot ? idx[j - S] : j;
-    const FlatShape& s = src[si];
+// The ray-independent part of a shape's intersection record (GeoRec).
+__device__ GeoRec pack_geo(const FlatShape& s, int si) {
     GeoRec g;
     for (int k = 0; k < 18; ++k) g.f[k] = 0.f;
     g.type = s.type;
@@ -98,15 +91,32 @@ __global__ void k_pack_shapes(const FlatShape* __restrict__ src, int S, const in
             g.f[16] = d00 * d11 - d01 * d01;
         }
     }
-    float4* out = leaf_slot ? geo_leaf + 5 * static_cast<size_t>(j - S) : geo_lin + 5 * static_cast<size_t>(j);
+    return g;
+}
+
+__device__ __forceinline__ void store_geo(float4* out, const GeoRec& g) {
     const float4* in = reinterpret_cast<const float4*>(&g);
     for (int k = 0; k < 5; ++k) out[k] = in[k];
-    if (!leaf_slot) {
-        const FlatMaterial& m = s.material;
-        mat[2 * j] = make_float4(m.color.x, m.color.y, m.color.z, m.fresnelStrength);
-        mat[2 * j + 1] = make_float4(m.ambientStrength, m.diffuseStrength, m.specularStrength,
-                                     static_cast<float>(m.shininess));
-    }
+}
+
+__device__ __forceinline__ void store_mat(float4* mat, int j, const FlatMaterial& m) {
+    mat[2 * j] = make_float4(m.color.x, m.color.y, m.color.z, m.fresnelStrength);
+    mat[2 * j + 1] =
+        make_float4(m.ambientStrength, m.diffuseStrength, m.specularStrength, static_cast<float>(m.shininess));
+}
+
+__global__ void k_pack_shapes(const FlatShape* __restrict__ src, int S, const int* __restrict__ idx, int I,
+                              float4* __restrict__ geo_lin, float4* __restrict__ geo_leaf,
+                              float4* __restrict__ mat) {
+    int j = blockIdx.x * blockDim.x + threadIdx.x;
+    int total = S + I;
+    if (j >= total) return;
+    const bool leaf_slot = j >= S;
+    const int si = leaf_slot ? idx[j - S] : j;
+    const FlatShape& s = src[si];
+    const GeoRec g = pack_geo(s, si);
+    store_geo(leaf_slot ? geo_leaf + 5 * static_cast<size_t>(j - S) : geo_lin + 5 * static_cast<size_t>(j), g);
+    if (!leaf_slot) store_mat(mat, j, s.material);
 }
 
 __global__ void k_pack_nodes(const FlatNode* __restrict__ src, int N, float4* __restrict__ nodes) {
@@ -1266,6 +1276,170 @@ __global__ __launch_bounds__(kOrderThreads) void k_tile_order(const unsigned* __
     }
 }
 
+// ---------------------------------------------------------------------------
+// Device animation (rt_animate): updateScene + updateBVH on the device.
+
+// Ordered-integer float atomics. A NaN coordinate adds nothing, as in
+// glm::min/max (BoundingBox.hpp:44-48: min(Min, p) keeps Min when p is NaN);
+// stored values are never NaN.
+__device__ __forceinline__ void atomic_min_f(float* p, float v) {
+    if (!(v == v)) return;
+    if (__float_as_int(v) >= 0)
+        atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
+    else
+        atomicMax(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
+}
+__device__ __forceinline__ void atomic_max_f(float* p, float v) {
+    if (!(v == v)) return;
+    if (__float_as_int(v) >= 0)
+        atomicMax(reinterpret_cast<int*>(p), __float_as_int(v));
+    else
+        atomicMin(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
+}
+
+// Wall::end (src/shapes/wall.hpp:16-31), host glm operation order.
+__device__ V wall_end(const FlatShape& s) {
+    const V n = mk(s.planeNormal.x, s.planeNormal.y, s.planeNormal.z);
+    const V t1 = fabsf(n.x) > fabsf(n.y) ? normalize(mk(-n.z, 0.f, n.x)) : normalize(mk(0.f, -n.z, n.y));
+    const V t2 = normalize(cross(n, t1));
+    return (mk(s.wallStart.x, s.wallStart.y, s.wallStart.z) + t1 * s.wallWidth) + t2 * s.wallHeight;
+}
+
+// BoundingBox::growToInclude(shape) (BoundingBox.hpp:50-95) from an empty box:
+// the points it adds, as a (lo, hi) pair; a shape that adds nothing leaves
+// lo = +inf, hi = -inf.
+__device__ void reference_box(const FlatShape& s, float lo[3], float hi[3]) {
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = INFINITY;
+        hi[a] = -INFINITY;
+    }
+    auto add = [&](V p) {
+        const float v[3] = {p.x, p.y, p.z};
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = v[a] < lo[a] ? v[a] : lo[a];
+            hi[a] = hi[a] < v[a] ? v[a] : hi[a];
+        }
+    };
+    if (s.type == RT_SPHERE) {
+        const float r = s.sphereRadius;
+        add(mk(s.sphereCenter.x + r, s.sphereCenter.y + r, s.sphereCenter.z + r));
+        add(mk(s.sphereCenter.x - r, s.sphereCenter.y - r, s.sphereCenter.z - r));
+    } else if (s.type == RT_WALL) {
+        add(mk(s.wallStart.x, s.wallStart.y, s.wallStart.z));
+        add(wall_end(s));
+    } else if (s.type == RT_TRIANGLE) {
+        if (isfinite(s.triP1.x) && isfinite(s.triP2.x) && isfinite(s.triP3.x)) {  // :52
+            add(mk(s.triP1.x, s.triP1.y, s.triP1.z));
+            add(mk(s.triP2.x, s.triP2.y, s.triP2.z));
+            add(mk(s.triP3.x, s.triP3.y, s.triP3.z));
+        }
+    }
+}
+
+// Per animated shape i (CSR lists built by prepare_animation on the host):
+//   nodes  : every reference node whose shape set lists it (leaves + ancestors)
+//   slots  : its geo_leaf slots (bvhIndices positions)
+//   prims  : its accelerator prim slots
+//   wpos   : wide-record slots (4*w + s) of the local nodes above those prims
+struct AnimMaps {
+    const int *ids, *node_off, *node_list, *slot_off, *slot_list, *prim_off, *prim_list, *wpos_off, *wpos_list;
+    int count;
+};
+enum { AF_BOUNDED = 1, AF_CONE = 2 };  // per-frame flags: conservative box valid; normal moved
+
+struct AnimOut {
+    FlatShape* shapes;  // staging copy of the full shape array
+    FlatNode* nodes;    // staging copy of the node array (authoritative boxes)
+    float4 *geo_lin, *geo_leaf, *mat;
+    float4 *anodes, *lnodes, *prims;  // accelerator (null when off)
+    const int* prim_seq;
+    float origin_lim;
+};
+
+// One thread per animated shape: rewrites its records, then grows the boxes of
+// every node listing it. Box growth is order-independent (min/max), so
+// concurrent threads reach the updateBVH result whatever their order.
+__global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __restrict__ flags, AnimMaps m,
+                          AnimOut o) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m.count) return;
+    const FlatShape s = fresh[i];
+    const int id = m.ids[i], fl = flags[i];
+    o.shapes[id] = s;
+    const GeoRec g = pack_geo(s, id);
+    store_geo(o.geo_lin + 5 * static_cast<size_t>(id), g);
+    store_mat(o.mat, id, s.material);
+    for (int q = m.slot_off[i]; q < m.slot_off[i + 1]; ++q) store_geo(o.geo_leaf + 5 * static_cast<size_t>(m.slot_list[q]), g);
+    float lo[3], hi[3];
+    reference_box(s, lo, hi);
+    for (int q = m.node_off[i]; q < m.node_off[i + 1]; ++q) {
+        FlatNode* n = o.nodes + m.node_list[q];
+        float* mn = &n->boundsMin.x;
+        float* mx = &n->boundsMax.x;
+        for (int a = 0; a < 3; ++a) {
+            atomic_min_f(mn + a, lo[a]);
+            atomic_max_f(mx + a, hi[a]);
+        }
+    }
+    if (!o.anodes) return;
+    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {
+        const int p = m.prim_list[q];
+        GeoRec gp = g;
+        gp.f[17] = __int_as_float(o.prim_seq[p]);  // rank in the reference walk (k_pack_prims)
+        store_geo(o.prims + 5 * static_cast<size_t>(p), gp);
+    }
+    if (!(fl & AF_BOUNDED)) return;
+    rta::Box3 b;
+    if (rta::classify(s, b, o.origin_lim) != rta::BOUNDED) return;  // the host checked the class
+    for (int q = m.node_off[i]; q < m.node_off[i + 1]; ++q) {  // content boxes (accel.h)
+        float* c = reinterpret_cast<float*>(o.anodes + 4 * static_cast<size_t>(m.node_list[q]) + 2);
+        for (int a = 0; a < 3; ++a) {
+            atomic_min_f(c + a, b.lo[a]);
+            atomic_max_f(c + 4 + a, b.hi[a]);
+        }
+    }
+    for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // local boxes in the wide records
+        const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
+        float* r = reinterpret_cast<float*>(o.lnodes + 11 * static_cast<size_t>(w)) + sl;
+        for (int a = 0; a < 3; ++a) {
+            atomic_min_f(r + 4 * a, b.lo[a]);
+            atomic_max_f(r + 4 * (3 + a), b.hi[a]);
+        }
+        if (fl & AF_CONE) r[4 * 9] = -4.f;  // the back-face cone no longer holds: never cull
+    }
+}
+
+// Re-derives every copy of the node boxes from the staging nodes and the
+// content boxes: the packed nodes (k_packet, k_lane), and the accelerator's
+// exact boxes plus its per-parent child copies (anodes rows 0-1, wnodes).
+__global__ void k_refresh_nodes(const FlatNode* __restrict__ src, int N, float4* __restrict__ nodes,
+                                float4* __restrict__ anodes, float4* __restrict__ wnodes) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= N) return;
+    const FlatNode& n = src[k];
+    const bool leaf = n.leftChild == -1;
+    const int a = leaf ? -(n.startShapeIdx + 1) : n.leftChild, b = leaf ? n.numShapes : n.rightChild;
+    nodes[2 * k] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, __int_as_float(a));
+    nodes[2 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, __int_as_float(b));
+    if (!anodes) return;
+    float4* an = anodes + 4 * static_cast<size_t>(k);
+    an[0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, an[0].w);
+    an[1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, an[1].w);
+    if (leaf) return;
+    const int ch[2] = {n.leftChild, n.rightChild};
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const FlatNode& cn = src[ch[s2]];
+        const float4* ca = anodes + 4 * static_cast<size_t>(ch[s2]);
+        float4* q = wnodes + 8 * static_cast<size_t>(k) + 4 * s2;
+        q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, q[0].w);
+        q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, q[1].w);
+        const float4 lo = ca[2], hi = ca[3];
+        q[2] = make_float4(lo.x, lo.y, lo.z, q[2].w);
+        q[3] = make_float4(hi.x, hi.y, hi.z, q[3].w);
+    }
+}
+
+
 }  // namespace
 
 // ===========================================================================
@@ -1330,6 +1504,19 @@ struct rt_ctx {
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
+    // animation (rt_set_animated / rt_animate)
+    std::vector<int> anim_ids;
+    std::vector<int> anim_cls;          // accelerator class of each at the last build (accel_bound.h)
+    std::vector<FlatShape> anim_base;   // the record the accelerator's cones were built from
+    int* anim_maps = nullptr;           // AnimMaps lists, one allocation
+    size_t anim_maps_cap = 0;
+    AnimMaps anim{};
+    void* anim_pinned = nullptr;        // per-frame upload: FlatShape[count] then int flags[count]
+    size_t anim_pinned_cap = 0;
+    char* anim_frame = nullptr;         // its device copy
+    size_t anim_frame_cap = 0;
+    hipEvent_t anim_copied = nullptr;   // the last upload from anim_pinned has completed
+    bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
 };
 
 namespace {
@@ -1423,7 +1610,7 @@ inline float bits_f(int v) {
 // Builds the accelerator from the host copies of the scene and uploads it;
 // expects geo_lin to be packed (k_pack_prims copies from it). On failure the
 // context keeps rendering with k_packet.
-int upload_accel(rt_ctx* c) {
+int build_upload_accel(rt_ctx* c) {
     free_accel(c);
     const int N = c->N;
     if (N == 0) return RT_OK;
@@ -1533,6 +1720,135 @@ int upload_accel(rt_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host vectors die here
     c->accel_ok = true;
     return RT_OK;
+}
+
+// Brings host_nodes up to the boxes rt_animate grew on the device.
+int sync_host_nodes(rt_ctx* c) {
+    if (!c->nodes_on_device_newer) return RT_OK;
+    HIP_TRY(hipMemcpyAsync(c->host_nodes.data(), c->staging_nodes, c->N * sizeof(FlatNode), hipMemcpyDeviceToHost,
+                           c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->nodes_on_device_newer = false;
+    return RT_OK;
+}
+
+// The device lists of rt_animate (AnimMaps) for the current scene and
+// accelerator. anim_base holds, per animated shape, the record the
+// accelerator's bounds and cones were built from.
+int prepare_animation(rt_ctx* c) {
+    const int n = static_cast<int>(c->anim_ids.size());
+    c->anim = AnimMaps{};
+    if (n == 0) return RT_OK;
+    const int N = c->N;
+    std::vector<int> which(c->S, -1);  // shape -> animated index
+    for (int i = 0; i < n; ++i) which[c->anim_ids[i]] = i;
+    const rta::AccelHost& A = c->accel;
+    c->anim_cls.assign(n, rta::UNBOUNDED);
+    for (int i = 0; i < n; ++i) {
+        rta::Box3 b;
+        c->anim_cls[i] = rta::classify(c->anim_base[i], b, A.origin_lim);
+    }
+    // reference nodes listing each shape: the leaves that list it and every node above
+    std::vector<std::vector<int>> parents(N);
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = c->host_nodes[k];
+        if (nd.leftChild != -1) {
+            parents[nd.leftChild].push_back(k);
+            if (nd.rightChild != nd.leftChild) parents[nd.rightChild].push_back(k);
+        }
+    }
+    std::vector<std::vector<int>> nodes_of(n), slots_of(n), prims_of(n), wpos_of(n);
+    std::vector<int> stamp(N, -1);
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = c->host_nodes[k];
+        if (nd.leftChild != -1) continue;
+        for (int j = nd.startShapeIdx; j < nd.startShapeIdx + nd.numShapes; ++j) {
+            const int i = which[c->host_idx[j]];
+            if (i < 0) continue;
+            slots_of[i].push_back(j);
+            nodes_of[i].push_back(k);
+        }
+    }
+    for (int i = 0; i < n; ++i) {
+        std::vector<int>& L = nodes_of[i];
+        std::vector<int> todo;
+        for (int k : L)
+            if (stamp[k] != i) {
+                stamp[k] = i;
+                todo.push_back(k);
+            }
+        L.clear();
+        while (!todo.empty()) {
+            const int k = todo.back();
+            todo.pop_back();
+            L.push_back(k);
+            for (int p : parents[k])
+                if (stamp[p] != i) {
+                    stamp[p] = i;
+                    todo.push_back(p);
+                }
+        }
+        std::sort(L.begin(), L.end());
+    }
+    if (c->accel_ok) {
+        const size_t P = A.prim_shape.size(), M = A.lbox.size();
+        std::vector<int> lleaf(P, -1), lparent(M, -1), wpos(M, -1);
+        for (size_t j = 0; j < M; ++j) {
+            if (A.la[j] < 0) {
+                const int st = -A.la[j] - 1;
+                for (int q = 0; q < A.lb[j]; ++q) lleaf[st + q] = static_cast<int>(j);
+            } else {
+                lparent[A.la[j]] = static_cast<int>(j);
+                lparent[A.lb[j] & 0x3fffffff] = static_cast<int>(j);
+            }
+        }
+        for (size_t q = 0; q < A.wchild.size(); ++q)
+            if (A.wchild[q] >= 0) wpos[A.wchild[q]] = static_cast<int>(q);
+        std::vector<int> wstamp(M, -1);
+        for (size_t p = 0; p < P; ++p) {
+            const int i = which[A.prim_shape[p]];
+            if (i < 0) continue;
+            prims_of[i].push_back(static_cast<int>(p));
+            for (int j = lleaf[p]; j >= 0; j = lparent[j])
+                if (wpos[j] >= 0 && wstamp[j] != i) {
+                    wstamp[j] = i;
+                    wpos_of[i].push_back(wpos[j]);
+                }
+        }
+    }
+    // one int allocation: ids, then (offsets, list) x 4
+    std::vector<int> buf(c->anim_ids);
+    auto append = [&](const std::vector<std::vector<int>>& lists, size_t& off_at, size_t& list_at) {
+        off_at = buf.size();
+        int run = 0;
+        buf.push_back(0);
+        for (const auto& l : lists) buf.push_back(run += static_cast<int>(l.size()));
+        list_at = buf.size();
+        for (const auto& l : lists) buf.insert(buf.end(), l.begin(), l.end());
+    };
+    size_t o[8];
+    append(nodes_of, o[0], o[1]);
+    append(slots_of, o[2], o[3]);
+    append(prims_of, o[4], o[5]);
+    append(wpos_of, o[6], o[7]);
+    int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int* d = c->anim_maps;
+    c->anim = AnimMaps{d, d + o[0], d + o[1], d + o[2], d + o[3], d + o[4], d + o[5], d + o[6], d + o[7], n};
+    return RT_OK;
+}
+
+// (Re)builds the accelerator after the host copies changed, then the animation lists.
+int upload_accel(rt_ctx* c) {
+    int rc = sync_host_nodes(c);
+    if (rc != RT_OK) return rc;
+    rc = build_upload_accel(c);
+    c->anim_base.resize(c->anim_ids.size());
+    for (size_t i = 0; i < c->anim_ids.size(); ++i) c->anim_base[i] = c->host_shapes[c->anim_ids[i]];
+    const int rc2 = prepare_animation(c);
+    return rc != RT_OK ? rc : rc2;
 }
 
 size_t sched_set_words(int tiles) {
@@ -1752,6 +2068,10 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->sched_cost);
     hipFree(c->sched_order);
     hipFree(c->sched_sets);
+    hipFree(c->anim_maps);
+    hipFree(c->anim_frame);
+    if (c->anim_pinned) hipHostFree(c->anim_pinned);
+    if (c->anim_copied) hipEventDestroy(c->anim_copied);
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -1816,6 +2136,8 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->host_idx.assign(idx, idx + I);
     c->host_shapes.assign(shapes, shapes + S);
     c->have_scene = true;
+    c->nodes_on_device_newer = false;
+    c->anim_ids.clear();  // ids refer to the previous scene
     return upload_accel(c);
 }
 
@@ -1851,7 +2173,95 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host array may be reused after return
     c->host_nodes.assign(nodes, nodes + N);
+    c->nodes_on_device_newer = false;
     return upload_accel(c);
+}
+
+int rt_set_animated(rt_ctx* c, const int* ids, int count) {
+    if (!c || !c->have_scene || count < 0 || (count > 0 && !ids)) return RT_ERR_INVALID;
+    std::vector<char> seen(c->S, 0);
+    for (int i = 0; i < count; ++i) {
+        if (ids[i] < 0 || ids[i] >= c->S || seen[ids[i]]) return RT_ERR_INVALID;
+        seen[ids[i]] = 1;
+    }
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    int rc = sync_host_nodes(c);
+    if (rc != RT_OK) return rc;
+    // shapes that stay animated keep the base record the accelerator was built from
+    std::vector<FlatShape> base(count);
+    for (int i = 0; i < count; ++i) {
+        base[i] = c->host_shapes[ids[i]];
+        for (size_t j = 0; j < c->anim_ids.size(); ++j)
+            if (c->anim_ids[j] == ids[i] && j < c->anim_base.size()) base[i] = c->anim_base[j];
+    }
+    c->anim_ids.assign(ids, ids + count);
+    c->anim_base = base;
+    return prepare_animation(c);
+}
+
+int rt_animate(rt_ctx* c, const FlatShape* shapes) {
+    if (!c || !c->have_scene || c->anim_ids.empty() || !shapes) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    const int n = static_cast<int>(c->anim_ids.size());
+    // host side: does each shape keep its kind of bound, did its normal move
+    bool rebuild = false;
+    std::vector<int> flags(n, 0);
+    for (int i = 0; i < n; ++i) {
+        const FlatShape &s = shapes[i], &b0 = c->anim_base[i];
+        int cls = rta::UNBOUNDED;
+        if (c->accel_ok) {
+            rta::Box3 b;
+            cls = rta::classify(s, b, c->accel.origin_lim);
+            if (cls != c->anim_cls[i]) rebuild = true;
+        }
+        const bool cone = s.type != b0.type || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
+                                                std::memcmp(&s.planeNormal, &b0.planeNormal, sizeof(rt_vec3)) != 0);
+        flags[i] = (cls == rta::BOUNDED ? AF_BOUNDED : 0) | (cone ? AF_CONE : 0);
+    }
+    const size_t bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
+    if (!c->anim_copied) {
+        HIP_TRY(hipEventCreateWithFlags(&c->anim_copied, hipEventDisableTiming));
+    } else {
+        HIP_TRY(hipEventSynchronize(c->anim_copied));  // the last upload has left the pinned buffer
+    }
+    if (c->anim_pinned_cap < bytes) {
+        if (c->anim_pinned) hipHostFree(c->anim_pinned);
+        c->anim_pinned = nullptr;
+        c->anim_pinned_cap = 0;
+        if (hipHostMalloc(&c->anim_pinned, bytes) != hipSuccess) return RT_ERR_NO_MEMORY;
+        c->anim_pinned_cap = bytes;
+    }
+    int rc = ensure_staging(c->anim_frame, c->anim_frame_cap, bytes);
+    if (rc != RT_OK) return rc;
+    char* pin = static_cast<char*>(c->anim_pinned);
+    std::memcpy(pin, shapes, n * sizeof(FlatShape));
+    std::memcpy(pin + n * sizeof(FlatShape), flags.data(), n * sizeof(int));
+    HIP_TRY(hipMemcpyAsync(c->anim_frame, pin, bytes, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipEventRecord(c->anim_copied, c->stream));
+    const bool acc = c->accel_ok;
+    const size_t P = c->accel.prim_shape.size();
+    const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat,
+                      acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
+                      acc ? c->prim_idx_dev + P : nullptr, c->accel.origin_lim};
+    hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
+                       reinterpret_cast<const FlatShape*>(c->anim_frame),
+                       reinterpret_cast<const int*>(c->anim_frame + n * sizeof(FlatShape)), c->anim, out);
+    if (c->N > 0)
+        hipLaunchKernelGGL(k_refresh_nodes, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, c->N,
+                           c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr);
+    HIP_TRY(hipGetLastError());
+    for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
+    c->nodes_on_device_newer = true;
+    return rebuild ? upload_accel(c) : RT_OK;  // a bound changed kind: rebuild from the grown nodes
+}
+
+int rt_read_nodes(rt_ctx* c, FlatNode* nodes, int N) {
+    if (!c || !c->have_scene || N != c->N || (N > 0 && !nodes)) return RT_ERR_INVALID;
+    if (N == 0) return RT_OK;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipMemcpyAsync(nodes, c->staging_nodes, N * sizeof(FlatNode), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RT_OK;
 }
 
 int rt_set_camera(rt_ctx* c, const FlatCamera* cam) {

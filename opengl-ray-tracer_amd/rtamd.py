@@ -178,6 +178,8 @@ RT_SYMBOLS = {
     "rt_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
     "rt_update_shapes": (_I, [_P, _I, _I, _P]),
     "rt_update_nodes": (_I, [_P, _P, _I]),
+    "rt_set_animated": (_I, [_P, _P, _I]), "rt_animate": (_I, [_P, _P]),
+    "rt_read_nodes": (_I, [_P, _P, _I]),
     "rt_set_camera": (_I, [_P, _P]), "rt_set_light": (_I, [_P, _P]),
     "rt_set_params": (_I, [_P, _P]), "rt_set_kernel": (_I, [_P, _I]),
     "rt_dispatch": (_I, [_P, _I, _I, _I, _I]),
@@ -408,6 +410,26 @@ class ComputeShader:
     def update_nodes(self, nodes):
         nodes = as_records(nodes, NODE_DTYPE)
         self._chk(self._lib.rt_update_nodes(self._h, _ptr(nodes), len(nodes)), "rt_update_nodes")
+
+    def set_animated(self, ids):
+        """Marks the animated shapes (animatedIndices, src/main.cpp:120,706-708)."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        self._n_animated = len(ids)
+        self._chk(self._lib.rt_set_animated(self._h, _ptr(ids), len(ids)), "rt_set_animated")
+
+    def animate(self, shapes):
+        """New records of the animated shapes, in set_animated order: updateScene +
+        updateBVH + serializeBVH + upload (src/main.cpp:336-346), on the device."""
+        shapes = as_records(shapes, SHAPE_DTYPE)
+        if len(shapes) != getattr(self, "_n_animated", -1):
+            raise ValueError("animate: one record per animated shape")
+        self._chk(self._lib.rt_animate(self._h, _ptr(shapes)), "rt_animate")
+
+    def read_nodes(self, num_nodes):
+        """The current node records (boxes grown by animate)."""
+        out = np.zeros(num_nodes, NODE_DTYPE)
+        self._chk(self._lib.rt_read_nodes(self._h, _ptr(out), num_nodes), "rt_read_nodes")
+        return out
 
     def set_camera(self, cam):
         cam = as_records(cam, CAMERA_DTYPE)

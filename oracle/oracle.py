@@ -30,6 +30,7 @@ ORACLE_SYMBOLS = {
     "orc_get_ray": (_I, [_P, _F, _F, _P, _P]),
     "orc_ray_aabb": (_I, [_P, _P, _P, _P]),
     "orc_wall_end": (_I, [_P, _P]),
+    "orc_update_bvh": (_I, [_P, _I, _P, _I, _P, _I, _P, _I]),
 }
 
 REF_SYMBOLS = {
@@ -112,6 +113,16 @@ def build_bvh(shapes: np.ndarray, max_depth: int):
     if rc != 0:
         raise RuntimeError("orc_build_bvh failed")
     return nodes, idx
+
+
+def update_bvh(fs: rtamd.FlatScene, ids):
+    """updateBVH (src/main.cpp:1068-1077) restated: grows fs.nodes in place for the
+    animated shapes `ids` at their current records in fs.shapes."""
+    ids = np.ascontiguousarray(ids, np.int32)
+    rc = lib().orc_update_bvh(_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes), _p(fs.indices),
+                              len(fs.indices), _p(ids), len(ids))
+    if rc != 0:
+        raise RuntimeError(f"orc_update_bvh rc={rc}")
 
 
 def intersect(shape_rec: np.ndarray, o, d, use_mt=False):

@@ -666,6 +666,48 @@ int orc_build_bvh(const FlatShape* shapes, int S, int max_depth, FlatNode* nodes
     return rc;
 }
 
+/* updateBVH (src/main.cpp:1068-1077) on the serialised tree: every node whose
+ * shapesIndices list an animated shape grows to include the shape's current
+ * geometry (BoundingBox::growToInclude, src/BoundingBox.hpp:44-95; grow-only).
+ * The reference keeps shapesIndices on inner nodes too: the union of its
+ * children's (split, src/main.cpp:1128-1144), i.e. every shape of the leaves
+ * below. This restatement derives that set from the flat tree: node k lists
+ * shape a iff a leaf reachable from k lists it. Boxes in nodes[] grow in place. */
+static int lists_shape(const FlatNode* nodes, const int* idx, int k, int a, signed char* memo, int depth) {
+    if (memo[k] >= 0) return memo[k];
+    int r = 0;
+    const FlatNode* n = &nodes[k];
+    if (n->leftChild == -1) {
+        for (int i = 0; i < n->numShapes && !r; ++i) r = idx[n->startShapeIdx + i] == a;
+    } else if (depth < 4096) {
+        r = lists_shape(nodes, idx, n->leftChild, a, memo, depth + 1) |
+            lists_shape(nodes, idx, n->rightChild, a, memo, depth + 1);
+    }
+    memo[k] = (signed char)r;
+    return r;
+}
+
+int orc_update_bvh(const FlatShape* shapes, int S, FlatNode* nodes, int N, const int* idx, int I, const int* ids,
+                   int count) {
+    (void)I;
+    signed char* memo = (signed char*)malloc((size_t)(N > 0 ? N : 1));
+    if (!memo) return -1;
+    for (int j = 0; j < count; ++j) {
+        const int a = ids[j];
+        if (a < 0 || a >= S) { free(memo); return -2; }
+        memset(memo, -1, (size_t)(N > 0 ? N : 1));
+        for (int k = 0; k < N; ++k) {
+            if (!lists_shape(nodes, idx, k, a, memo, 0)) continue;
+            box_t b = {fv(nodes[k].boundsMin), fv(nodes[k].boundsMax)};
+            box_shape(&b, &shapes[a]);
+            nodes[k].boundsMin.x = b.lo.x; nodes[k].boundsMin.y = b.lo.y; nodes[k].boundsMin.z = b.lo.z;
+            nodes[k].boundsMax.x = b.hi.x; nodes[k].boundsMax.y = b.hi.y; nodes[k].boundsMax.z = b.hi.z;
+        }
+    }
+    free(memo);
+    return 0;
+}
+
 /* ------------------------------------------------------------------------ */
 /* Known-answer helpers for tests/                                           */
 

@@ -178,3 +178,53 @@ def test_accel_sphere_silhouettes_from_afar(check_lib):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     lim = rng.uniform(1, 400, R)
     compare(check_lib, fs2, o, d, lim)
+
+
+def test_accel_small_shapes_far_origins(check_lib):
+    """Small triangles and walls near the origin in a scene whose magnitude is
+    set by one far sphere, hit from origins up to origin_lim: the slab test and
+    the reference's plane-based hit point both err by ~u*|o| there, more than
+    the size-relative padding of a small box; the origin-relative padding
+    (accel_bound.h, kOriginErr) covers it."""
+    fs = rtamd.generate(3, 0, 96, 54)
+    rng = np.random.default_rng(17)
+    n = 400
+    tri = np.zeros(n, fs.shapes.dtype)
+    tri["type"] = 3
+    p1 = rng.uniform(-2, 2, (n, 3)).astype(np.float32)
+    p2 = (p1 + rng.uniform(-0.03, 0.03, (n, 3))).astype(np.float32)
+    p3 = (p1 + rng.uniform(-0.03, 0.03, (n, 3))).astype(np.float32)
+    nn = np.cross(p2.astype(np.float64) - p1, p3.astype(np.float64) - p1)
+    nn /= np.linalg.norm(nn, axis=1, keepdims=True)
+    tri["triP1"], tri["triP2"], tri["triP3"] = p1, p2, p3
+    tri["planeNormal"] = nn.astype(np.float32)
+    tri["planeD"] = -(nn * p1).sum(1).astype(np.float32)
+    tri["material"] = fs.shapes["material"][0]
+    far = np.zeros(1, fs.shapes.dtype)
+    far["type"] = 0
+    far["sphereCenter"] = (3000.0, 0.0, 0.0)
+    far["sphereRadius"] = 1.0
+    far["material"] = fs.shapes["material"][0]
+    shapes = np.concatenate([tri, far])
+    nodes = np.zeros(1, rtamd.NODE_DTYPE)
+    nodes["boundsMin"], nodes["boundsMax"] = -1e4, 1e4
+    nodes["leftChild"] = nodes["rightChild"] = -1
+    nodes["numShapes"] = len(shapes)
+    idx = np.arange(len(shapes), dtype=np.int32)
+    fs2 = rtamd.FlatScene(shapes, nodes, idx, fs.camera, fs.light)
+    R = 12000
+    k = rng.integers(0, n, R)
+    # aim at points on the triangle edges, slightly in or out
+    a, b = rng.integers(0, 3, R), rng.uniform(0, 1, R)
+    P = np.stack([p1[k], p2[k], p3[k]], 1).astype(np.float64)
+    e0, e1 = P[np.arange(R), a], P[np.arange(R), (a + 1) % 3]
+    cen = P.mean(1)
+    edge = e0 + (e1 - e0) * b[:, None]
+    tgt = edge + (edge - cen) * rng.uniform(-0.02, 0.02, R)[:, None]
+    u = rng.normal(size=(R, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    o = np.clip(tgt + u * rng.uniform(2e3, 1.5e4, (R, 1)), -1.15e4, 1.15e4)  # origin_lim ~ 4 * 3002
+    d = tgt - o
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    lim = rng.uniform(1, 3e4, R)
+    compare(check_lib, fs2, o, d, lim)

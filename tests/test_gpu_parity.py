@@ -409,3 +409,131 @@ def test_obj_scene_parity(ctx, kernel):
     p = oracle.params(W, H, 3)
     ref, _ = oracle.render(fs, W, H, p)
     check(gpu_rows(ctx, fs, W, H, p, kernel=kernel), ref, f"obj kernel{kernel}")
+
+
+# --------------------------------------------------------------------------
+# Device-side animation (rt_set_animated / rt_animate): updateScene +
+# updateBVH + serializeBVH (src/main.cpp:336-346, 981-992, 1068-1077) on the
+# device, against oracle.update_bvh (the restated updateBVH) + oracle.render.
+
+def _rotate(points, center, axis, angle):
+    """Rodrigues rotation about `axis` through `center` (float64, then float32)."""
+    a = np.asarray(axis, np.float64) / np.linalg.norm(axis)
+    p = points.astype(np.float64) - center
+    c, s = np.cos(angle), np.sin(angle)
+    r = p * c + np.cross(a, p) * s + np.outer(p @ a, a) * (1 - c)
+    return (r + center).astype(np.float32)
+
+
+def _animation_steps(fs, ids, steps, renormal):
+    """Yields successive records of shapes `ids`: spheres bounce on Y
+    (bounceSphere, src/main.cpp:1079-1082), triangles turn about an axis
+    (updateWheelAnimations :1084-1109, stored normals left as they were unless
+    `renormal`), walls slide."""
+    base = fs.shapes[ids].copy()
+    for k in range(1, steps + 1):
+        rec = base.copy()
+        sph = rec["type"] == 0
+        rec["sphereCenter"][sph, 1] = base["sphereCenter"][sph, 1] + np.float32(2 * np.sin(0.7 * k))
+        tri = np.where(rec["type"] == 3)[0]
+        if tri.size:
+            cen = base["triP1"][tri].astype(np.float64).mean(0)
+            for f in ("triP1", "triP2", "triP3"):
+                rec[f][tri] = _rotate(base[f][tri], cen, (0.3, 0.2, 1.0), 0.35 * k)
+            if renormal:
+                e1 = rec["triP2"][tri].astype(np.float64) - rec["triP1"][tri]
+                e2 = rec["triP3"][tri].astype(np.float64) - rec["triP1"][tri]
+                n = np.cross(e1, e2)
+                n /= np.linalg.norm(n, axis=1, keepdims=True)
+                rec["planeNormal"][tri] = n.astype(np.float32)
+                rec["planeD"][tri] = -(n * rec["triP1"][tri]).sum(1).astype(np.float32)
+        wal = rec["type"] == 2
+        rec["wallStart"][wal] = base["wallStart"][wal] + np.float32([1.5 * k, 0.0, -0.5 * k])
+        yield rec
+
+
+def _refit_case(ctx, fs, ids, steps, kernel, W=160, H=120, renormal=False, mutate=None):
+    ref = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3, True)
+    ctx.set_kernel(kernel)
+    ctx.set_animated(ids)
+    p = oracle.params(W, H, 3)
+    for k, rec in enumerate(_animation_steps(fs, ids, steps, renormal)):
+        if mutate is not None:
+            mutate(k, rec)
+        ref.shapes[ids] = rec
+        oracle.update_bvh(ref, ids)
+        ctx.animate(rec)
+        got = ctx.read_nodes(len(ref.nodes))
+        for f in ("boundsMin", "boundsMax"):
+            assert np.array_equal(got[f], ref.nodes[f]), f"step {k}: {f} differs from updateBVH"
+        for f in ("leftChild", "rightChild", "startShapeIdx", "numShapes"):
+            assert np.array_equal(got[f], ref.nodes[f])
+        img = ctx.render(W, H)
+        want, _ = oracle.render(ref, W, H, p)
+        check(img, want, f"refit step {k} kernel {kernel}")
+    return ref
+
+
+@pytest.mark.parametrize("kernel", [rtamd.KERNEL_ACCEL, rtamd.KERNEL_PACKET])
+@pytest.mark.parametrize("depth", [1, 8])
+def test_device_refit_matches_update_bvh(ctx, kernel, depth):
+    fs = _soup(3, n_tri=1200)
+    fs.nodes, fs.indices = oracle.build_bvh(fs.shapes, depth)
+    types = fs.shapes["type"]
+    ids = np.concatenate([np.where(types == 0)[0][:12], np.where(types == 3)[0][100:260],
+                          np.where(types == 2)[0]]).astype(np.int32)
+    _refit_case(ctx, fs, ids, 4, kernel)
+
+
+def test_device_refit_moved_normals_and_far_moves(ctx):
+    """Triangle normals recomputed (the back-face cones above them must give
+    way) and a sphere thrown far outside the scene (its boxes grow past the
+    scene's magnitude)."""
+    fs = _soup(4, n_tri=1200)
+    fs.nodes, fs.indices = oracle.build_bvh(fs.shapes, 6)
+    types = fs.shapes["type"]
+    ids = np.concatenate([np.where(types == 0)[0][:6], np.where(types == 3)[0][:300]]).astype(np.int32)
+
+    def far(k, rec):
+        if k == 2:
+            rec["sphereCenter"][0] = (400.0, 30.0, -200.0)
+    _refit_case(ctx, fs, ids, 4, rtamd.KERNEL_ACCEL, renormal=True, mutate=far)
+
+
+def test_device_refit_class_change_rebuilds(ctx):
+    """A triangle that collapses to a sliver (no conservative bound) and a
+    sphere that becomes infinite: the host rebuild path, same frames."""
+    fs = _soup(5, n_tri=800)
+    fs.nodes, fs.indices = oracle.build_bvh(fs.shapes, 5)
+    types = fs.shapes["type"]
+    ids = np.concatenate([np.where(types == 0)[0][:4], np.where(types == 3)[0][:50]]).astype(np.int32)
+
+    def degenerate(k, rec):
+        if k >= 1:
+            t = np.where(rec["type"] == 3)[0][0]
+            rec["triP3"][t] = rec["triP1"][t] + (rec["triP2"][t] - rec["triP1"][t]) * np.float32(0.5)
+        if k == 3:
+            rec["sphereRadius"][0] = np.float32(np.inf)
+    _refit_case(ctx, fs, ids, 4, rtamd.KERNEL_ACCEL, mutate=degenerate)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+
+
+def test_device_refit_equals_host_path(ctx):
+    """The device refit and the reference's own host path (update_shapes +
+    update_nodes with updateBVH's boxes) give the same frame."""
+    W, H = 200, 150
+    fs = _soup(6, n_tri=1000)
+    fs.nodes, fs.indices = oracle.build_bvh(fs.shapes, 10)
+    ids = np.where(fs.shapes["type"] == 0)[0].astype(np.int32)
+    ref = _refit_case(ctx, fs, ids, 2, rtamd.KERNEL_AUTO, W, H)
+    a = ctx.render(W, H)
+    ctx.upload(fs)
+    ctx.update_shapes(0, ref.shapes)
+    ctx.update_nodes(ref.nodes)
+    assert np.array_equal(ctx.render(W, H), a)
+    with pytest.raises(rtamd.RTError):
+        ctx.set_animated(np.array([0, 0], np.int32))  # duplicates
+    with pytest.raises(rtamd.RTError):
+        ctx.set_animated(np.array([len(fs.shapes)], np.int32))
