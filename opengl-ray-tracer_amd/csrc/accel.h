@@ -13,8 +13,9 @@
 //     are *conservative*: each contains every point the reference test can
 //     return as an INNER hit for that shape, padded well beyond float error.
 //     Shapes without such a bound (planes, walls with a ±Y normal whose basis
-//     is NaN, triangles whose stored plane disagrees with their vertices or
-//     that are too thin to bound their barycentric error) are tested always;
+//     is NaN, triangles whose stored plane is steep to their vertices' plane
+//     or that are too thin to bound their barycentric error) are tested
+//     always (accel_bound.h, classify);
 //   * a lane skips a local box only if its entry distance exceeds the lane's
 //     best hit by a relative margin, and every candidate carries its rank in
 //     the reference walk ("seq"), so the winner is the lexicographic minimum

@@ -39,6 +39,8 @@ struct Box3 {
 
 constexpr double kPadRel = 1e-3;
 constexpr double kMinSin2 = 1e-3;    // thinnest triangle bounded (sin^2 of its corner angle)
+constexpr double kMinCos = 0.05;     // steepest stored plane bounded (cos to the vertices' plane)
+constexpr double kCosRef = 0.5;      // below it the padding scales with 1/cos
 constexpr double kSphereErr = 4e-6;  // k of the sphere-root error above, with room
 constexpr double kOriginRel = 4.0;   // origin_lim = kOriginRel * (scene magnitude + 1)
 constexpr double kOriginErr = 4e-6;  // padding per unit of origin_lim (origin-relative error above)
@@ -98,8 +100,10 @@ struct BoxAcc {
     }
 };
 
-RTA_HD Box3 finish(const BoxAcc& acc, double origin_lim) {
-    return acc.padded(kPadRel * (acc.extent() + acc.mag() + 1.0) + kOriginErr * origin_lim + 1e-6);
+// `amp`: error amplification of the shape's hit point (>= 1; the lift of a
+// triangle onto a steep stored plane divides its errors by the cosine).
+RTA_HD Box3 finish(const BoxAcc& acc, double origin_lim, double amp = 1.0) {
+    return acc.padded(amp * (kPadRel * (acc.extent() + acc.mag() + 1.0) + kOriginErr * origin_lim) + 1e-6);
 }
 
 // UNBOUNDED: no finite bound; BOUNDED: `out` is set; NEVER: the reference test
@@ -148,6 +152,16 @@ RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
             return BOUNDED;
         }
         case RT_TRIANGLE: {
+            // gpu_shader.comp:196-240: the hit point p lies on the STORED plane
+            // (N, D); the barycentric solve then projects p orthogonally onto
+            // the vertices' own plane. So the INNER points are the stored-plane
+            // points whose projection falls inside the triangle: the triangle
+            // lifted along its own normal nt onto the stored plane. The stored
+            // plane need not pass through the vertices (updateWheelAnimations,
+            // src/main.cpp:1084-1109, moves vertices and keeps the old plane);
+            // it must only not be nearly perpendicular to them (|cos| >=
+            // kMinCos); below kCosRef the padding grows as 1/|cos|, the float
+            // error of the lift.
             D3 p1 = d3(s.triP1), p2 = d3(s.triP2), p3 = d3(s.triP3), N = d3(s.planeNormal);
             double D = s.planeD;
             if (!finite3(p1) || !finite3(p2) || !finite3(p3) || !finite3(N) || !isfinite(D)) return UNBOUNDED;
@@ -155,16 +169,15 @@ RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
             double d00 = dot(e1, e1), d11 = dot(e2, e2), c2 = dot(cr, cr);
             if (!(d00 > 0) || !(d11 > 0) || !(c2 >= kMinSin2 * d00 * d11)) return UNBOUNDED;  // thin: error unbounded
             D3 nt = cr * (1.0 / sqrt(c2));
-            double nl = sqrt(dot(N, N));
-            if (fabs(nl - 1.0) > 1e-3 || fabs(dot(N, nt)) < nl * (1.0 - 1e-4)) return UNBOUNDED;
-            double mag = fmax(fmax(maxabs(p1), maxabs(p2)), maxabs(p3)) + 1.0;
-            if (fabs(dot(N, p1) + D) > 1e-4 * mag || fabs(dot(N, p2) + D) > 1e-4 * mag ||
-                fabs(dot(N, p3) + D) > 1e-4 * mag)
-                return UNBOUNDED;  // stored plane off the vertices
-            acc.add(p1);
-            acc.add(p2);
-            acc.add(p3);
-            out = finish(acc, origin_lim);
+            double nl = sqrt(dot(N, N)), cn = dot(N, nt);
+            if (!(nl > 1e-6 && nl < 1e6) || !(fabs(cn) >= kMinCos * nl)) return UNBOUNDED;
+            const D3 q[3] = {p1, p2, p3};
+            for (int i = 0; i < 3; ++i) {
+                const double h = -(dot(N, q[i]) + D) / cn;  // q + h*nt lies on the stored plane
+                if (!isfinite(h)) return UNBOUNDED;
+                acc.add(q[i] + nt * h);
+            }
+            out = finish(acc, origin_lim, fmax(1.0, kCosRef * nl / fabs(cn)));
             return BOUNDED;
         }
         case RT_PLANE:

@@ -1279,24 +1279,6 @@ __global__ __launch_bounds__(kOrderThreads) void k_tile_order(const unsigned* __
 // ---------------------------------------------------------------------------
 // Device animation (rt_animate): updateScene + updateBVH on the device.
 
-// Ordered-integer float atomics. A NaN coordinate adds nothing, as in
-// glm::min/max (BoundingBox.hpp:44-48: min(Min, p) keeps Min when p is NaN);
-// stored values are never NaN.
-__device__ __forceinline__ void atomic_min_f(float* p, float v) {
-    if (!(v == v)) return;
-    if (__float_as_int(v) >= 0)
-        atomicMin(reinterpret_cast<int*>(p), __float_as_int(v));
-    else
-        atomicMax(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
-}
-__device__ __forceinline__ void atomic_max_f(float* p, float v) {
-    if (!(v == v)) return;
-    if (__float_as_int(v) >= 0)
-        atomicMax(reinterpret_cast<int*>(p), __float_as_int(v));
-    else
-        atomicMin(reinterpret_cast<unsigned*>(p), __float_as_uint(v));
-}
-
 // Wall::end (src/shapes/wall.hpp:16-31), host glm operation order.
 __device__ V wall_end(const FlatShape& s) {
     const V n = mk(s.planeNormal.x, s.planeNormal.y, s.planeNormal.z);
@@ -1336,14 +1318,16 @@ __device__ void reference_box(const FlatShape& s, float lo[3], float hi[3]) {
     }
 }
 
-// Per animated shape i (CSR lists built by prepare_animation on the host):
-//   nodes  : every reference node whose shape set lists it (leaves + ancestors)
+// CSR lists built by prepare_animation on the host. Per animated shape i:
 //   slots  : its geo_leaf slots (bvhIndices positions)
 //   prims  : its accelerator prim slots
 //   wpos   : wide-record slots (4*w + s) of the local nodes above those prims
+// Per reference node j that lists an animated shape (node_ids[j]):
+//   node   : the animated shapes it lists (updateBVH's set, leaves + ancestors)
 struct AnimMaps {
-    const int *ids, *node_off, *node_list, *slot_off, *slot_list, *prim_off, *prim_list, *wpos_off, *wpos_list;
-    int count;
+    const int *ids, *slot_off, *slot_list, *prim_off, *prim_list, *wpos_off, *wpos_list;
+    const int *node_ids, *node_off, *node_list;
+    int count, nodes;
 };
 enum { AF_BOUNDED = 1, AF_CONE = 2 };  // per-frame flags: conservative box valid; normal moved
 
@@ -1352,13 +1336,15 @@ struct AnimOut {
     FlatNode* nodes;    // staging copy of the node array (authoritative boxes)
     float4 *geo_lin, *geo_leaf, *mat;
     float4 *anodes, *lnodes, *prims;  // accelerator (null when off)
+    float4* pbox;                     // conservative box per prim (lo, hi), for k_refit_local
     const int* prim_seq;
+    float4* sbox;                     // per animated shape: reference box, conservative box (4 float4)
     float origin_lim;
 };
 
-// One thread per animated shape: rewrites its records, then grows the boxes of
-// every node listing it. Box growth is order-independent (min/max), so
-// concurrent threads reach the updateBVH result whatever their order.
+// One thread per animated shape: rewrites its records and derives its two
+// boxes (the reference's growToInclude box and the accelerator's conservative
+// one); k_grow_nodes then grows the nodes listing it.
 __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __restrict__ flags, AnimMaps m,
                           AnimOut o) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1372,15 +1358,11 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
     for (int q = m.slot_off[i]; q < m.slot_off[i + 1]; ++q) store_geo(o.geo_leaf + 5 * static_cast<size_t>(m.slot_list[q]), g);
     float lo[3], hi[3];
     reference_box(s, lo, hi);
-    for (int q = m.node_off[i]; q < m.node_off[i + 1]; ++q) {
-        FlatNode* n = o.nodes + m.node_list[q];
-        float* mn = &n->boundsMin.x;
-        float* mx = &n->boundsMax.x;
-        for (int a = 0; a < 3; ++a) {
-            atomic_min_f(mn + a, lo[a]);
-            atomic_max_f(mx + a, hi[a]);
-        }
-    }
+    float4* sb = o.sbox + 4 * static_cast<size_t>(i);
+    sb[0] = make_float4(lo[0], lo[1], lo[2], 0.f);
+    sb[1] = make_float4(hi[0], hi[1], hi[2], 0.f);
+    sb[2] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);  // no conservative box unless bounded
+    sb[3] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
     if (!o.anodes) return;
     for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {
         const int p = m.prim_list[q];
@@ -1388,24 +1370,88 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
         gp.f[17] = __int_as_float(o.prim_seq[p]);  // rank in the reference walk (k_pack_prims)
         store_geo(o.prims + 5 * static_cast<size_t>(p), gp);
     }
+    if (fl & AF_CONE)
+        for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
+            const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
+            reinterpret_cast<float*>(o.lnodes + 11 * static_cast<size_t>(w) + 9)[sl] = -4.f;  // never cull
+        }
     if (!(fl & AF_BOUNDED)) return;
     rta::Box3 b;
     if (rta::classify(s, b, o.origin_lim) != rta::BOUNDED) return;  // the host checked the class
-    for (int q = m.node_off[i]; q < m.node_off[i + 1]; ++q) {  // content boxes (accel.h)
-        float* c = reinterpret_cast<float*>(o.anodes + 4 * static_cast<size_t>(m.node_list[q]) + 2);
-        for (int a = 0; a < 3; ++a) {
-            atomic_min_f(c + a, b.lo[a]);
-            atomic_max_f(c + 4 + a, b.hi[a]);
-        }
+    sb[2] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
+    sb[3] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
+    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {  // the prim's box for k_refit_local
+        float4* pb = o.pbox + 2 * static_cast<size_t>(m.prim_list[q]);
+        pb[0] = sb[2];
+        pb[1] = sb[3];
     }
-    for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // local boxes in the wide records
-        const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
-        float* r = reinterpret_cast<float*>(o.lnodes + 11 * static_cast<size_t>(w)) + sl;
+}
+
+__device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
+    for (int off = 32; off > 0; off >>= 1)
         for (int a = 0; a < 3; ++a) {
-            atomic_min_f(r + 4 * a, b.lo[a]);
-            atomic_max_f(r + 4 * (3 + a), b.hi[a]);
+            lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
+            hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
         }
-        if (fl & AF_CONE) r[4 * 9] = -4.f;  // the back-face cone no longer holds: never cull
+}
+
+// One wave per reference node listing an animated shape: the union of their
+// boxes (lanes stride the list, then a wave reduction), then one grow of the
+// node's box - updateBVH's growToInclude of each listed shape - and of its
+// content box. A single writer per node: no atomics, and the min/max result is
+// the same in any order (no stored value is NaN; a NaN coordinate adds nothing).
+__global__ __launch_bounds__(256) void k_grow_nodes(AnimMaps m, AnimOut o) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= m.nodes) return;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int q = m.node_off[j] + lane; q < m.node_off[j + 1]; q += 64) {
+        const float4* sb = o.sbox + 4 * static_cast<size_t>(m.node_list[q]);
+        const float4 a = sb[0], b = sb[1], c = sb[2], d = sb[3];
+        lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
+        hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
+        clo[0] = fminf(clo[0], c.x), clo[1] = fminf(clo[1], c.y), clo[2] = fminf(clo[2], c.z);
+        chi[0] = fmaxf(chi[0], d.x), chi[1] = fmaxf(chi[1], d.y), chi[2] = fmaxf(chi[2], d.z);
+    }
+    wave_minmax(lo, hi);
+    wave_minmax(clo, chi);
+    if (lane != 0) return;
+    const int k = m.node_ids[j];
+    float* mn = &o.nodes[k].boundsMin.x;
+    float* mx = &o.nodes[k].boundsMax.x;
+    for (int a = 0; a < 3; ++a) {  // glm::min(Min, p) = (p < Min) ? p : Min (BoundingBox.hpp:46)
+        mn[a] = lo[a] < mn[a] ? lo[a] : mn[a];
+        mx[a] = mx[a] < hi[a] ? hi[a] : mx[a];
+    }
+    if (!o.anodes) return;
+    float* c = reinterpret_cast<float*>(o.anodes + 4 * static_cast<size_t>(k) + 2);  // content box (accel.h)
+    for (int a = 0; a < 3; ++a) {
+        c[a] = fminf(c[a], clo[a]);
+        c[4 + a] = fmaxf(c[4 + a], chi[a]);
+    }
+}
+
+// Exact refit of the local boxes above moved prims (they are the
+// accelerator's own, so unlike the reference nodes they may shrink): one wave
+// per dirty wide-record slot, the union of pbox over the slot's prim range
+// (a local subtree's prims are contiguous, accel.cpp LocalBuilder).
+// dirty[j] = (4*w + s, first prim, end prim, 0).
+__global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ dirty, int n,
+                                                     const float4* __restrict__ pbox, float4* __restrict__ lnodes) {
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (j >= n) return;
+    const int4 d = dirty[j];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int p = d.y + lane; p < d.z; p += 64) {
+        const float4 a = pbox[2 * static_cast<size_t>(p)], b = pbox[2 * static_cast<size_t>(p) + 1];
+        lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
+        hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
+    }
+    wave_minmax(lo, hi);
+    if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
+        const int w = d.x >> 2, sl = d.x & 3;
+        const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
+        reinterpret_cast<float*>(lnodes + 11 * static_cast<size_t>(w) + lane)[sl] = v;
     }
 }
 
@@ -1516,6 +1562,12 @@ struct rt_ctx {
     char* anim_frame = nullptr;         // its device copy
     size_t anim_frame_cap = 0;
     hipEvent_t anim_copied = nullptr;   // the last upload from anim_pinned has completed
+    float4* anim_sbox = nullptr;        // per animated shape boxes (AnimOut::sbox)
+    size_t anim_sbox_cap = 0;
+    float4* pbox = nullptr;             // per prim conservative box (AnimOut::pbox)
+    int4* refit_dirty = nullptr;        // k_refit_local work list
+    int n_dirty = 0;
+    int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
 };
 
@@ -1551,6 +1603,11 @@ void free_accel(rt_ctx* c) {
     hipFree(c->tleaf);
     hipFree(c->prims);
     hipFree(c->prim_idx_dev);
+    hipFree(c->pbox);
+    hipFree(c->refit_dirty);
+    c->pbox = nullptr;
+    c->refit_dirty = nullptr;
+    c->n_dirty = 0;
     c->anodes = c->lnodes = c->wnodes = c->prims = nullptr;
     c->tleaf = nullptr;
     c->prim_idx_dev = nullptr;
@@ -1805,6 +1862,7 @@ int prepare_animation(rt_ctx* c) {
         for (size_t q = 0; q < A.wchild.size(); ++q)
             if (A.wchild[q] >= 0) wpos[A.wchild[q]] = static_cast<int>(q);
         std::vector<int> wstamp(M, -1);
+        std::vector<char> dirty(M, 0);
         for (size_t p = 0; p < P; ++p) {
             const int i = which[A.prim_shape[p]];
             if (i < 0) continue;
@@ -1813,8 +1871,48 @@ int prepare_animation(rt_ctx* c) {
                 if (wpos[j] >= 0 && wstamp[j] != i) {
                     wstamp[j] = i;
                     wpos_of[i].push_back(wpos[j]);
+                    dirty[j] = 1;
                 }
         }
+        // prim range of every local subtree (contiguous: LocalBuilder emits a subtree's prims together)
+        std::vector<int> first(M, 0), end(M, 0);
+        for (size_t j = M; j-- > 0;) {  // children have larger indices than their parent
+            if (A.la[j] < 0) {
+                first[j] = -A.la[j] - 1;
+                end[j] = first[j] + A.lb[j];
+            } else {
+                const int l = A.la[j], r = A.lb[j] & 0x3fffffff;
+                if (end[l] != first[r]) return RT_ERR_BVH;  // not contiguous: cannot happen
+                first[j] = first[l];
+                end[j] = end[r];
+            }
+        }
+        std::vector<int4> work;
+        for (size_t j = 0; j < M; ++j)
+            if (dirty[j]) work.push_back(make_int4(wpos[j], first[j], end[j], 0));
+        std::vector<float4> pb(2 * (P ? P : 1), make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+        for (size_t p = 0; p < P; ++p) {
+            rta::Box3 b;
+            if (rta::classify(c->host_shapes[A.prim_shape[p]], b, A.origin_lim) != rta::BOUNDED) {
+                pb[2 * p + 1] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+                continue;
+            }
+            pb[2 * p] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
+            pb[2 * p + 1] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
+        }
+        hipFree(c->pbox);
+        hipFree(c->refit_dirty);
+        c->pbox = nullptr;
+        c->refit_dirty = nullptr;
+        c->n_dirty = 0;
+        if (hipMalloc(&c->pbox, pb.size() * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&c->refit_dirty, (work.empty() ? 1 : work.size()) * sizeof(int4)) != hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        HIP_TRY(hipMemcpyAsync(c->pbox, pb.data(), pb.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+        if (!work.empty())
+            HIP_TRY(hipMemcpyAsync(c->refit_dirty, work.data(), work.size() * sizeof(int4), hipMemcpyHostToDevice,
+                                   c->stream));
+        c->n_dirty = static_cast<int>(work.size());
     }
     // one int allocation: ids, then (offsets, list) x 4
     std::vector<int> buf(c->anim_ids);
@@ -1826,18 +1924,36 @@ int prepare_animation(rt_ctx* c) {
         list_at = buf.size();
         for (const auto& l : lists) buf.insert(buf.end(), l.begin(), l.end());
     };
+    // per reference node, the animated shapes it lists (k_grow_nodes)
+    std::vector<int> node_ids;
+    std::vector<std::vector<int>> lists_of;
+    {
+        std::vector<int> slot(N, -1);
+        for (int i = 0; i < n; ++i)
+            for (int k : nodes_of[i]) {
+                if (slot[k] < 0) {
+                    slot[k] = static_cast<int>(node_ids.size());
+                    node_ids.push_back(k);
+                    lists_of.emplace_back();
+                }
+                lists_of[slot[k]].push_back(i);
+            }
+    }
     size_t o[8];
-    append(nodes_of, o[0], o[1]);
-    append(slots_of, o[2], o[3]);
-    append(prims_of, o[4], o[5]);
-    append(wpos_of, o[6], o[7]);
+    append(slots_of, o[0], o[1]);
+    append(prims_of, o[2], o[3]);
+    append(wpos_of, o[4], o[5]);
+    append(lists_of, o[6], o[7]);
+    const size_t o_ids = buf.size();
+    buf.insert(buf.end(), node_ids.begin(), node_ids.end());
     int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
     if (rc != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int* d = c->anim_maps;
-    c->anim = AnimMaps{d, d + o[0], d + o[1], d + o[2], d + o[3], d + o[4], d + o[5], d + o[6], d + o[7], n};
-    return RT_OK;
+    c->anim = AnimMaps{d,         d + o[0], d + o[1], d + o[2], d + o[3], d + o[4],
+                       d + o[5],  d + o_ids, d + o[6], d + o[7], n,        static_cast<int>(node_ids.size())};
+    return ensure_staging(c->anim_sbox, c->anim_sbox_cap, 4 * static_cast<size_t>(n));
 }
 
 // (Re)builds the accelerator after the host copies changed, then the animation lists.
@@ -2070,6 +2186,7 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->sched_sets);
     hipFree(c->anim_maps);
     hipFree(c->anim_frame);
+    hipFree(c->anim_sbox);
     if (c->anim_pinned) hipHostFree(c->anim_pinned);
     if (c->anim_copied) hipEventDestroy(c->anim_copied);
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
@@ -2242,17 +2359,25 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     const size_t P = c->accel.prim_shape.size();
     const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat,
                       acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
-                      acc ? c->prim_idx_dev + P : nullptr, c->accel.origin_lim};
+                      acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
+                      c->accel.origin_lim};
     hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
                        reinterpret_cast<const FlatShape*>(c->anim_frame),
                        reinterpret_cast<const int*>(c->anim_frame + n * sizeof(FlatShape)), c->anim, out);
+    if (c->anim.nodes > 0)
+        hipLaunchKernelGGL(k_grow_nodes, dim3((c->anim.nodes + 3) / 4), dim3(256), 0, c->stream, c->anim, out);
+    if (acc && c->n_dirty > 0)
+        hipLaunchKernelGGL(k_refit_local, dim3((c->n_dirty + 3) / 4), dim3(256), 0, c->stream, c->refit_dirty,
+                           c->n_dirty, c->pbox, c->lnodes);
     if (c->N > 0)
         hipLaunchKernelGGL(k_refresh_nodes, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, c->N,
                            c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr);
     HIP_TRY(hipGetLastError());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
     c->nodes_on_device_newer = true;
-    return rebuild ? upload_accel(c) : RT_OK;  // a bound changed kind: rebuild from the grown nodes
+    if (!rebuild) return RT_OK;
+    ++c->anim_rebuilds;
+    return upload_accel(c);  // a bound changed kind: rebuild from the grown nodes
 }
 
 int rt_read_nodes(rt_ctx* c, FlatNode* nodes, int N) {
@@ -2417,6 +2542,8 @@ extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
     out->last_kernel = c->last_kind;
     return RT_OK;
 }
+
+extern "C" int rt_debug_anim_rebuilds(rt_ctx* c) { return c ? c->anim_rebuilds : -1; }
 
 extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
     if (!c || lane_from_depth < 0) return RT_ERR_INVALID;

@@ -504,6 +504,13 @@ class ComputeShader:
         o = np.ascontiguousarray(order if order is not None else [], np.int32)
         self._chk(fn(self._h, _ptr(o) if o.size else None, int(o.size)), "rt_debug_tile_order")
 
+    def debug_anim_rebuilds(self):
+        """Host rebuilds rt_animate fell back to since the context was made."""
+        fn = self._lib.rt_debug_anim_rebuilds
+        fn.argtypes = [_P]
+        fn.restype = _I
+        return int(fn(self._h))
+
     def debug_spec(self, mode):
         fn = self._lib.rt_debug_spec
         fn.argtypes = [_P, _I]

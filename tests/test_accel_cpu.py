@@ -228,3 +228,51 @@ def test_accel_small_shapes_far_origins(check_lib):
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     lim = rng.uniform(1, 3e4, R)
     compare(check_lib, fs2, o, d, lim)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_accel_stale_triangle_planes(check_lib, seed):
+    """Triangles turned while their stored plane stays (updateWheelAnimations,
+    src/main.cpp:1084-1109): the reference hits the stored plane and projects
+    onto the vertices' plane, so the INNER points are the triangle lifted onto
+    the stored plane; the conservative box is that lift (accel_bound.h). Angles
+    up to 88 degrees (past 87 degrees they stay unbounded), plus offsets."""
+    import test_gpu_parity as tg
+    fs = tg._soup(seed, n_tri=1500)
+    rng = np.random.default_rng(seed)
+    tri = np.where(fs.shapes["type"] == 3)[0]
+    turn = tri[rng.random(tri.size) < 0.6]
+    s = fs.shapes
+    for i in turn:
+        P = np.stack([s["triP1"][i], s["triP2"][i], s["triP3"][i]]).astype(np.float64)
+        c = P.mean(0)
+        ax = rng.normal(size=3)
+        ax /= np.linalg.norm(ax)
+        ang = rng.uniform(0, np.radians(89))
+        q = P - c
+        r = q * np.cos(ang) + np.cross(ax, q) * np.sin(ang) + np.outer(q @ ax, ax) * (1 - np.cos(ang))
+        r = (r + c + rng.normal(size=3) * 0.3).astype(np.float32)
+        s["triP1"][i], s["triP2"][i], s["triP3"][i] = r
+    # rays aimed at the edges of the lifted triangles, from near and far origins
+    R = 6000
+    k = rng.choice(turn, R)
+    P = np.stack([s["triP1"][k], s["triP2"][k], s["triP3"][k]], 1).astype(np.float64)
+    N = s["planeNormal"][k].astype(np.float64)
+    D = s["planeD"][k].astype(np.float64)
+    nt = np.cross(P[:, 1] - P[:, 0], P[:, 2] - P[:, 0])
+    nt /= np.linalg.norm(nt, axis=1, keepdims=True)
+    b = rng.dirichlet([1, 1, 1], R)
+    b[:, rng.integers(0, 3, R)[0]] *= rng.uniform(0.0, 0.05)  # pull towards an edge
+    b /= b.sum(1, keepdims=True)
+    q = (P * b[:, :, None]).sum(1)
+    h = -((N * q).sum(1) + D) / (N * nt).sum(1)
+    tgt = q + nt * np.clip(h, -1e3, 1e3)[:, None]
+    u = rng.normal(size=(R, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    ot = tgt + u * rng.choice([3.0, 30.0, 90.0], (R, 1))
+    dt = (tgt - ot) / np.linalg.norm(tgt - ot, axis=1, keepdims=True)
+    o, d = random_rays(rng, 6000)
+    o1, d1 = camera_rays(fs, 64, 48)
+    o, d = np.concatenate([o, o1, ot]), np.concatenate([d, d1, dt])
+    lim = rng.uniform(1, 200, len(o))
+    compare(check_lib, fs, o, d, lim)

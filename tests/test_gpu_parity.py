@@ -512,11 +512,13 @@ def test_device_refit_class_change_rebuilds(ctx):
 
     def degenerate(k, rec):
         if k >= 1:
-            t = np.where(rec["type"] == 3)[0][0]
+            t = np.where(rec["type"] == 3)[0][1]  # [0] is one of _soup's slivers already
             rec["triP3"][t] = rec["triP1"][t] + (rec["triP2"][t] - rec["triP1"][t]) * np.float32(0.5)
         if k == 3:
             rec["sphereRadius"][0] = np.float32(np.inf)
+    r0 = ctx.debug_anim_rebuilds()
     _refit_case(ctx, fs, ids, 4, rtamd.KERNEL_ACCEL, mutate=degenerate)
+    assert ctx.debug_anim_rebuilds() - r0 == 2  # the sliver at step 1, the infinite sphere at step 3
     ctx.set_kernel(rtamd.KERNEL_AUTO)
 
 
