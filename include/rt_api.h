@@ -64,6 +64,11 @@ typedef struct rt_accel_info {
     int always_prims;        /* shapes tested whenever their leaf is entered          */
     int max_stack;           /* worst-case wave stack entries                          */
     int last_kernel;         /* rt_kernel of the latest render dispatch               */
+    int scene_tree;          /* 1 if the scene tree is built (rt_set_tree)             */
+    int scene_nodes;         /* its wide nodes                                         */
+    int scene_items;         /* its leaves (shapes of one reference leaf each)         */
+    int scene_height;        /* its binary height                                      */
+    int tree_nested;         /* the reference tree's child boxes lie in their parents' */
 } rt_accel_info;
 
 /* Work counted on the reference's own traversal (gpu_shader.comp:380-430 and
@@ -191,6 +196,16 @@ int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
  * when pixels are computed, never their values. */
 enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1 };
 int rt_set_schedule(struct rt_ctx* ctx, int mode);
+
+/* Which tree the accelerated kernel walks. RT_TREE_SCENE (default): when the
+ * reference tree's child boxes nest in their parents' boxes, rays whose slab
+ * values cannot be NaN walk one SAH tree over all reference leaves' shapes,
+ * testing each leaf's own exact box before its shapes (the nesting makes that
+ * test equivalent to the reference's walk down to the leaf); other rays, and
+ * animated scenes (rt_set_animated), walk the reference tree. RT_TREE_REFERENCE:
+ * every ray walks the reference tree. Same image either way. */
+enum rt_tree { RT_TREE_REFERENCE = 0, RT_TREE_SCENE = 1 };
+int rt_set_tree(struct rt_ctx* ctx, int mode);
 
 /* Accelerator statistics for the uploaded scene. */
 int rt_accel_info_get(struct rt_ctx* ctx, rt_accel_info* out);

@@ -278,6 +278,296 @@ int make_wide(AccelHost& A, int j, int budget, std::vector<int>& memo, int& pend
 
 }  // namespace
 
+namespace {
+
+// An atom of the scene tree: the bounded shapes of a small reference leaf
+// (kept together), one bounded shape of a large leaf, or up to four unbounded
+// shapes of one leaf (infinite box). `first`/`n` index SceneBuilder::ap.
+struct Atom {
+    int ref, first, n;
+    Box3 box;
+    float c[3];
+};
+
+int log2_ceil(int n) {
+    int h = 0;
+    while ((1 << h) < n) ++h;
+    return h;
+}
+
+// Binned SAH over atom centroids (cost = box area x shapes), into T's
+// lbox / la / lb / prim_shape / prim_seq (the layout of a local tree, so the
+// cone and wide-collapse passes apply). A leaf holds atoms of one reference
+// leaf only (n == 1, or all of one leaf with <= 4 shapes). Splits fall back to
+// the median where the SAH choice would let the height exceed `hmax`.
+struct SceneBuilder {
+    AccelHost& T;
+    std::vector<Atom> atoms;
+    std::vector<std::pair<int, int>> ap;  // (shape, seq)
+    std::vector<int> leaf_ref;            // per node: reference leaf of a leaf, -1 inner
+    int hmax = 0, height = 0;
+
+    int leaf(int b, int e) {
+        const int k = static_cast<int>(T.lbox.size());
+        Box3 box = empty_box();
+        std::vector<std::pair<int, int>> ps;
+        for (int i = b; i < e; ++i) {
+            grow(box, atoms[i].box);
+            for (int q = atoms[i].first; q < atoms[i].first + atoms[i].n; ++q) ps.push_back(ap[q]);
+        }
+        std::sort(ps.begin(), ps.end(), [](const auto& x, const auto& y) { return x.second < y.second; });
+        T.lbox.push_back(box);
+        T.la.push_back(-(static_cast<int>(T.prim_shape.size()) + 1));
+        T.lb.push_back(static_cast<int>(ps.size()));
+        leaf_ref.push_back(atoms[b].ref);
+        for (auto [si, seq] : ps) {
+            T.prim_shape.push_back(si);
+            T.prim_seq.push_back(seq);
+        }
+        return k;
+    }
+
+    int inner(const Box3& box, int l, int r, int axis) {
+        const int k = static_cast<int>(T.lbox.size());
+        T.lbox.push_back(box);
+        T.la.push_back(l);
+        T.lb.push_back(r | (axis << 30));
+        leaf_ref.push_back(-1);
+        return k;
+    }
+
+    // bounded = false: atoms with infinite boxes, split by count only.
+    int build(int b, int e, int depth, bool bounded) {
+        height = std::max(height, depth);
+        const int n = e - b;
+        bool same = true;
+        int tot = 0;
+        for (int i = b; i < e; ++i) {
+            same = same && atoms[i].ref == atoms[b].ref;
+            tot += atoms[i].n;
+        }
+        if (n == 1 || (same && tot <= 4)) return leaf(b, e);
+        Box3 box = empty_box();
+        float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i = b; i < e; ++i) {
+            grow(box, atoms[i].box);
+            for (int a = 0; a < 3; ++a) {
+                clo[a] = std::min(clo[a], atoms[i].c[a]);
+                chi[a] = std::max(chi[a], atoms[i].c[a]);
+            }
+        }
+        int axis = 0;
+        for (int a = 1; a < 3; ++a)
+            if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+        const int room = hmax - depth - 1;
+        constexpr int kBins = 32;
+        auto bin_of = [&](const Atom& it, int ax) {
+            const float ext = chi[ax] - clo[ax];
+            int k = static_cast<int>((it.c[ax] - clo[ax]) / ext * kBins);
+            return std::min(kBins - 1, std::max(0, k));
+        };
+        float best = INFINITY;
+        int best_k = -1, best_axis = -1;
+        for (int ax = 0; bounded && ax < 3; ++ax) {
+            if (!(chi[ax] - clo[ax] > 0)) continue;
+            int cnt[kBins] = {0}, acnt[kBins] = {0};
+            Box3 bb[kBins];
+            for (auto& x : bb) x = empty_box();
+            for (int i = b; i < e; ++i) {
+                const int k = bin_of(atoms[i], ax);
+                cnt[k] += atoms[i].n;
+                ++acnt[k];
+                grow(bb[k], atoms[i].box);
+            }
+            Box3 lacc = empty_box();
+            int lcnt = 0, lat = 0;
+            float lcost[kBins];
+            int lats[kBins];
+            for (int k = 0; k < kBins - 1; ++k) {
+                grow(lacc, bb[k]);
+                lcnt += cnt[k];
+                lat += acnt[k];
+                lcost[k] = lcnt ? area(lacc) * lcnt : 0.f;
+                lats[k] = lat;
+            }
+            Box3 racc = empty_box();
+            int rcnt = 0, rat = 0;
+            for (int k = kBins - 1; k >= 1; --k) {
+                grow(racc, bb[k]);
+                rcnt += cnt[k];
+                rat += acnt[k];
+                const float c = lcost[k - 1] + (rcnt ? area(racc) * rcnt : 0.f);
+                if (rat && rat < n && log2_ceil(lats[k - 1]) <= room && log2_ceil(rat) <= room && c < best) {
+                    best = c;
+                    best_k = k;
+                    best_axis = ax;
+                }
+            }
+        }
+        int mid = b;
+        if (best_k > 0) {
+            axis = best_axis;
+            auto it = std::partition(atoms.begin() + b, atoms.begin() + e,
+                                     [&](const Atom& x) { return bin_of(x, axis) < best_k; });
+            mid = static_cast<int>(it - atoms.begin());
+        }
+        if (mid <= b || mid >= e) {  // median (no useful SAH split, height bound, or unbounded atoms)
+            mid = b + n / 2;
+            if (bounded)
+                std::nth_element(atoms.begin() + b, atoms.begin() + mid, atoms.begin() + e,
+                                 [&](const Atom& x, const Atom& y) { return x.c[axis] < y.c[axis]; });
+        }
+        const int k = inner(box, 0, 0, axis);
+        const int l = build(b, mid, depth + 1, bounded);
+        const int r = build(mid, e, depth + 1, bounded);
+        T.la[k] = l;
+        T.lb[k] = r | (axis << 30);
+        return k;
+    }
+};
+
+bool boxes_nest(const FlatNode& p, const FlatNode& ch) {
+    const float plo[3] = {p.boundsMin.x, p.boundsMin.y, p.boundsMin.z};
+    const float phi[3] = {p.boundsMax.x, p.boundsMax.y, p.boundsMax.z};
+    const float clo[3] = {ch.boundsMin.x, ch.boundsMin.y, ch.boundsMin.z};
+    const float chi[3] = {ch.boundsMax.x, ch.boundsMax.y, ch.boundsMax.z};
+    for (int a = 0; a < 3; ++a)
+        if (!(plo[a] <= clo[a] && clo[a] <= phi[a] && plo[a] <= chi[a] && chi[a] <= phi[a])) return false;
+    return true;
+}
+
+}  // namespace
+
+// Builds out.st (accel.h, SceneTree) when the reference tree's boxes nest
+// (out.st.wroot = -1 otherwise); st.max_stack <= cap sizes its LDS stack.
+// Binary height bound of the scene tree (median splits below it).
+constexpr int kSceneHeight = 40;
+
+static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int N, const int* idx,
+                             const std::vector<char>& reach, const std::vector<int>& seq_base,
+                             const std::vector<int>& scls, const std::vector<Box3>& sbox, int cap, AccelHost& out) {
+    SceneTree& st = out.st;
+    st = SceneTree();
+    out.st_cone.clear();
+    if (N <= 0 || N >= (1 << 28)) return;
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = nodes[k];
+        if (!reach[k] || nd.leftChild == -1) continue;
+        if (!boxes_nest(nd, nodes[nd.leftChild]) || !boxes_nest(nd, nodes[nd.rightChild])) return;
+    }
+    st.nested = 1;
+    AccelHost T;
+    SceneBuilder sb{T, {}, {}, {}, kSceneHeight, 0};
+    std::vector<Atom> unb;
+    const Box3 inf_box{{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}};
+    // An unbounded shape is tested only when the ray passes its reference leaf's
+    // exact box; that box, padded like the shape bounds, contains every such
+    // ray's slab interval (accel_math.h), though not necessarily the hit.
+    auto leaf_pad = [&](const FlatNode& nd) {
+        BoxAcc acc;
+        for (int q = 0; q < 8; ++q)
+            acc.add(D3{(q & 1) ? nd.boundsMax.x : nd.boundsMin.x, (q & 2) ? nd.boundsMax.y : nd.boundsMin.y,
+                       (q & 4) ? nd.boundsMax.z : nd.boundsMin.z});
+        Box3 b = finish(acc, out.origin_lim);
+        for (int a = 0; a < 3; ++a)
+            if (!(b.lo[a] <= b.hi[a])) return inf_box;  // NaN from infinite bounds: no bound at all
+        return b;
+    };
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = nodes[k];
+        if (!reach[k] || nd.leftChild != -1) continue;
+        std::vector<int> bnd;
+        std::vector<std::pair<int, int>> ub;
+        for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
+            const int si = idx[nd.startShapeIdx + i];
+            if (scls[si] == NEVER) continue;
+            if (scls[si] == UNBOUNDED) ub.push_back({si, seq_base[k] + i});
+            else bnd.push_back(i);
+        }
+        auto add = [&](std::vector<Atom>& dst, const std::vector<std::pair<int, int>>& ps, const Box3& box) {
+            Atom at{k, static_cast<int>(sb.ap.size()), static_cast<int>(ps.size()), box, {0.f, 0.f, 0.f}};
+            for (int a = 0; a < 3; ++a) at.c[a] = std::isfinite(box.lo[a]) ? 0.5f * (box.lo[a] + box.hi[a]) : 0.f;
+            sb.ap.insert(sb.ap.end(), ps.begin(), ps.end());
+            dst.push_back(at);
+        };
+        if (bnd.size() <= 4) {
+            if (!bnd.empty()) {
+                Box3 box = empty_box();
+                std::vector<std::pair<int, int>> ps;
+                for (int i : bnd) {
+                    const int si = idx[nd.startShapeIdx + i];
+                    grow(box, sbox[si]);
+                    ps.push_back({si, seq_base[k] + i});
+                }
+                add(sb.atoms, ps, box);
+            }
+        } else {
+            for (int i : bnd) {
+                const int si = idx[nd.startShapeIdx + i];
+                add(sb.atoms, {{si, seq_base[k] + i}}, sbox[si]);
+            }
+        }
+        for (size_t q = 0; q < ub.size(); q += 4)
+            add(unb, std::vector<std::pair<int, int>>(ub.begin() + q, ub.begin() + std::min(ub.size(), q + 4)),
+                leaf_pad(nd));
+    }
+    const int nb = static_cast<int>(sb.atoms.size()), nu = static_cast<int>(unb.size());
+    if (nb + nu == 0) return;
+    sb.atoms.insert(sb.atoms.end(), unb.begin(), unb.end());
+    // bounded atoms under one SAH tree, unbounded ones under another whose
+    // boxes carry no distance bound (kNoPrune: entered at parameter 0)
+    int root, unb_root = -1;
+    if (nb > 0 && nu > 0) {
+        root = sb.inner(inf_box, 0, 0, 0);
+        const int l = sb.build(0, nb, 1, true);
+        unb_root = sb.build(nb, nb + nu, 1, true);
+        T.la[root] = l;
+        T.lb[root] = unb_root;
+    } else {
+        root = sb.build(0, nb + nu, 0, true);
+        if (nu > 0) unb_root = root;
+    }
+    st.height = sb.height;
+    build_cones(shapes, T);
+    if (unb_root >= 0) {  // the unbounded subtree is built last: its nodes are [unb_root, end)
+        for (size_t j = static_cast<size_t>(unb_root); j < T.lbox.size(); ++j) T.lcone[4 * j + 3] = kNoPrune;
+    }
+    // Full 4-wide collapse: the walks have no static stack bound on the scene
+    // tree (a lane that runs out of entries walks the reference tree instead,
+    // rt_kernels.hip lane_walk), so max_stack only sizes the LDS stack.
+    int pend = 0;
+    if (T.la[root] >= 0) {
+        std::vector<int> memo(T.lbox.size(), -1);
+        st.wroot = make_wide(T, root, 1 << 20, memo, pend);
+    } else {
+        st.wroot = 0;
+        T.wchild.assign(kWide, -1);
+        T.wsub.assign(kWide, -1);
+        T.wchild[0] = root;
+    }
+    st.max_stack = std::min(pend + 2, cap);
+    // merge: the scene tree's prims follow the local ones
+    const int P0 = static_cast<int>(out.prim_shape.size());
+    out.prim_shape.insert(out.prim_shape.end(), T.prim_shape.begin(), T.prim_shape.end());
+    out.prim_seq.insert(out.prim_seq.end(), T.prim_seq.begin(), T.prim_seq.end());
+    st.box = T.lbox;
+    st.a = T.la;
+    st.b = T.lb;
+    st.item_of.assign(T.lbox.size(), -1);
+    for (size_t j = 0; j < T.lbox.size(); ++j) {
+        if (T.la[j] >= 0) continue;
+        const int start = -T.la[j] - 1 + P0;
+        st.a[j] = -(start + 1);
+        st.item_of[j] = static_cast<int>(st.item_ref.size());
+        st.item_ref.push_back(sb.leaf_ref[j]);
+        st.item_start.push_back(start);
+        st.item_count.push_back(T.lb[j]);
+    }
+    st.wchild = T.wchild;
+    st.wsub = T.wsub;
+    out.st_cone = T.lcone;
+}
+
 // Wide collapse of every local tree within the lane stack budget `cap`;
 // returns the stack bound of the lane walk over them.
 static int build_wide(AccelHost& A, const std::vector<int>& ref_depth, int cap) {
@@ -424,6 +714,9 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     visit(N - 1);
     build_cones(shapes, out);
     max_stack = std::max(max_stack, build_wide(out, depth, kLaneStack));
+    if (max_stack > stack_cap) return false;
+    build_scene_tree(shapes, nodes, N, idx, reach, seq_base, scls, sbox, std::min(stack_cap, kLaneStack), out);
+    if (out.st.wroot >= 0) max_stack = std::max(max_stack, out.st.max_stack);
     out.max_stack = max_stack;
     return max_stack <= stack_cap;
 }

@@ -30,6 +30,35 @@
 
 namespace rta {
 
+// Scene tree (build_scene_tree): one SAH tree over the shapes of every
+// reference leaf, for rays whose slab values cannot be NaN (finite origin,
+// finite non-zero 1/d). When every child box of the reference tree lies inside
+// its parent's box, such a ray passes the exact test (gpu_shader.comp:364-377)
+// of every ancestor of a leaf whose own box it passes: per axis the rounded
+// slab values of the child lie between the parent's (rounding is monotone),
+// so tmin only grows and tmax only shrinks going up. The reference therefore
+// tests a leaf's shapes iff the ray passes that leaf's own box, and the tree
+// above the leaves may be any tree. Each scene-tree leaf ("item") holds shapes
+// of ONE reference leaf and carries that leaf's exact box, tested before its
+// shapes; the inner boxes are the conservative shape bounds, as in the local
+// BVHs. Unbounded shapes (planes, ...) sit in a separate subtree over their
+// leaves' padded exact boxes, which bound where the ray may be when the leaf
+// is entered but not where it hits: those nodes have cone threshold kNoPrune
+// (never culled by cone or distance; entered at parameter 0).
+struct SceneTree {
+    // binary nodes: inner a = left, b = right | axis << 30; leaf a = -(start+1), b = count
+    std::vector<Box3> box;
+    std::vector<int> a, b;
+    std::vector<int> item_of;   // per node: item id of a leaf, -1 for inner
+    std::vector<int> item_ref;  // per item: its reference leaf
+    std::vector<int> item_start, item_count;  // per item: prim range (AccelHost prims)
+    std::vector<int> wchild, wsub;            // wide collapse (as AccelHost)
+    int wroot = -1;             // wide root, -1: no scene tree for this scene
+    int max_stack = 0;          // the lane walk's stack bound over it
+    int height = 0;             // binary height
+    int nested = 0;             // the reference tree's boxes nest (the condition above)
+};
+
 struct AccelHost {
     // prims: the shapes in the order the accelerated kernel reads them.
     std::vector<int> prim_shape;  // shape index per prim slot
@@ -60,6 +89,10 @@ struct AccelHost {
     // frame (rt_kernels.hip, launch()).
     float scene_mag = 0.f, origin_lim = 0.f;
     int always_prims = 0, bounded_prims = 0, local_leaves = 0;
+    // Scene tree; its prims follow the local ones in prim_shape / prim_seq,
+    // its cones are in st_cone (4 per binary node, as lcone).
+    SceneTree st;
+    std::vector<float> st_cone;
 };
 
 // Builds the accelerator for a validated reference tree (see check_tree).
@@ -71,6 +104,8 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 void build_cones(const FlatShape* shapes, AccelHost& A);
 
 constexpr int kWide = 4;
+// Cone threshold of a scene-tree node without a distance bound (SceneTree).
+constexpr float kNoPrune = -8.0f;
 // Stack entries the lane walk keeps per lane in LDS (6 B each: code + bf16
 // entry parameter): 26 x 64 lanes x 6 B fits 16 waves per CU in 160 KB. The
 // wide collapse stays within it wherever the binary tree allows.

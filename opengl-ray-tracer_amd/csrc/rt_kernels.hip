@@ -27,6 +27,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <new>
 #include <vector>
 
@@ -535,13 +536,16 @@ struct AccelPtrs {
     const float4* __restrict__ lnodes;  // 6 float4 per local inner node: both child boxes + codes, cones
     const float4* __restrict__ wnodes;  // 8 float4 per reference inner node: both children's exact + content boxes
     const int4* __restrict__ tleaf;     // per reference leaf: plain start, plain count, local root code
+    const float4* __restrict__ titems;  // 2 float4 per scene-tree item: exact box of its reference leaf + range
+    int troot;                          // scene-tree root code (kLocal|w), kNoChild: reference tree only
+    int scene_stack;                    // stack entries a scene-tree walk may use (<= the walk's own cap)
     int N;
     float origin_lim;                   // AccelHost::origin_lim
     int boxes_finite;                   // no reference node box holds a NaN (ray_aabb_fast)
 };
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
-constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u, kTopLeaf = 0x20000000u;
+constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u, kTopLeaf = 0x20000000u, kItem = 0x10000000u;
 constexpr int kNoChild = 0x7fffffff;
 
 struct Best {
@@ -672,6 +676,24 @@ __device__ __forceinline__ bool cone_ok(const rta::RayC& c, float4 k) {
     return !rta::cone_culls(c, k.x, k.y, k.z, k.w);
 }
 
+// Scene-tree item (accel.h, SceneTree): the exact box test of its reference
+// leaf (gpu_shader.comp:364-377; NaN-free for the rays that take the scene
+// tree), then its prim range.
+__device__ __forceinline__ bool enter_item(const AccelPtrs& A, unsigned uc, const Ray& r, const V& inv, int& start,
+                                           int& count) {
+    const float4* q = A.titems + 2 * static_cast<size_t>(uc & 0x0fffffffu);
+    const float4 e0 = q[0], e1 = q[1];
+    start = __float_as_int(e0.w);
+    count = __float_as_int(e1.w);
+    return ray_aabb_fast(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z));
+}
+
+// A ray walks the scene tree when one is built and its slab values cannot be
+// NaN (aabb_fast_ok) and the padded tests are in their bounded mode (c.ix != 0).
+__device__ __forceinline__ bool use_scene(const AccelPtrs& A, bool fast, const rta::RayC& c) {
+    return A.troot != kNoChild && fast && c.ix != 0.0f;
+}
+
 // The root has no parent: its own exact box decides entry (gpu_shader.comp:386-395),
 // then its content box.
 __device__ __forceinline__ bool enter_root(const AccelPtrs& A, const Ray& r, const V& inv, const rta::RayC& c,
@@ -755,14 +777,17 @@ __device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f
     const f2 dz = {c.dz, c.dz}, dy = {c.dy, c.dy}, dx = {c.dx, c.dx};
     const f2 dn = fma2(ax, dx, fma2(ay, dy, az * dz));
     const f2 thr = th - (f2){rta::kConeEps, rta::kConeEps};
-    float tn[2], tf[2];
+    float tn[2], tf[2], te[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
+        // kNoPrune children (accel.h): no distance limit, entered at parameter 0
+        const bool np = th[k] < -6.0f;
         tn[k] = fmaxf(fmaxf(fminf(x0[k], x1[k]), fminf(y0[k], y1[k])), fmaxf(fminf(z0[k], z1[k]), 0.0f));
-        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), fminf(fmaxf(z0[k], z1[k]), tl));
+        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), fminf(fmaxf(z0[k], z1[k]), np ? INFINITY : tl));
+        te[k] = np ? 0.0f : tn[k];
     }
-    t0 = tn[0];
-    t1 = tn[1];
+    t0 = te[0];
+    t1 = te[1];
     h0 = (tn[0] <= tf[0]) & !(dn[0] < thr[0]);
     h1 = (tn[1] <= tf[1]) & !(dn[1] < thr[1]);
 }
@@ -817,8 +842,17 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
     const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
     const rta::RayC c = ray_c(r, A.origin_lim);
     float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
-    int sp = 0, cur = 0;
-    bool have = enter_root(A, r, inv, c, tl, cur);
+    int sp = 0, cur = A.troot;
+    bool have = true;
+    // The scene tree has no static stack bound: a lane whose push would not fit
+    // drops it and marks `ovf`; when its walk ends it walks the reference tree
+    // from the root (with the best hit so far), whose bound the builder checked.
+    bool ovf = false;
+    int pcap = min(cap, A.scene_stack);  // push bound of the tree being walked
+    if (!use_scene(A, fast, c)) {
+        have = enter_root(A, r, inv, c, tl, cur);
+        pcap = cap;
+    }
     bool ended = false;
     for (;;) {
         // While-while: a lane descends until it holds a leaf. SPEC (speculative):
@@ -832,6 +866,14 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 if (SPEC ? __ballot(!ended && count == 0) == 0 : count > 0) break;
                 if (!have) {
                     if (sp == 0) {
+                        if (ovf) {  // a scene-tree push was dropped: the reference tree, from its root
+                            ovf = false;
+                            pcap = cap;
+                            if (enter_root(A, r, inv, c, tl, cur)) {
+                                have = true;
+                                continue;
+                            }
+                        }
                         if (count == 0) ended = true;  // walk finished (a held leaf is still tested)
                         break;
                     }
@@ -845,8 +887,14 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 if (COUNT) wc.nodes++;
                 if (WSTAT && first_active()) wc.wnodes++;
                 have = false;
-                if (uc & kTopLeaf) {
-                    const int4 lf = A.tleaf[uc & 0x1fffffffu];
+                if ((uc & (kTopLeaf | kItem)) == (kTopLeaf | kItem)) {
+                    int s0, n0;
+                    if (enter_item(A, uc, r, inv, s0, n0)) {
+                        start = s0;
+                        count = n0;
+                    }
+                } else if (uc & kTopLeaf) {
+                    const int4 lf = A.tleaf[uc & 0x0fffffffu];
                     start = lf.x;
                     count = lf.y;
                     if (lf.z != kNoChild) {
@@ -861,10 +909,14 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     sort4(w);
 #pragma unroll
                     for (int s2 = 3; s2 >= 1; --s2) {
-                        if (w.t[s2] < INFINITY && sp < cap) {
-                            stk[sp * stride] = w.code[s2];
-                            stt[sp * stride] = f_bf16_down(w.t[s2]);
-                            ++sp;
+                        if (w.t[s2] < INFINITY) {
+                            if (sp < pcap) {
+                                stk[sp * stride] = w.code[s2];
+                                stt[sp * stride] = f_bf16_down(w.t[s2]);
+                                ++sp;
+                            } else {
+                                ovf = true;  // scene tree only: local trees fit their bound
+                            }
                         }
                     }
                     if (w.t[0] < INFINITY) {
@@ -922,16 +974,37 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
     float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
     WaveStack st{0, 0, 0, 0};
     int cur = 0;
+    unsigned long long ovf = 0;  // lanes whose scene-tree pushes were dropped (see lane_walk)
+    int pcap = kMaxStack;        // push bound of the tree being walked (uniform)
     {
         int code = 0;
-        const bool h = enter_root(A, r, inv, c, tl, code) && active;  // code is the same in every lane
-        m = __ballot(h);
+        const bool scene = use_scene(A, fast, c);
+        const bool hr = enter_root(A, r, inv, c, tl, code);  // code is the same in every lane
+        const unsigned long long mr = __ballot(active && !scene && hr), ms = __ballot(active && scene);
         cur = uni(code);
+        m = mr;
+        if (ms) {  // scene-tree lanes first; reference-tree lanes (if any) follow as if overflowed
+            ovf = mr;
+            cur = A.troot;
+            m = ms;
+            pcap = min(kMaxStack, A.scene_stack);
+        }
     }
     unsigned long long done = 0;
     for (;;) {
         if (m == 0) {
-            if (st.sp == 0) return;
+            if (st.sp == 0) {
+                if (!ovf) return;
+                // scene-tree pushes were dropped for the lanes in ovf: they walk the
+                // reference tree from its root (with their best hits so far)
+                int code = 0;
+                const bool hr = enter_root(A, r, inv, c, tl, code);
+                m = __ballot(lane_in(ovf) && hr) & ~done;
+                ovf = 0;
+                pcap = kMaxStack;
+                cur = uni(code);
+                continue;
+            }
             st.pop(cur, m);
             cur = uni(cur);
             if (SHADOW) m &= ~done;
@@ -942,8 +1015,13 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
         const unsigned uc = static_cast<unsigned>(cur);
         Kids k{0, 0, 0.f, 0.f, false, false};
         int start = 0, count = 0;
-        if (uc & kTopLeaf) {
-            const int4 lf = A.tleaf[uc & 0x1fffffffu];
+        bool item_in = true;
+        if ((uc & (kTopLeaf | kItem)) == (kTopLeaf | kItem)) {
+            item_in = enter_item(A, uc, r, inv, start, count);
+            start = uni(start);
+            count = uni(count);
+        } else if (uc & kTopLeaf) {
+            const int4 lf = A.tleaf[uc & 0x0fffffffu];
             start = uni(lf.x);
             count = uni(lf.y);
             k.ca = uni(lf.z);
@@ -981,7 +1059,10 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
 #undef RT_CAS3
 #pragma unroll
             for (int s2 = 3; s2 >= 1; --s2)
-                if (wm[s2] && st.sp < kMaxStack) st.push(code[s2], wm[s2]);
+                if (wm[s2]) {
+                    if (st.sp < pcap) st.push(code[s2], wm[s2]);
+                    else ovf |= wm[s2];  // scene tree only: local trees fit their bound
+                }
             cur = code[0];
             m = wm[0];
             continue;
@@ -991,7 +1072,7 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
             k.cb = uni(k.cb);
         }
         if (count > 0) {
-            bool live = lane_in(m);
+            bool live = lane_in(m) && item_in;
             for (int i = 0; i < count; ++i) {
                 const GeoRec g = load_rec(A.prims, start + i);
                 if (WSTAT) wc.wtests += lane_id() == 0 ? 1u : 0u;
@@ -1517,6 +1598,10 @@ struct rt_ctx {
     // exact-result accelerator (accel.h); device copies in the layouts of AccelPtrs
     float4 *anodes = nullptr, *lnodes = nullptr, *wnodes = nullptr, *prims = nullptr;
     int4* tleaf = nullptr;
+    float4* titems = nullptr;  // scene-tree items (AccelPtrs::titems)
+    int st_root = 0x7fffffff;  // scene-tree root code, kNoChild if none
+    int tree_mode = 1;         // rt_set_tree
+    int scene_stack = 0;       // rt_debug_scene_stack (0: the walk's own cap)
     int* prim_idx_dev = nullptr;
     bool accel_ok = false;
     int boxes_finite = 0;
@@ -1601,6 +1686,9 @@ void free_accel(rt_ctx* c) {
     hipFree(c->lnodes);
     hipFree(c->wnodes);
     hipFree(c->tleaf);
+    hipFree(c->titems);
+    c->titems = nullptr;
+    c->st_root = kNoChild;
     hipFree(c->prims);
     hipFree(c->prim_idx_dev);
     hipFree(c->pbox);
@@ -1675,7 +1763,7 @@ int build_upload_accel(rt_ctx* c) {
     if (!rta::build_accel(c->host_shapes.data(), c->S, c->host_nodes.data(), N, c->host_idx.data(), c->I,
                           kLeafScan, kMaxStack, A))
         return RT_OK;
-    if (N >= (1 << 29)) return RT_OK;  // codes carry the node index in 29 bits
+    if (N >= (1 << 28)) return RT_OK;  // codes carry the node index in 28 bits
     c->boxes_finite = 1;
     for (int k = 0; k < N; ++k) {
         const FlatNode& n = c->host_nodes[k];
@@ -1700,30 +1788,53 @@ int build_upload_accel(rt_ctx* c) {
         if (st >= (1u << 22) || cnt > 255u) codes_ok = false;
         return static_cast<int>(kLocal | kLeaf | (st << 8) | cnt);
     };
+    // The scene tree's wide nodes (accel.h, SceneTree) follow the local ones;
+    // its leaves are item codes (kTopLeaf | kItem | item).
+    const rta::SceneTree& T = A.st;
+    const bool use_st = T.wroot >= 0;
     const size_t nw = A.wchild.size() / rta::kWide;
-    std::vector<float4> ln(11 * (nw ? nw : 1));
-    for (size_t w = 0; w < nw; ++w) {
+    const size_t nws = use_st ? T.wchild.size() / rta::kWide : 0;
+    if (nw + nws >= (1u << 28) || T.item_ref.size() >= (1u << 28)) return RT_OK;
+    std::vector<float4> ln(11 * (nw + nws ? nw + nws : 1));
+    auto emit_wide = [&](size_t w, size_t at, const std::vector<int>& wchild, const std::vector<int>& wsub,
+                         const std::vector<rta::Box3>& boxes, const std::vector<float>& cones,
+                         const std::function<int(int)>& leaf_of, size_t sub_base) {
         float v[11][4];
         for (int s2 = 0; s2 < 4; ++s2) {
-            const int j = A.wchild[rta::kWide * w + s2];
+            const int j = wchild[rta::kWide * w + s2];
             int code = kNoChild;
             float box[6] = {0, 0, 0, 0, 0, 0}, cone[4] = {0, 0, 0, -4.f};
             if (j >= 0) {
-                const rta::Box3& bx = A.lbox[j];
+                const rta::Box3& bx = boxes[j];
                 for (int a = 0; a < 3; ++a) {
                     box[a] = bx.lo[a];
                     box[3 + a] = bx.hi[a];
                 }
-                for (int a = 0; a < 4; ++a) cone[a] = A.lcone[4 * j + a];
-                if (!c->cone_cull) cone[3] = -4.f;
-                code = A.la[j] < 0 ? leaf_code(static_cast<size_t>(j))
-                                   : static_cast<int>(kLocal | static_cast<unsigned>(A.wsub[rta::kWide * w + s2]));
+                for (int a = 0; a < 4; ++a) cone[a] = cones[4 * j + a];
+                if (!c->cone_cull && cone[3] > rta::kNoPrune) cone[3] = -4.f;
+                const int sub = wsub[rta::kWide * w + s2];
+                code = sub < 0 ? leaf_of(j) : static_cast<int>(kLocal | static_cast<unsigned>(sub_base + sub));
             }
             for (int a = 0; a < 6; ++a) v[a][s2] = box[a];
             for (int a = 0; a < 4; ++a) v[6 + a][s2] = cone[a];
             v[10][s2] = bits_f(code);
         }
-        for (int r = 0; r < 11; ++r) ln[11 * w + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+        for (int r = 0; r < 11; ++r) ln[11 * at + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+    };
+    for (size_t w = 0; w < nw; ++w)
+        emit_wide(w, w, A.wchild, A.wsub, A.lbox, A.lcone, [&](int j) { return leaf_code(static_cast<size_t>(j)); },
+                  0);
+    std::vector<float4> ti(2 * (use_st ? T.item_ref.size() : 1));
+    if (use_st) {
+        for (size_t w = 0; w < nws; ++w)
+            emit_wide(w, nw + w, T.wchild, T.wsub, T.box, A.st_cone,
+                      [&](int j) { return static_cast<int>(kTopLeaf | kItem | static_cast<unsigned>(T.item_of[j])); },
+                      nw);
+        for (size_t i = 0; i < T.item_ref.size(); ++i) {
+            const FlatNode& n = c->host_nodes[T.item_ref[i]];
+            ti[2 * i] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(T.item_start[i]));
+            ti[2 * i + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(T.item_count[i]));
+        }
     }
     // wnodes: per reference inner node both children's exact + content boxes;
     // tleaf: per reference leaf its plain range and local root code.
@@ -1762,6 +1873,7 @@ int build_upload_accel(rt_ctx* c) {
         hipMalloc(&c->lnodes, ln.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->wnodes, wn.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->tleaf, tl.size() * sizeof(int4)) != hipSuccess ||
+        hipMalloc(&c->titems, ti.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->prims, 5 * (P ? P : 1) * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->prim_idx_dev, ps.size() * sizeof(int)) != hipSuccess)
         return RT_ERR_NO_MEMORY;
@@ -1769,12 +1881,14 @@ int build_upload_accel(rt_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->lnodes, ln.data(), ln.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->tleaf, tl.data(), tl.size() * sizeof(int4), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->titems, ti.data(), ti.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->prim_idx_dev, ps.data(), ps.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     if (P > 0)
         hipLaunchKernelGGL(k_pack_prims, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->geo_lin, c->prim_idx_dev,
                            c->prim_idx_dev + P, static_cast<int>(P), c->prims);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host vectors die here
+    c->st_root = use_st ? static_cast<int>(kLocal | static_cast<unsigned>(nw + T.wroot)) : kNoChild;
     c->accel_ok = true;
     return RT_OK;
 }
@@ -2086,7 +2200,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
         const size_t lds =
             k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6 : 0;
-        const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, kp.N, c->accel.origin_lim,
+        // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
+        const int troot = (c->tree_mode == RT_TREE_SCENE && c->anim_ids.empty()) ? c->st_root : kNoChild;
+        const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
+                          c->scene_stack > 0 ? c->scene_stack : kMaxStack, kp.N, c->accel.origin_lim,
                           c->boxes_finite};
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
         if (k2.tile_cost) {
@@ -2375,6 +2492,7 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     HIP_TRY(hipGetLastError());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
     c->nodes_on_device_newer = true;
+    c->st_root = kNoChild;  // the scene tree's bounds are not refit: stale until the next build
     if (!rebuild) return RT_OK;
     ++c->anim_rebuilds;
     return upload_accel(c);  // a bound changed kind: rebuild from the grown nodes
@@ -2540,6 +2658,17 @@ extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
     out->always_prims = c->accel.always_prims;
     out->max_stack = c->accel.max_stack;
     out->last_kernel = c->last_kind;
+    out->scene_tree = c->accel_ok && c->st_root != kNoChild ? 1 : 0;
+    out->scene_nodes = static_cast<int>(c->accel.st.wchild.size() / rta::kWide);
+    out->scene_items = static_cast<int>(c->accel.st.item_ref.size());
+    out->scene_height = c->accel.st.height;
+    out->tree_nested = c->accel.st.nested;
+    return RT_OK;
+}
+
+extern "C" int rt_set_tree(rt_ctx* c, int mode) {
+    if (!c || (mode != RT_TREE_REFERENCE && mode != RT_TREE_SCENE)) return RT_ERR_INVALID;
+    c->tree_mode = mode;
     return RT_OK;
 }
 
@@ -2556,6 +2685,14 @@ extern "C" int rt_debug_cone_cull(rt_ctx* c, int on) {
     if (!c) return RT_ERR_INVALID;
     c->cone_cull = on ? 1 : 0;
     return c->have_scene ? upload_accel(c) : RT_OK;
+}
+
+// Diagnostics: cap the stack entries of scene-tree walks (0 = none). Exact at
+// any value: a lane that runs out walks the reference tree (lane_walk).
+extern "C" int rt_debug_scene_stack(rt_ctx* c, int n) {
+    if (!c || n < 0) return RT_ERR_INVALID;
+    c->scene_stack = n;
+    return RT_OK;
 }
 
 // Diagnostics: override the per-lane LDS stack depth of k_accel (0 = computed

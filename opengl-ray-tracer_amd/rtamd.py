@@ -71,6 +71,7 @@ LIGHT_DTYPE = np.dtype({
 SPHERE, PLANE, WALL, TRIANGLE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_LANE, KERNEL_PACKET, KERNEL_ACCEL = 0, 1, 2, 3
 SCHED_ROWS, SCHED_COST = 0, 1
+TREE_REFERENCE, TREE_SCENE = 0, 1
 
 
 class rt_params(C.Structure):
@@ -81,7 +82,8 @@ class rt_params(C.Structure):
 
 class rt_accel_info(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("built", "local_nodes", "local_leaves", "bounded_prims", "always_prims",
-                                       "max_stack", "last_kernel")]
+                                       "max_stack", "last_kernel", "scene_tree", "scene_nodes", "scene_items",
+                                       "scene_height", "tree_nested")]
 
 
 class rt_stats(C.Structure):
@@ -192,6 +194,7 @@ RT_SYMBOLS = {
     "rt_accel_info_get": (_I, [_P, _P]),
     "rt_set_launch": (_I, [_P, _I, _I]),
     "rt_set_walk": (_I, [_P, _I]),
+    "rt_set_tree": (_I, [_P, _I]),
     "rt_set_schedule": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
@@ -489,9 +492,19 @@ class ComputeShader:
     def set_walk(self, lane_from_depth):
         self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
 
+    def set_tree(self, mode):
+        """TREE_SCENE (default): one SAH tree over the reference leaves where exact; TREE_REFERENCE: the reference tree."""
+        self._chk(self._lib.rt_set_tree(self._h, int(mode)), "rt_set_tree")
+
     def set_schedule(self, mode):
         """SCHED_COST (default): tiles start longest-first by their last duration; SCHED_ROWS: row-major."""
         self._chk(self._lib.rt_set_schedule(self._h, int(mode)), "rt_set_schedule")
+
+    def debug_scene_stack(self, n):
+        """Diagnostics: cap the stack a scene-tree walk may use (0 = no cap); exact at any value."""
+        fn = self._lib.rt_debug_scene_stack
+        fn.argtypes = [C.c_void_p, C.c_int]
+        self._chk(fn(self._h, int(n)), "rt_debug_scene_stack")
 
     def debug_lane_stack(self, n):
         fn = self._lib.rt_debug_lane_stack

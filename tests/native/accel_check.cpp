@@ -84,7 +84,9 @@ extern "C" {
 
 // For each ray (o[i], d[i]): the accelerated closest hit (shape index or -1)
 // and the rays' shadow query against lim[i]. Returns -1 if the accelerator
-// cannot be built for this tree.
+// cannot be built for this tree. out_info[8] (in): 1 = rays take the scene
+// tree where the device would; out: [9] scene tree built, [10] rays that took
+// it, [11] the reference boxes nest.
 int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
                 const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
                 int* out_shadow, int* out_info) {
@@ -94,7 +96,14 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
     out_info[1] = A.always_prims;
     out_info[2] = A.bounded_prims;
     out_info[3] = A.max_stack;
-    long long tests = 0;
+    const bool use_tree = out_info[8] != 0;
+    bool boxes_finite = true;
+    for (int k = 0; k < N; ++k)
+        for (float v : {nodes[k].boundsMin.x, nodes[k].boundsMin.y, nodes[k].boundsMin.z, nodes[k].boundsMax.x,
+                        nodes[k].boundsMax.y, nodes[k].boundsMax.z})
+            if (std::isnan(v)) boxes_finite = false;
+    constexpr int kSceneBase = 1 << 29;
+    long long tests = 0, scene_rays = 0;
     for (int r = 0; r < R; ++r) {
         long long nodes_before = 0;
         V ro = mk(o[3 * r], o[3 * r + 1], o[3 * r + 2]), rd = mk(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
@@ -105,7 +114,16 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
             Best b{1e20f, 0x7fffffff, mk(0, 0, 0), -1};
             bool hit_shadow = false;
             std::vector<int> st;
-            if (N > 0) st.push_back(N - 1);
+            // Scene tree (accel.h, SceneTree): taken by the rays the device sends
+            // there (rt_kernels.hip, use_scene) when out_info[8] asks for it.
+            const bool fast = boxes_finite && std::fabs(ro.x) < 3.0e38f && std::fabs(ro.y) < 3.0e38f &&
+                              std::fabs(ro.z) < 3.0e38f && std::fabs(inv.x) < 3.0e38f &&
+                              std::fabs(inv.y) < 3.0e38f && std::fabs(inv.z) < 3.0e38f && inv.x != 0.0f &&
+                              inv.y != 0.0f && inv.z != 0.0f;
+            const bool scene = use_tree && A.st.wroot >= 0 && fast && rc.ix != 0.0f;
+            if (scene) ++scene_rays;
+            if (scene) st.push_back(-(A.st.wroot + 1) - kSceneBase);
+            else if (N > 0) st.push_back(N - 1);
             while (!st.empty() && !(shadow && hit_shadow)) {
                 int code = st.back();
                 st.pop_back();
@@ -126,7 +144,26 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                 };
                 if (std::getenv("ACDBG")) std::printf("pop %d lim %g best %d %g\n", code, l, b.shape, b.d);
                 ++nodes_before;
-                if (code >= 0) {
+                if (code <= -kSceneBase) {
+                    // scene-tree wide node: padded boxes and cones; an item tests its
+                    // reference leaf's exact box before its shapes
+                    const int w = -(code + kSceneBase) - 1;
+                    for (int s2 = 0; s2 < rta::kWide; ++s2) {
+                        const int j = A.st.wchild[rta::kWide * w + s2];
+                        if (j < 0) continue;
+                        const float* k = &A.st_cone[4 * j];
+                        if (!padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
+                        if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                        const int sub = A.st.wsub[rta::kWide * w + s2];
+                        if (sub >= 0) {
+                            st.push_back(-(sub + 1) - kSceneBase);
+                            continue;
+                        }
+                        const int it = A.st.item_of[j];
+                        const FlatNode& rl = nodes[A.st.item_ref[it]];
+                        if (ref_aabb(ro, inv, rl.boundsMin, rl.boundsMax)) scan(A.st.item_start[it], A.st.item_count[it]);
+                    }
+                } else if (code >= 0) {
                     const FlatNode& nd = nodes[code];
                     if (!ref_aabb(ro, inv, nd.boundsMin, nd.boundsMax)) continue;
                     if ((A.flags[code] & 8) && !padded(rc, A.content[code], l)) continue;
@@ -159,6 +196,9 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
         }
     }
     out_info[4] = static_cast<int>(tests / (R > 0 ? R : 1));
+    out_info[9] = A.st.wroot >= 0 ? 1 : 0;
+    out_info[10] = static_cast<int>(scene_rays);
+    out_info[11] = A.st.nested;
     return 0;
 }
 }

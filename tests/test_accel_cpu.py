@@ -41,7 +41,7 @@ def _p(a):
     return C.c_void_p(a.ctypes.data) if a.size else None
 
 
-def compare(lib, fs, o, d, lim):
+def compare(lib, fs, o, d, lim, tree=1):
     fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)  # enforce record layout
     R = len(o)
     o = np.ascontiguousarray(o, np.float32)
@@ -49,7 +49,8 @@ def compare(lib, fs, o, d, lim):
     lim = np.ascontiguousarray(lim, np.float32)
     outs = [np.zeros(R, np.int32), np.zeros(R, np.float32), np.zeros(R, np.int32)]
     refs = [np.zeros(R, np.int32), np.zeros(R, np.float32), np.zeros(R, np.int32)]
-    info = np.zeros(8, np.int32)
+    info = np.zeros(12, np.int32)
+    info[8] = tree
     args = [_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes), _p(fs.indices), len(fs.indices),
             _p(o), _p(d), _p(lim), R]
     assert lib.accel_check(*args, *[_p(x) for x in outs], _p(info)) == 0
@@ -79,8 +80,9 @@ def random_rays(rng, R, box=30.0):
     return o, d
 
 
+@pytest.mark.parametrize("tree", [0, 1])
 @pytest.mark.parametrize("cfg", [1, 2, 3, 5])
-def test_accel_matches_reference_walk(check_lib, cfg):
+def test_accel_matches_reference_walk(check_lib, cfg, tree):
     W, H = 96, 54
     fs = rtamd.generate(cfg, 0, W, H)
     o, d = camera_rays(fs, W, H)
@@ -88,9 +90,13 @@ def test_accel_matches_reference_walk(check_lib, cfg):
     o2, d2 = random_rays(rng, 4000)
     o, d = np.concatenate([o, o2]), np.concatenate([d, d2])
     lim = rng.uniform(1, 80, len(o))
-    info = compare(check_lib, fs, o, d, lim)
+    info = compare(check_lib, fs, o, d, lim, tree)
     if cfg == 3:
         assert info[0] > 100  # local BVHs were built for the giant leaves
+    # the generated scenes come from the reference builder: their boxes nest
+    assert info[11] == 1 and info[9] == 1
+    if tree:
+        assert info[10] > len(o) // 2  # most rays took the scene tree
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
@@ -104,6 +110,7 @@ def test_accel_matches_on_soup(check_lib, seed):
     lim = rng.uniform(1, 80, len(o))
     info = compare(check_lib, fs, o, d, lim)
     assert info[1] > 0  # unbounded shapes present
+    assert info[9] == 1 and info[10] > len(o) // 2  # ... and under the scene tree's infinite boxes
 
 
 def test_accel_ties(check_lib):
@@ -276,3 +283,52 @@ def test_accel_stale_triangle_planes(check_lib, seed):
     o, d = np.concatenate([o, o1, ot]), np.concatenate([d, d1, dt])
     lim = rng.uniform(1, 200, len(o))
     compare(check_lib, fs, o, d, lim)
+
+
+def test_scene_tree_grazing_rays(check_lib):
+    """Rays aimed exactly at corners and edge midpoints of reference leaf boxes
+    (the exact-test decisions the scene tree relies on the nesting for), with
+    one-ulp nudges of the direction: same hits and shadows as the reference walk."""
+    fs = rtamd.generate(5, 0, 64, 36)
+    nodes = fs.nodes
+    leaves = np.where(nodes["leftChild"] == -1)[0]
+    rng = np.random.default_rng(11)
+    pick = rng.choice(leaves, 300, replace=False)
+    o, d = [], []
+    for k in pick:
+        lo = np.array(nodes["boundsMin"][k], np.float32)
+        hi = np.array(nodes["boundsMax"][k], np.float32)
+        targets = [np.where(np.array([(c >> a) & 1 for a in range(3)], bool), hi, lo) for c in range(8)]
+        targets += [0.5 * (lo + hi)]
+        for t in targets:
+            src = rng.uniform(-60, 60, 3).astype(np.float32)
+            v = (t - src).astype(np.float32)
+            v /= np.float32(np.linalg.norm(v))
+            for nudge in (0, 1, -1):
+                w = v.copy()
+                ax = rng.integers(3)
+                w[ax] = np.nextafter(w[ax], np.float32(np.inf) if nudge > 0 else np.float32(-np.inf)) if nudge else w[ax]
+                o.append(src)
+                d.append(w)
+    o, d = np.array(o, np.float32), np.array(d, np.float32)
+    lim = rng.uniform(1, 120, len(o))
+    info = compare(check_lib, fs, o, d, lim, 1)
+    assert info[9] == 1 and info[10] > len(o) // 2
+
+
+def test_scene_tree_off_when_boxes_do_not_nest(check_lib):
+    """A child box reaching outside its parent's box breaks the equivalence:
+    no scene tree, and the reference walk's results still hold."""
+    fs = rtamd.generate(2, 0, 64, 48)
+    nodes = fs.nodes.copy()
+    root = len(nodes) - 1
+    ch = nodes["leftChild"][root]
+    assert ch >= 0
+    nodes["boundsMax"][ch, 0] = nodes["boundsMax"][root, 0] + np.float32(0.25)
+    fs2 = rtamd.FlatScene(fs.shapes, nodes, fs.indices, fs.camera, fs.light)
+    o, d = camera_rays(fs2, 64, 48)
+    rng = np.random.default_rng(3)
+    o2, d2 = random_rays(rng, 3000)
+    o, d = np.concatenate([o, o2]), np.concatenate([d, d2])
+    info = compare(check_lib, fs2, o, d, rng.uniform(1, 80, len(o)), 1)
+    assert info[11] == 0 and info[9] == 0 and info[10] == 0

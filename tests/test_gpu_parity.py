@@ -308,6 +308,7 @@ def test_accel_exact_on_adversarial_soup(ctx, seed, fresnel):
     img = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
     info = ctx.accel_info()
     assert info["built"] and info["last_kernel"] == rtamd.KERNEL_ACCEL and info["always_prims"] > 0
+    assert info["scene_tree"] == 1
     check(img, ref, f"soup {seed}")
 
 
@@ -342,6 +343,63 @@ def test_far_camera_falls_back_exactly(ctx):
     img = gpu_rows(ctx, fs2, W, H, p, kernel=rtamd.KERNEL_AUTO)
     assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_PACKET
     check(img, ref, "far camera")
+
+
+@pytest.mark.parametrize("walk", [0, 1, 99])
+@pytest.mark.parametrize("scene", ["c2", "c3", "c5", "soup"])
+def test_scene_tree_equals_reference_tree(ctx, scene, walk):
+    """The scene tree (rt_set_tree, accel.h SceneTree) against the reference
+    tree walk: identical full frames for every walk policy."""
+    if scene == "soup":
+        W, H, mb = 800, 600, 3
+        fs = _soup(1)
+    else:
+        cfg = int(scene[1])
+        W, H = (800, 600) if cfg == 2 else (1920, 1080)
+        mb = CFG_BOUNCES[cfg]
+        fs = rtamd.generate(cfg, 0, W, H)
+    p = oracle.params(W, H, mb)
+    ctx.set_walk(walk)
+    try:
+        ctx.set_tree(rtamd.TREE_REFERENCE)
+        a = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+        ctx.set_tree(rtamd.TREE_SCENE)
+        b = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+    finally:
+        ctx.set_walk(1)
+        ctx.set_tree(rtamd.TREE_SCENE)
+    info = ctx.accel_info()
+    assert info["scene_tree"] == 1 and info["tree_nested"] == 1 and info["last_kernel"] == rtamd.KERNEL_ACCEL
+    bad = int((a != b).any(axis=-1).sum())
+    assert bad == 0, f"{bad} pixels differ between the scene tree and the reference tree"
+
+
+@pytest.mark.parametrize("cap", [1, 3, 6])
+@pytest.mark.parametrize("scene", ["c3", "c5", "soup"])
+def test_scene_tree_stack_overflow_is_exact(ctx, scene, cap):
+    """Scene-tree walks whose stack runs out (capped by rt_debug_scene_stack)
+    finish on the reference tree: still the reference tree's image."""
+    if scene == "soup":
+        W, H, fs = 400, 300, _soup(2)
+    else:
+        W, H = 960, 540
+        fs = rtamd.generate(int(scene[1]), 0, W, H)
+    p = oracle.params(W, H, 3)
+    ctx.set_walk(1)
+    ctx.set_tree(rtamd.TREE_REFERENCE)
+    a = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+    ctx.set_tree(rtamd.TREE_SCENE)
+    try:
+        for walk in (0, 1, 99):
+            ctx.set_walk(walk)
+            ctx.debug_scene_stack(cap)
+            b = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+            assert ctx.accel_info()["scene_tree"] == 1
+            bad = int((a != b).any(axis=-1).sum())
+            assert bad == 0, f"walk {walk} cap {cap}: {bad} pixels differ"
+    finally:
+        ctx.debug_scene_stack(0)
+        ctx.set_walk(1)
 
 
 @pytest.mark.parametrize("walk", [0, 1, 99])

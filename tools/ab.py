@@ -35,6 +35,8 @@ VARIANTS = {
     "lpt_rows": dict(kernel=3, wpb=1, persistent=False, walk=1, order="rows"),
     "stack20": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=20),
     "stack16": dict(kernel=3, wpb=1, persistent=False, walk=1, stack=16),
+    "reftree": dict(kernel=3, wpb=1, persistent=False, walk=1, tree=0),
+    "reftree_lane": dict(kernel=3, wpb=1, persistent=False, walk=0, tree=0),
 }
 
 ap = argparse.ArgumentParser()
@@ -100,6 +102,8 @@ for rnd in range(a.rounds):
             ctx.debug_spec(v.get("spec", 1))
         if hasattr(ctx._lib, "rt_debug_lane_stack"):
             ctx.debug_lane_stack(v.get("stack", 0))
+        if hasattr(ctx._lib, "rt_set_tree"):
+            ctx.set_tree(v.get("tree", 1))
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         ctx.sync()
         img = out.cpu().numpy()
@@ -128,6 +132,8 @@ if a.times:
             ctx.debug_spec(v.get("spec", 1))
         if hasattr(ctx._lib, "rt_debug_lane_stack"):
             ctx.debug_lane_stack(v.get("stack", 0))
+        if hasattr(ctx._lib, "rt_set_tree"):
+            ctx.set_tree(v.get("tree", 1))
         ctx.debug_tile_times(tiles)
         ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         t = ctx.tile_times(tiles).astype(np.int64)
