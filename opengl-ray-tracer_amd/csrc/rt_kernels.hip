@@ -661,7 +661,9 @@ __device__ __forceinline__ bool first_active() {
 }
 
 // Codes of the walk: a reference inner node k; kTopLeaf|k a reference leaf;
-// kLocal|j a local inner node; kLocal|kLeaf|start<<8|count a local leaf.
+// kTopLeaf|kItem|i a scene-tree item; kLocal|j a wide node (local or scene
+// tree); kLocal|kLeaf|start<<6|count a local leaf (start < 2^22, count < 64:
+// bits 28-29 stay clear, so kTopLeaf and kItem are never set in a local code).
 __device__ __forceinline__ int top_code(int k, int ia) { return ia < 0 ? static_cast<int>(kTopLeaf | k) : k; }
 
 __device__ __forceinline__ rta::RayC ray_c(const Ray& r, float origin_lim) {
@@ -883,7 +885,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     have = true;
                 }
                 const unsigned uc = static_cast<unsigned>(cur);
-                if (count > 0 && ((uc & kTopLeaf) || ((uc & kLocal) && (uc & kLeaf)))) break;  // park
+                if (count > 0 && (uc & (kTopLeaf | kLeaf))) break;  // park on a leaf
                 if (COUNT) wc.nodes++;
                 if (WSTAT && first_active()) wc.wnodes++;
                 have = false;
@@ -902,8 +904,8 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                         have = true;
                     }
                 } else if (uc & kLeaf) {
-                    start = static_cast<int>((uc >> 8) & 0x3fffffu);
-                    count = static_cast<int>(uc & 0xffu);
+                    start = static_cast<int>((uc >> 6) & 0x3fffffu);
+                    count = static_cast<int>(uc & 0x3fu);
                 } else if (uc & kLocal) {
                     Kids4 w = wide_kids(A, uc, c, tl, true);
                     sort4(w);
@@ -1027,8 +1029,8 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
             k.ca = uni(lf.z);
             k.ha = (k.ca != kNoChild) && lane_in(m);  // local root: entered with the leaf
         } else if (uc & kLeaf) {
-            start = static_cast<int>((uc >> 8) & 0x3fffffu);
-            count = static_cast<int>(uc & 0xffu);
+            start = static_cast<int>((uc >> 6) & 0x3fffffu);
+            count = static_cast<int>(uc & 0x3fu);
         } else if (uc & kLocal) {
             // wide node: children ordered by the entry parameters of the first lane
             // that enters any of them; the rest pushed far to near
@@ -1785,8 +1787,8 @@ int build_upload_accel(rt_ctx* c) {
     bool codes_ok = true;
     auto leaf_code = [&](size_t j) -> int {
         const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
-        if (st >= (1u << 22) || cnt > 255u) codes_ok = false;
-        return static_cast<int>(kLocal | kLeaf | (st << 8) | cnt);
+        if (st >= (1u << 22) || cnt > 63u) codes_ok = false;
+        return static_cast<int>(kLocal | kLeaf | (st << 6) | cnt);
     };
     // The scene tree's wide nodes (accel.h, SceneTree) follow the local ones;
     // its leaves are item codes (kTopLeaf | kItem | item).
