@@ -539,6 +539,8 @@ struct AccelPtrs {
     const float4* __restrict__ titems;  // 2 float4 per scene-tree item: exact box of its reference leaf + range
     int troot;                          // scene-tree root code (kLocal|w), kNoChild: reference tree only
     int scene_stack;                    // stack entries a scene-tree walk may use (<= the walk's own cap)
+    int nfew;                           // > 0: items are gated by a per-ray mask over nfew reference leaves
+                                        //      whose exact boxes are titems[0 .. 2*nfew) (few_mask)
     int N;
     float origin_lim;                   // AccelHost::origin_lim
     int boxes_finite;                   // no reference node box holds a NaN (ray_aabb_fast)
@@ -688,6 +690,18 @@ __device__ __forceinline__ bool enter_item(const AccelPtrs& A, unsigned uc, cons
     start = __float_as_int(e0.w);
     count = __float_as_int(e1.w);
     return ray_aabb_fast(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z));
+}
+
+// Few-leaf scenes (<= 8 reference leaves): the exact box tests of all of them
+// once per walk; items are then local-leaf codes with kItem set and the leaf's
+// index in bits 3-5 (no item record load on the walk).
+__device__ __forceinline__ unsigned few_mask(const AccelPtrs& A, const Ray& r, const V& inv) {
+    unsigned fm = 0;
+    for (int i = 0; i < A.nfew; ++i) {
+        const float4 e0 = A.titems[2 * i], e1 = A.titems[2 * i + 1];
+        if (ray_aabb_fast(r.o, inv, mk(e0.x, e0.y, e0.z), mk(e1.x, e1.y, e1.z))) fm |= 1u << i;
+    }
+    return fm;
 }
 
 // A ray walks the scene tree when one is built and its slab values cannot be
@@ -851,9 +865,12 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
     // from the root (with the best hit so far), whose bound the builder checked.
     bool ovf = false;
     int pcap = min(cap, A.scene_stack);  // push bound of the tree being walked
+    unsigned fm = 0;
     if (!use_scene(A, fast, c)) {
         have = enter_root(A, r, inv, c, tl, cur);
         pcap = cap;
+    } else if (A.nfew > 0) {
+        fm = few_mask(A, r, inv);
     }
     bool ended = false;
     for (;;) {
@@ -906,6 +923,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 } else if (uc & kLeaf) {
                     start = static_cast<int>((uc >> 6) & 0x3fffffu);
                     count = static_cast<int>(uc & 0x3fu);
+                    if (uc & kItem) count = ((fm >> (count >> 3)) & 1u) ? (count & 7) : 0;  // few-leaf item
                 } else if (uc & kLocal) {
                     Kids4 w = wide_kids(A, uc, c, tl, true);
                     sort4(w);
@@ -977,12 +995,14 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
     WaveStack st{0, 0, 0, 0};
     int cur = 0;
     unsigned long long ovf = 0;  // lanes whose scene-tree pushes were dropped (see lane_walk)
+    unsigned fm = 0;             // few-leaf mask (few_mask)
     int pcap = kMaxStack;        // push bound of the tree being walked (uniform)
     {
         int code = 0;
         const bool scene = use_scene(A, fast, c);
         const bool hr = enter_root(A, r, inv, c, tl, code);  // code is the same in every lane
         const unsigned long long mr = __ballot(active && !scene && hr), ms = __ballot(active && scene);
+        if (ms && A.nfew > 0) fm = few_mask(A, r, inv);
         cur = uni(code);
         m = mr;
         if (ms) {  // scene-tree lanes first; reference-tree lanes (if any) follow as if overflowed
@@ -1031,6 +1051,10 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
         } else if (uc & kLeaf) {
             start = static_cast<int>((uc >> 6) & 0x3fffffu);
             count = static_cast<int>(uc & 0x3fu);
+            if (uc & kItem) {  // few-leaf item
+                item_in = (fm >> (count >> 3)) & 1u;
+                count &= 7;
+            }
         } else if (uc & kLocal) {
             // wide node: children ordered by the entry parameters of the first lane
             // that enters any of them; the rest pushed far to near
@@ -1604,6 +1628,7 @@ struct rt_ctx {
     int st_root = 0x7fffffff;  // scene-tree root code, kNoChild if none
     int tree_mode = 1;         // rt_set_tree
     int scene_stack = 0;       // rt_debug_scene_stack (0: the walk's own cap)
+    int nfew = 0;              // few-leaf mode (AccelPtrs::nfew)
     int* prim_idx_dev = nullptr;
     bool accel_ok = false;
     int boxes_finite = 0;
@@ -1826,17 +1851,41 @@ int build_upload_accel(rt_ctx* c) {
     for (size_t w = 0; w < nw; ++w)
         emit_wide(w, w, A.wchild, A.wsub, A.lbox, A.lcone, [&](int j) { return leaf_code(static_cast<size_t>(j)); },
                   0);
-    std::vector<float4> ti(2 * (use_st ? T.item_ref.size() : 1));
+    // Items: with <= 8 distinct reference leaves (few-leaf mode, few_mask) a
+    // local-leaf code kLocal|kLeaf|kItem|start<<6|leaf<<3|count and titems =
+    // the leaves' exact boxes; otherwise kTopLeaf|kItem|item and titems = per
+    // item its leaf's exact box + prim range.
+    std::vector<int> few;
     if (use_st) {
-        for (size_t w = 0; w < nws; ++w)
-            emit_wide(w, nw + w, T.wchild, T.wsub, T.box, A.st_cone,
-                      [&](int j) { return static_cast<int>(kTopLeaf | kItem | static_cast<unsigned>(T.item_of[j])); },
-                      nw);
-        for (size_t i = 0; i < T.item_ref.size(); ++i) {
-            const FlatNode& n = c->host_nodes[T.item_ref[i]];
-            ti[2 * i] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(T.item_start[i]));
-            ti[2 * i + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(T.item_count[i]));
-        }
+        for (int k : T.item_ref)
+            if (std::find(few.begin(), few.end(), k) == few.end()) {
+                few.push_back(k);
+                if (few.size() > 8) break;
+            }
+        if (few.size() > 8) few.clear();
+        for (size_t i = 0; i < T.item_ref.size() && !few.empty(); ++i)
+            if (T.item_count[i] > 7 || T.item_start[i] >= (1 << 22)) few.clear();
+    }
+    c->nfew = static_cast<int>(few.size());
+    auto item_code = [&](int j) {
+        const int i = T.item_of[j];
+        if (few.empty()) return static_cast<int>(kTopLeaf | kItem | static_cast<unsigned>(i));
+        const unsigned f = static_cast<unsigned>(std::find(few.begin(), few.end(), T.item_ref[i]) - few.begin());
+        return static_cast<int>(kLocal | kLeaf | kItem | (static_cast<unsigned>(T.item_start[i]) << 6) | (f << 3) |
+                                static_cast<unsigned>(T.item_count[i]));
+    };
+    std::vector<float4> ti(2 * (use_st ? std::max<size_t>(T.item_ref.size(), 1) : 1));
+    if (use_st) {
+        for (size_t w = 0; w < nws; ++w) emit_wide(w, nw + w, T.wchild, T.wsub, T.box, A.st_cone, item_code, nw);
+        auto put = [&](size_t i, int ref, int start, int count) {
+            const FlatNode& n = c->host_nodes[ref];
+            ti[2 * i] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(start));
+            ti[2 * i + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(count));
+        };
+        if (!few.empty())
+            for (size_t i = 0; i < few.size(); ++i) put(i, few[i], 0, 0);
+        else
+            for (size_t i = 0; i < T.item_ref.size(); ++i) put(i, T.item_ref[i], T.item_start[i], T.item_count[i]);
     }
     // wnodes: per reference inner node both children's exact + content boxes;
     // tleaf: per reference leaf its plain range and local root code.
@@ -2205,7 +2254,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
         const int troot = (c->tree_mode == RT_TREE_SCENE && c->anim_ids.empty()) ? c->st_root : kNoChild;
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
-                          c->scene_stack > 0 ? c->scene_stack : kMaxStack, kp.N, c->accel.origin_lim,
+                          c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
                           c->boxes_finite};
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
         if (k2.tile_cost) {
