@@ -587,10 +587,14 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
     }
     if (g.type < 1 || g.type > 3) return;
     V n = mk(f[0], f[1], f[2]);
-    float np = dot(n, r.d);
-    if (np == 0.0f) return;
-    float t = -(f[3] + dot(n, r.o)) / np;
-    if (!(t > 0.0f) || !(np > 0.0f)) return;
+    const float np = dot(n, r.d);
+    // INNER needs np > 0 and t = num / np > 0 (gpu_shader.comp:206-212,276-283):
+    // both signs are known before the division, which only the survivors pay.
+    if (!(np > 0.0f)) return;
+    const float num = -(f[3] + dot(n, r.o));
+    if (!(num > 0.0f)) return;
+    const float t = num / np;
+    if (!(t > 0.0f)) return;
     V p = r.o + t * r.d;
     float d = dist(r.o, p);
     if (!lex_better(d, seq, b)) return;
@@ -627,10 +631,12 @@ __device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float 
     }
     if (g.type < 1 || g.type > 3) return false;
     V n = mk(f[0], f[1], f[2]);
-    float np = dot(n, r.d);
-    if (np == 0.0f) return false;
-    float t = -(f[3] + dot(n, r.o)) / np;
-    if (!(t > 0.0f) || !(np > 0.0f)) return false;
+    const float np = dot(n, r.d);
+    if (!(np > 0.0f)) return false;  // signs first, as in try_closest
+    const float num = -(f[3] + dot(n, r.o));
+    if (!(num > 0.0f)) return false;
+    const float t = num / np;
+    if (!(t > 0.0f)) return false;
     V p = r.o + t * r.d;
     if (!(dist(r.o, p) < lim)) return false;
     if (g.type == 2) {
