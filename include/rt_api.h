@@ -197,6 +197,20 @@ int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1 };
 int rt_set_schedule(struct rt_ctx* ctx, int mode);
 
+/* Opt-in device BVH build (lbvh.hip). Builds a linear
+ * BVH (Karras 2012: Morton codes of the shapes' split() centres, radix sort,
+ * one shape per leaf) on the GPU over the current shapes, in the FlatNode /
+ * bvhIndices layout (root at N-1 = 2S-2, node boxes = the reference's
+ * BoundingBox of their shapes), and adopts it as if the host had passed it to
+ * rt_upload_scene (which also clears the animated set). It replaces the
+ * reference builder's tree (src/main.cpp:1111-1193), so frames are the
+ * reference shader's frames over THIS tree: read it back with rt_scene_size,
+ * rt_read_nodes and rt_read_indices to reproduce them elsewhere.
+ * *device_ms (optional) = device time of the build kernels. */
+int rt_build_lbvh(struct rt_ctx* ctx, float* device_ms);
+int rt_scene_size(struct rt_ctx* ctx, int* num_shapes, int* num_nodes, int* num_indices);
+int rt_read_indices(struct rt_ctx* ctx, int* indices, int num_indices);
+
 /* Which tree the accelerated kernel walks. RT_TREE_SCENE (default): when the
  * reference tree's child boxes nest in their parents' boxes, rays whose slab
  * values cannot be NaN walk one SAH tree over all reference leaves' shapes,

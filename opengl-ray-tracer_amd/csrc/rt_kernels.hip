@@ -34,6 +34,7 @@
 #include "../../include/rt_api.h"
 #include "accel.h"
 #include "accel_math.h"
+#include "lbvh.h"
 #include "rt_device.h"
 
 using namespace rtd;
@@ -2553,6 +2554,53 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (!rebuild) return RT_OK;
     ++c->anim_rebuilds;
     return upload_accel(c);  // a bound changed kind: rebuild from the grown nodes
+}
+
+int rt_build_lbvh(rt_ctx* c, float* device_ms) {
+    if (!c || !c->have_scene) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    const int S = c->S;
+    const int N = S > 0 ? 2 * S - 1 : 0;
+    std::vector<FlatNode> nodes(static_cast<size_t>(N));
+    std::vector<int> idx(static_cast<size_t>(S));
+    float ms = 0.f;
+    if (S > 0) {
+        FlatNode* dn = nullptr;
+        int* di = nullptr;
+        if (hipMalloc(&dn, N * sizeof(FlatNode)) != hipSuccess || hipMalloc(&di, S * sizeof(int)) != hipSuccess) {
+            (void)hipFree(dn);
+            return RT_ERR_NO_MEMORY;
+        }
+        // staging_shapes holds the current records (uploads, updates and rt_animate frames)
+        int rc = rtl::lbvh_build(c->staging_shapes, S, dn, di, c->stream, &ms) == 0 ? RT_OK : RT_ERR_DEVICE;
+        if (rc == RT_OK &&
+            (hipMemcpyAsync(nodes.data(), dn, N * sizeof(FlatNode), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             hipMemcpyAsync(idx.data(), di, S * sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess))
+            rc = RT_ERR_DEVICE;
+        (void)hipFree(dn);
+        (void)hipFree(di);
+        if (rc != RT_OK) return rc;
+    }
+    if (device_ms) *device_ms = ms;
+    // adopt the tree exactly as if the host had uploaded it (validation, leaf
+    // order, accelerator); the animated set is cleared as by any upload
+    const std::vector<FlatShape> shapes(c->host_shapes);
+    return rt_upload_scene(c, shapes.data(), S, nodes.data(), N, idx.data(), S);
+}
+
+int rt_scene_size(rt_ctx* c, int* num_shapes, int* num_nodes, int* num_indices) {
+    if (!c || !c->have_scene) return RT_ERR_INVALID;
+    if (num_shapes) *num_shapes = c->S;
+    if (num_nodes) *num_nodes = c->N;
+    if (num_indices) *num_indices = c->I;
+    return RT_OK;
+}
+
+int rt_read_indices(rt_ctx* c, int* indices, int num_indices) {
+    if (!c || !c->have_scene || num_indices != c->I || (num_indices > 0 && !indices)) return RT_ERR_INVALID;
+    std::copy(c->host_idx.begin(), c->host_idx.end(), indices);
+    return RT_OK;
 }
 
 int rt_read_nodes(rt_ctx* c, FlatNode* nodes, int N) {

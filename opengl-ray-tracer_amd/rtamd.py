@@ -195,6 +195,9 @@ RT_SYMBOLS = {
     "rt_set_launch": (_I, [_P, _I, _I]),
     "rt_set_walk": (_I, [_P, _I]),
     "rt_set_tree": (_I, [_P, _I]),
+    "rt_build_lbvh": (_I, [_P, _P]),
+    "rt_scene_size": (_I, [_P, _P, _P, _P]),
+    "rt_read_indices": (_I, [_P, _P, _I]),
     "rt_set_schedule": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
@@ -491,6 +494,27 @@ class ComputeShader:
 
     def set_walk(self, lane_from_depth):
         self._chk(self._lib.rt_set_walk(self._h, int(lane_from_depth)), "rt_set_walk")
+
+    def build_lbvh(self):
+        """Device LBVH over the current shapes (rt_build_lbvh); returns the build's device ms."""
+        ms = C.c_float()
+        self._chk(self._lib.rt_build_lbvh(self._h, C.byref(ms)), "rt_build_lbvh")
+        return ms.value
+
+    def scene_size(self):
+        s, n, i = C.c_int(), C.c_int(), C.c_int()
+        self._chk(self._lib.rt_scene_size(self._h, C.byref(s), C.byref(n), C.byref(i)), "rt_scene_size")
+        return s.value, n.value, i.value
+
+    def read_tree(self):
+        """(nodes, indices) of the current scene tree as FlatNode records and int32."""
+        _, n, i = self.scene_size()
+        nodes = np.zeros(n, NODE_DTYPE)
+        idx = np.zeros(i, np.int32)
+        if n:
+            self._chk(self._lib.rt_read_nodes(self._h, _ptr(nodes), n), "rt_read_nodes")
+        self._chk(self._lib.rt_read_indices(self._h, _ptr(idx) if i else None, i), "rt_read_indices")
+        return nodes, idx
 
     def set_tree(self, mode):
         """TREE_SCENE (default): one SAH tree over the reference leaves where exact; TREE_REFERENCE: the reference tree."""
