@@ -29,6 +29,9 @@ VARIANTS = {
     "nocone": dict(kernel=3, wpb=1, persistent=False, walk=1, cone=0),
     "packet": dict(kernel=2, wpb=4, persistent=False, walk=1),
     "lpt": dict(kernel=3, wpb=1, persistent=False, walk=1, order="lpt"),
+    "mix1": dict(kernel=3, wpb=1, persistent=False, walk=1, order="mix1"),
+    "mix3": dict(kernel=3, wpb=1, persistent=False, walk=1, order="mix3"),
+    "mix7": dict(kernel=3, wpb=1, persistent=False, walk=1, order="mix7"),
     "rows": dict(kernel=3, wpb=1, persistent=False, walk=1, sched=0),
     "spec_on": dict(kernel=3, wpb=1, persistent=False, walk=1, spec=1),
     "spec_off": dict(kernel=3, wpb=1, persistent=False, walk=1, spec=0),
@@ -75,6 +78,18 @@ if any(VARIANTS[n.partition("@")[0]].get("order") for n in names):
     cx.debug_tile_times(0)
     d = tt[:, 1] - tt[:, 0]
     orders["lpt"] = np.argsort(-d, kind="stable").astype(np.int32)
+    # heaviest tiles interleaved with the lightest, k light per heavy, so that a
+    # heavy wave shares its SIMD with short ones rather than with other heavy ones
+    for k in (1, 3, 7):
+        desc = orders["lpt"]
+        nh = len(desc) // (k + 1)
+        heavy, light = desc[:nh], desc[nh:][::-1]
+        mix = []
+        for q in range(nh):
+            mix.append(heavy[q])
+            mix.extend(light[q * k:(q + 1) * k])
+        mix.extend(light[nh * k:])
+        orders[f"mix{k}"] = np.array(mix, np.int32)
     rowcost = d.reshape((H + 7) // 8, -1).sum(axis=1)
     orders["rows"] = np.concatenate([np.arange(r * ((W + 7) // 8), (r + 1) * ((W + 7) // 8))
                                      for r in np.argsort(-rowcost, kind="stable")]).astype(np.int32)
