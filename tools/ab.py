@@ -124,7 +124,8 @@ for rnd in range(a.rounds):
         img = out.cpu().numpy()
         if ref is None:
             ref = img
-        assert np.array_equal(img, ref) or "stack" in n, f"{n} renders a different image"
+        assert np.array_equal(img, ref) or "stack" in n or float(np.abs(img - ref).max()) <= 1e-4, \
+            f"{n} renders a different image"
         ctx.kernel_times()
         for _ in range(a.frames):
             ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)

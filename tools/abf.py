@@ -1,0 +1,82 @@
+"""A/B of two librtamd.so builds in the bench's regime: sustained ms per frame
+with F frames in flight (F contexts, streams and surfaces). Each build runs in
+its own child process (a second build loaded into one process does not overlap
+its frames), alternating A, B, A, B ...; the image of every run is compared.
+
+    python tools/abf.py --lib2 build_ab/REV/librtamd.so [--config 3] [--inflight 2] [--rounds 3] [--frames 200]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
+import rtamd  # noqa: E402
+
+WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 1920, 1080, 3)}
+ap = argparse.ArgumentParser()
+ap.add_argument("--lib2", required=True)
+ap.add_argument("--config", type=int, default=3)
+ap.add_argument("--inflight", type=int, default=2)
+ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--frames", type=int, default=200)
+ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
+a = ap.parse_args()
+
+if a.child is None:
+    import subprocess
+    res = {"current": [], "lib2": []}
+    ref = None
+    for _ in range(a.rounds):
+        for name in ("current", "lib2"):
+            out = subprocess.run([sys.executable, __file__, "--lib2", a.lib2, "--config", str(a.config),
+                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--child", name],
+                                 capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
+            r = json.loads(out)
+            res[name].append(r["ms"])
+            img = np.load(r["img"])
+            ref = img if ref is None else ref
+            diff = float(np.abs(img - ref).max())
+            assert diff <= 1e-4, f"{name} renders an image {diff} away"
+    print(json.dumps({"config": a.config, "inflight": a.inflight,
+                      "ms_per_frame": {n: {"median": float(np.median(v)), "min": float(np.min(v))}
+                                       for n, v in res.items()}}))
+    sys.exit(0)
+
+cfg, W, H, mb = WL[a.config]
+fs = rtamd.generate(cfg, 0, W, H)
+F = a.inflight
+path = None if a.child == "current" else a.lib2
+ctxs, bufs = [], []
+for _ in range(F):
+    s = torch.cuda.Stream()
+    c = rtamd.ComputeShader(0, lib_path=path)
+    c.set_stream(s.cuda_stream)
+    c.upload(fs)
+    c.set_params(W, H, mb, True)
+    ctxs.append((c, s))
+    bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
+
+
+def run(n):
+    for i in range(n):
+        c, _ = ctxs[i % F]
+        c.set_camera(fs.camera)
+        c.set_light(fs.light)
+        c.dispatch_rows(W, H, 0, 1, 1, H, bufs[i % F].data_ptr(), W * 16)
+
+
+run(4 * F)
+torch.cuda.synchronize()
+t0 = time.perf_counter()
+run(a.frames)
+torch.cuda.synchronize()
+ms = (time.perf_counter() - t0) / a.frames * 1e3
+imgpath = f"/tmp/abf_{a.child}_{os.getpid()}.npy"
+np.save(imgpath, bufs[0].cpu().numpy())
+print(json.dumps({"ms": ms, "img": imgpath}))
