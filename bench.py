@@ -106,6 +106,38 @@ def cpu_baseline(fs, W, H, mb, seconds, threads):
             "cpu": platform.processor() or platform.machine()}
 
 
+def cpu_reference_1core(seconds):
+    """BASELINE.md "CPU-ref": the reference's own CPU path, cpuRayTracer
+    (src/main.cpp:848-894: brute force over every shape, primary rays only, CPU
+    phong) restated in oracle/rt_oracle.c, on ONE core as the reference runs it.
+    Config 1 (800x600, 4 spheres + 1 plane) whole frames, and the car scene's
+    1920x1080 primary rays on a band of rows (the whole frame would take minutes)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (cpu_baseline leg only)
+    fs1 = rtamd.generate(1, 0, 800, 600)
+    oracle.cpu_raytracer(fs1, 800, 600, threads=1)  # warm-up
+    n1, t0 = 0, time.perf_counter()
+    while n1 < 3 or time.perf_counter() - t0 < 1.0:
+        oracle.cpu_raytracer(fs1, 800, 600, threads=1)
+        n1 += 1
+    ms1 = (time.perf_counter() - t0) / n1 * 1e3
+    fs3 = rtamd.generate(3, 0, 1920, 1080)
+    rows, y0 = 2, 539
+    while True:
+        t0 = time.perf_counter()
+        oracle.cpu_raytracer(fs3, 1920, 1080, y0=y0, y1=y0 + rows, threads=1)
+        dt = time.perf_counter() - t0
+        if dt >= seconds * 0.5 or rows >= 64:
+            break
+        rows = min(64, max(rows * 2, int(rows * seconds / max(dt, 1e-3) * 0.9)))
+    return {"kind": "port", "path": "cpuRayTracer (src/main.cpp:848-894)", "cores": 1,
+            "config1_ms_per_frame": ms1, "config1_mrays_primary_per_s": 800 * 600 / ms1 / 1e3,
+            "config3_primary_only_mrays_per_s": rows * 1920 / dt / 1e6,
+            "config3_primary_only_ms_per_frame_equiv": dt * 1e3 * 1080 / rows,
+            "sample": f"cpuRayTracer restated (oracle/rt_oracle.c orc_cpu_raytracer), 1 thread: config 1 {n1} "
+                      f"whole 800x600 frames; config 3 rows [{y0},{y0 + rows}) of 1920x1080 in {dt:.2f} s"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -267,6 +299,7 @@ def main():
         if world == 1 and not a.no_cpu:
             thr = a.cpu_threads or min(16, os.cpu_count() or 1)
             out["cpu_baseline"] = cpu_baseline(fs, W, H, mb, a.cpu_seconds, thr)
+            out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(a.cpu_seconds / 2)
         print(json.dumps(out), flush=True)
     for c_ in ctxs:
         c_.close()

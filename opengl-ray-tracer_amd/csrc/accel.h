@@ -109,6 +109,9 @@ constexpr float kNoPrune = -8.0f;
 // Stack entries the lane walk keeps per lane in LDS (6 B each: code + bf16
 // entry parameter): 26 x 64 lanes x 6 B fits 16 waves per CU in 160 KB. The
 // wide collapse stays within it wherever the binary tree allows.
-constexpr int kLaneStack = 26;
+#ifndef RT_LANE_STACK
+#define RT_LANE_STACK 26
+#endif
+constexpr int kLaneStack = RT_LANE_STACK;
 
 }  // namespace rta

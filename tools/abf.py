@@ -25,6 +25,10 @@ ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--inflight", type=int, default=2)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--frames", type=int, default=200)
+ap.add_argument("--walk2", type=int, default=-1, help="walk policy (rt_set_walk) for the lib2 runs")
+ap.add_argument("--set2", default="", help="lib2 settings, e.g. schedule=0,launch=2,walk=0")
+ap.add_argument("--nocheck", action="store_true", help="timing only: images may differ (experiments)")
+ap.add_argument("--bounces", type=int, default=0, help="override maxBounces")
 ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
 a = ap.parse_args()
 
@@ -35,20 +39,21 @@ if a.child is None:
     for _ in range(a.rounds):
         for name in ("current", "lib2"):
             out = subprocess.run([sys.executable, __file__, "--lib2", a.lib2, "--config", str(a.config),
-                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--child", name],
+                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--bounces", str(a.bounces), "--walk2", str(a.walk2), "--set2", a.set2, "--child", name],
                                  capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
             r = json.loads(out)
             res[name].append(r["ms"])
             img = np.load(r["img"])
             ref = img if ref is None else ref
             diff = float(np.abs(img - ref).max())
-            assert diff <= 1e-4, f"{name} renders an image {diff} away"
+            assert a.nocheck or diff <= 1e-4, f"{name} renders an image {diff} away"
     print(json.dumps({"config": a.config, "inflight": a.inflight,
                       "ms_per_frame": {n: {"median": float(np.median(v)), "min": float(np.min(v))}
                                        for n, v in res.items()}}))
     sys.exit(0)
 
 cfg, W, H, mb = WL[a.config]
+mb = a.bounces or mb
 fs = rtamd.generate(cfg, 0, W, H)
 F = a.inflight
 path = None if a.child == "current" else a.lib2
@@ -59,6 +64,13 @@ for _ in range(F):
     c.set_stream(s.cuda_stream)
     c.upload(fs)
     c.set_params(W, H, mb, True)
+    if a.child == "lib2" and a.walk2 >= 0:
+        c.set_walk(a.walk2)
+    if a.child == "lib2" and a.set2:
+        for kv in a.set2.split(","):
+            k, v = kv.split("=")
+            {"schedule": lambda x: c.set_schedule(x), "launch": lambda x: c.set_launch(x, False),
+             "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x)}[k](int(v))
     ctxs.append((c, s))
     bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
 
