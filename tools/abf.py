@@ -45,7 +45,7 @@ if a.child is None:
             res[name].append(r["ms"])
             img = np.load(r["img"])
             ref = img if ref is None else ref
-            diff = float(np.abs(img - ref).max())
+            diff = float(np.abs(img - ref).max())  # NaN if a pixel was not written
             assert a.nocheck or diff <= 1e-4, f"{name} renders an image {diff} away"
     print(json.dumps({"config": a.config, "inflight": a.inflight,
                       "ms_per_frame": {n: {"median": float(np.median(v)), "min": float(np.min(v))}
@@ -70,6 +70,7 @@ for _ in range(F):
         for kv in a.set2.split(","):
             k, v = kv.split("=")
             {"schedule": lambda x: c.set_schedule(x), "launch": lambda x: c.set_launch(x, False),
+             "persistent": lambda x: c.set_launch(1, bool(x)),
              "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x)}[k](int(v))
     ctxs.append((c, s))
     bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
@@ -89,6 +90,11 @@ t0 = time.perf_counter()
 run(a.frames)
 torch.cuda.synchronize()
 ms = (time.perf_counter() - t0) / a.frames * 1e3
+# the compared image: one more frame into a poisoned surface (no pixel may be left over)
+bufs[0].fill_(float("nan"))
+torch.cuda.synchronize()
+run(1)
+torch.cuda.synchronize()
 imgpath = f"/tmp/abf_{a.child}_{os.getpid()}.npy"
 np.save(imgpath, bufs[0].cpu().numpy())
 print(json.dumps({"ms": ms, "img": imgpath}))
