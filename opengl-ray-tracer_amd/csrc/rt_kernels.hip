@@ -1665,6 +1665,9 @@ struct rt_ctx {
     unsigned* sched_sets = nullptr;      // 2 sets of per-group bucket histograms, alternating by frame
     int sched_parity = 0;
     int sched_cap = 0, sched_valid = 0;  // buffer capacity; tile count the order is for (0: none)
+    // The order is re-derived on every sched_period-th dispatch (and whenever the tile
+    // count changes); the dispatches between reuse it and record no work counts.
+    int sched_period = 8, sched_frame = 0;
     int lane_stack_override = 0;  // diagnostics only (rt_debug_lane_stack): breaks exactness if too small
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
@@ -2251,8 +2254,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 c->sched_cap = k2.tiles;
             }
             k2.sched_hist = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
-            if (c->sched_valid == k2.tiles) k2.tile_order = c->sched_order;
-            k2.tile_cost = c->sched_cost;
+            const bool have = c->sched_valid == k2.tiles;
+            if (have) k2.tile_order = c->sched_order;
+            if (!have || c->sched_frame % c->sched_period == 0) {
+                k2.tile_cost = c->sched_cost;
+                c->sched_frame = 0;
+            }
+            ++c->sched_frame;
         }
         k2.lane_from_depth = c->lane_from_depth;
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
@@ -2802,6 +2810,14 @@ extern "C" int rt_debug_scene_stack(rt_ctx* c, int n) {
 
 // Diagnostics: override the per-lane LDS stack depth of k_accel (0 = computed
 // bound). A value below the bound can drop stack entries: timing studies only.
+// Diagnostics: re-derive the cost order every `period` dispatches (1: every one).
+extern "C" int rt_debug_sched_period(rt_ctx* c, int period) {
+    if (!c || period < 1) return RT_ERR_INVALID;
+    c->sched_period = period;
+    c->sched_frame = 0;
+    return RT_OK;
+}
+
 extern "C" int rt_debug_lane_stack(rt_ctx* c, int n) {
     if (!c || n < 0 || n > kMaxStack) return RT_ERR_INVALID;
     c->lane_stack_override = n;

@@ -530,6 +530,11 @@ class ComputeShader:
         fn.argtypes = [C.c_void_p, C.c_int]
         self._chk(fn(self._h, int(n)), "rt_debug_scene_stack")
 
+    def debug_sched_period(self, period):
+        fn = self._lib.rt_debug_sched_period
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(period)), "rt_debug_sched_period")
+
     def debug_lane_stack(self, n):
         fn = self._lib.rt_debug_lane_stack
         fn.argtypes = [_P, _I]
