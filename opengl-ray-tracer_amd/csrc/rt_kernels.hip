@@ -1197,9 +1197,9 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
     }
 }
 
-// Walk counts (node steps, tests) are always kept: they are the cost that
-// orders the next dispatch (rt_set_schedule). COUNT adds the per-walk records.
-template <bool COUNT, bool SPEC>
+// Walk counts (node steps, tests) are kept when COST: they are the cost that
+// orders a later dispatch (rt_set_schedule). COUNT adds the per-walk records.
+template <bool COUNT, bool SPEC, bool COST = true>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
     // Pixel coordinates and the background are recomputed where needed rather than
@@ -1220,9 +1220,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         WalkCount w0 = wc;
         unsigned long long c0 = COUNT ? clock64() : 0;
         if (lane_mode)
-            lane_walk<false, true, COUNT, SPEC>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
+            lane_walk<false, COST || COUNT, COUNT, SPEC>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
         else
-            packet_walk<false, true, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+            packet_walk<false, COST || COUNT, COUNT>(A, ray, alive, 0.f, best, unused, wc);
         if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
         if (alive && best.slot < 0) {
             acc = acc + mulv(att, background(kp, tile_pixel(kp, tile).y));
@@ -1242,9 +1242,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         w0 = wc;
         c0 = COUNT ? clock64() : 0;
         if (lane_mode)
-            lane_walk<true, true, COUNT, SPEC>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
+            lane_walk<true, COST || COUNT, COUNT, SPEC>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
         else
-            packet_walk<true, true, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+            packet_walk<true, COST || COUNT, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
         if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
         if (alive) {
             const GeoRec g = load_rec(A.prims, best.slot);
@@ -1264,7 +1264,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 #ifndef RT_ACCEL_ATTR
 #define RT_ACCEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
-template <bool PERSISTENT, bool TIMED, bool SPEC>
+// COST = false: a dispatch that records no tile work (rt_set_schedule reuses the
+// last order), without the walk counters' registers (12 -> 3 spilled VGPRs).
+template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true>
 __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
     // per-lane stacks, entry j of lane i at [j * blockDim.x + i]: codes, then bf16 entry parameters
@@ -1284,7 +1286,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         if (kp.tile_order) tile = kp.tile_order[tile];  // dispatch order -> image tile (a permutation)
         WalkCount wc{0u, 0u, 0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
-        accel_tile<TIMED, SPEC>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
+        accel_tile<TIMED, SPEC, COST>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1307,7 +1309,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 o[5] = mt;
             }
         }
-        if (kp.tile_cost) {
+        if (COST && kp.tile_cost) {
             const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
             const unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
             if (lane == 0) {
@@ -2268,6 +2270,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6 : 0;
         // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
         const int troot = (c->tree_mode == RT_TREE_SCENE && c->anim_ids.empty()) ? c->st_root : kNoChild;
+        // production shape on a dispatch that records no tile work: the counter-free kernel
+        if (kfn == k_accel<false, false, true> && !k2.tile_cost) kfn = k_accel<false, false, true, false>;
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
                           c->boxes_finite};
