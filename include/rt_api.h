@@ -197,6 +197,17 @@ int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1 };
 int rt_set_schedule(struct rt_ctx* ctx, int mode);
 
+/* Ray compaction in the accelerated kernel: the rays still alive after bounce
+ * from_bounce - 1 are queued per 64x64-pixel region, and a second kernel runs
+ * their remaining bounces 64 rays to a wave instead of in their half-empty tile
+ * waves. 0 = off; RT_TAIL_AUTO (default) = from bounce 2 on scenes whose scene
+ * tree has at least 8,192 items (the 100k-triangle config: -5 %), off otherwise
+ * (the car: the extra kernel costs more than it saves). Same image for every
+ * value (the bounces' arithmetic is the same; a ray's walk does not depend on
+ * its wave's other rays). */
+enum { RT_TAIL_AUTO = -1 };
+int rt_set_tail(struct rt_ctx* ctx, int from_bounce);
+
 /* Opt-in device BVH build (lbvh.hip). Builds a linear
  * BVH (Karras 2012: Morton codes of the shapes' split() centres, radix sort,
  * one shape per leaf) on the GPU over the current shapes, in the FlatNode /

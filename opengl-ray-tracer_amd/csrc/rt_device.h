@@ -92,6 +92,15 @@ struct KParams {
     unsigned* __restrict__ sched_hist;       // with tile_cost: work-bucket histogram copies of this frame
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane
     int lane_stack;                          // per-lane LDS stack entries
+    // compaction (rt_set_tail): k_accel queues the rays alive after bounce tail_from - 1,
+    // k_accel_tail runs their remaining bounces 64 to a wave; tail_queue == nullptr: off
+    float4* __restrict__ tail_queue;         // 4 float4 per ray: o|acc.x, d|acc.y, att|acc.z, row, x
+    int* __restrict__ tail_count;            // per region: rays queued by this dispatch
+    int* __restrict__ tail_count_next;       // the next dispatch's counters (zeroed by k_accel_tail)
+    int tail_from;
+    int tail_rx, tail_regions;               // 64x64-pixel regions: per row, total (one counter each)
+    int tail_counters;                       // counters per set (>= tail_regions; all zeroed for the next)
+    int tail_max_lanes;                      // a wave queues its rays only if at most this many are alive
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).

@@ -1171,6 +1171,10 @@ __device__ __forceinline__ PixelCoord tile_pixel(const KParams& kp, int tile) {
 //   [23] node-step iterations of the wave (all walks).
 constexpr int kTileRec = 24;
 
+// Ray compaction (rt_set_tail): queue entries per 64x64-pixel region.
+constexpr int kTailRegion = 64 * 64;
+constexpr size_t kTailAutoItems = 8192;  // RT_TAIL_AUTO threshold
+
 // Cost-ordered dispatch (rt_set_schedule, k_tile_order): 32 half-octave
 // buckets of a tile's work; the render kernel counts them per group of
 // kOrderThreads tiles (one k_tile_order workgroup each).
@@ -1197,9 +1201,55 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
     }
 }
 
+// One bounce of gpu_shader.comp:450-517 for a wave's rays: closest hit, background
+// on a miss, the shadow ray, then Phong and the mirror ray (shade_bounce).
+// bg_y() gives the lane's image row (recomputed, not kept live through the walks).
+template <bool COUNT, bool SPEC, bool COST, class BgY>
+__device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp,
+                                            int depth, Ray& ray, bool& alive, V& acc, V& att, BgY bg_y, int* stk,
+                                            unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
+    Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
+    bool unused = false;
+    const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
+    WalkCount w0 = wc;
+    unsigned long long c0 = COUNT ? clock64() : 0;
+    if (lane_mode)
+        lane_walk<false, COST || COUNT, COUNT, SPEC>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
+    else
+        packet_walk<false, COST || COUNT, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+    if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
+    if (alive && best.slot < 0) {
+        acc = acc + mulv(att, background(kp, bg_y()));
+        alive = false;
+    }
+    // The shadow ray; the hit's normal and material are fetched again after the
+    // shadow walk rather than kept live through it (register pressure).
+    Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
+    float ld = 0.f;
+    if (alive) {
+        const V hn = shape_normal(load_rec(A.prims, best.slot), best.p);
+        sr = Ray{best.p + hn * 1e-3f, normalize(kp.light_pos - best.p)};
+        ld = dist(kp.light_pos, best.p);
+    }
+    bool shadow = false;
+    Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
+    w0 = wc;
+    c0 = COUNT ? clock64() : 0;
+    if (lane_mode)
+        lane_walk<true, COST || COUNT, COUNT, SPEC>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
+    else
+        packet_walk<true, COST || COUNT, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+    if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
+    if (alive) {
+        const GeoRec g = load_rec(A.prims, best.slot);
+        alive = shade_bounce(kp, ray, best.p, shape_normal(g, best.p), load_mat(mat, g.idx), shadow, acc, att,
+                             1e-3f);
+    }
+}
+
 // Walk counts (node steps, tests) are kept when COST: they are the cost that
 // orders a later dispatch (rt_set_schedule). COUNT adds the per-walk records.
-template <bool COUNT, bool SPEC, bool COST = true>
+template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
     // Pixel coordinates and the background are recomputed where needed rather than
@@ -1212,48 +1262,37 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         alive = pc.active;
     }
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
+    bool deferred = false;  // the lane's remaining bounces run in k_accel_tail
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
-        Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
-        bool unused = false;
-        const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
-        WalkCount w0 = wc;
-        unsigned long long c0 = COUNT ? clock64() : 0;
-        if (lane_mode)
-            lane_walk<false, COST || COUNT, COUNT, SPEC>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
-        else
-            packet_walk<false, COST || COUNT, COUNT>(A, ray, alive, 0.f, best, unused, wc);
-        if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
-        if (alive && best.slot < 0) {
-            acc = acc + mulv(att, background(kp, tile_pixel(kp, tile).y));
-            alive = false;
-        }
-        // The shadow ray; the hit's normal and material are fetched again after the
-        // shadow walk rather than kept live through it (register pressure).
-        Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
-        float ld = 0.f;
-        if (alive) {
-            const V hn = shape_normal(load_rec(A.prims, best.slot), best.p);
-            sr = Ray{best.p + hn * 1e-3f, normalize(kp.light_pos - best.p)};
-            ld = dist(kp.light_pos, best.p);
-        }
-        bool shadow = false;
-        Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
-        w0 = wc;
-        c0 = COUNT ? clock64() : 0;
-        if (lane_mode)
-            lane_walk<true, COST || COUNT, COUNT, SPEC>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
-        else
-            packet_walk<true, COST || COUNT, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
-        if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
-        if (alive) {
-            const GeoRec g = load_rec(A.prims, best.slot);
-            alive = shade_bounce(kp, ray, best.p, shape_normal(g, best.p), load_mat(mat, g.idx), shadow, acc, att,
-                                 1e-3f);
+        bounce_step<COUNT, SPEC, COST>(A, mat, kp, depth, ray, alive, acc, att,
+                                       [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec);
+        if (TAIL && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
+            // Compaction: the rays still alive go to the tail queue (one atomic per wave)
+            // per 64x64-pixel region (8x8 tiles), so a tail wave's rays come from one area
+            const unsigned long long m = __ballot(alive);
+            if (m) {
+                const int rid = (tile / kp.tiles_x / 8) * kp.tail_rx + (tile % kp.tiles_x) / 8;
+                int base = 0;
+                if ((threadIdx.x & 63) == 0) base = rid * kTailRegion + atomicAdd(kp.tail_count + rid, __popcll(m));
+                base = __shfl(base, 0);
+                if (alive) {
+                    const int lane = threadIdx.x & 63;
+                    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                    const PixelCoord pc = tile_pixel(kp, tile);
+                    float4* q = kp.tail_queue + 4 * static_cast<size_t>(pos);
+                    q[0] = make_float4(ray.o.x, ray.o.y, ray.o.z, acc.x);
+                    q[1] = make_float4(ray.d.x, ray.d.y, ray.d.z, acc.y);
+                    q[2] = make_float4(att.x, att.y, att.z, acc.z);
+                    q[3] = make_float4(__int_as_float(pc.r), __int_as_float(pc.x), 0.f, 0.f);
+                }
+            }
+            deferred = alive;
+            break;
         }
     }
     const PixelCoord pc = tile_pixel(kp, tile);
-    if (pc.active) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+    if (pc.active && !deferred) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
 }
 
 // PERSISTENT: each wave pulls tiles from one device counter until none is
@@ -1266,7 +1305,8 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 #endif
 // COST = false: a dispatch that records no tile work (rt_set_schedule reuses the
 // last order), without the walk counters' registers (12 -> 3 spilled VGPRs).
-template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true>
+// TAIL: queue the rays alive after bounce tail_from - 1 for k_accel_tail (rt_set_tail).
+template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true, bool TAIL = false>
 __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
     // per-lane stacks, entry j of lane i at [j * blockDim.x + i]: codes, then bf16 entry parameters
@@ -1286,7 +1326,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         if (kp.tile_order) tile = kp.tile_order[tile];  // dispatch order -> image tile (a permutation)
         WalkCount wc{0u, 0u, 0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
-        accel_tile<TIMED, SPEC, COST>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
+        accel_tile<TIMED, SPEC, COST, TAIL>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1322,6 +1362,79 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         if (lane == 0) t = atomicAdd(kp.tile_counter, 1);
         tile = __shfl(t, 0);
     }
+}
+
+// The queued rays' remaining bounces (rt_set_tail): a resident grid, wave w
+// taking queue chunks w, w + G, ... of 64 rays. The same bounce arithmetic as
+// k_accel; a ray's walk does not depend on the other lanes, so compacting rays
+// from different tiles into one wave leaves every pixel's value unchanged.
+__device__ __forceinline__ int wave_sum_int(int v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+template <bool SPEC>
+__global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A, const float4* __restrict__ mat,
+                                                                      KParams kp) {
+    extern __shared__ int lds_stack[];
+    int* stk = lds_stack + threadIdx.x;
+    unsigned short* stt =
+        reinterpret_cast<unsigned short*>(lds_stack + static_cast<size_t>(kp.lane_stack) * blockDim.x) + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (blockDim.x >> 6);
+    // chunks of 64 queued rays, region after region: total chunk count first
+    int total = 0;
+    for (int b = 0; b < kp.tail_regions; b += 64) {
+        const int cnt = b + lane < kp.tail_regions ? kp.tail_count[b + lane] : 0;
+        total += wave_sum_int((cnt + 63) >> 6);
+    }
+    for (int chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk < total; chunk += waves) {
+        // the region holding chunk: running prefix of the regions' chunk counts
+        int rid = 0, first = 0, n = 0, acc0 = 0;
+        for (int b = 0; b < kp.tail_regions; b += 64) {
+            const int cnt = b + lane < kp.tail_regions ? kp.tail_count[b + lane] : 0;
+            const int ch = (cnt + 63) >> 6;
+            int incl = ch;  // inclusive prefix over the 64 lanes
+            for (int off = 1; off < 64; off <<= 1) {
+                const int y = __shfl_up(incl, off);
+                if (lane >= off) incl += y;
+            }
+            const unsigned long long hit = __ballot(acc0 + incl > chunk && acc0 + incl - ch <= chunk && ch > 0);
+            if (hit) {
+                const int l = __builtin_ctzll(hit);
+                rid = b + l;
+                first = __shfl(acc0 + incl - ch, l);
+                n = __shfl(cnt, l);
+                break;
+            }
+            acc0 += __shfl(incl, 63);
+        }
+        const int k = (chunk - first) * 64 + lane;  // index within the region
+        const int i = rid * kTailRegion + k;
+        bool alive = k < n;
+        Ray ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
+        V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
+        int r = 0, x = 0;
+        if (alive) {
+            const float4* q = kp.tail_queue + 4 * static_cast<size_t>(i);
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            ray = Ray{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z)};
+            acc = mk(q0.w, q1.w, q2.w);
+            att = mk(q2.x, q2.y, q2.z);
+            r = __float_as_int(q3.x);
+            x = __float_as_int(q3.y);
+        }
+        const bool have = alive;
+        WalkCount wc{0u, 0u, 0u, 0u};
+        for (int depth = kp.tail_from; depth < kp.maxBounces; ++depth) {
+            if (__ballot(alive) == 0) break;
+            bounce_step<false, SPEC, false>(A, mat, kp, depth, ray, alive, acc, att,
+                                            [&]() { return image_row(kp, r); }, stk, stt, kp.lane_stack, wc, nullptr);
+        }
+        if (have) store_px(kp, r, x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+    }
+    if (blockIdx.x == 0)
+        for (int b = threadIdx.x; b < kp.tail_counters; b += blockDim.x) kp.tail_count_next[b] = 0;
 }
 
 __global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __restrict__ prim_shape,
@@ -1670,6 +1783,14 @@ struct rt_ctx {
     // The order is re-derived on every sched_period-th dispatch (and whenever the tile
     // count changes); the dispatches between reuse it and record no work counts.
     int sched_period = 8, sched_frame = 0;
+    // compaction (rt_set_tail): bounces >= tail_from run in k_accel_tail (0: off)
+    int tail_from = RT_TAIL_AUTO;
+    float4* tail_queue = nullptr;
+    size_t tail_cap = 0;     // queue entries
+    int* tail_counts = nullptr;  // two sets of per-region counters, alternating by dispatch
+    int tail_regions_cap = 0;
+    int tail_max_lanes = 64;  // rt_debug_tail_lanes
+    int tail_parity = 0;
     int lane_stack_override = 0;  // diagnostics only (rt_debug_lane_stack): breaks exactness if too small
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
@@ -2271,11 +2392,62 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
         const int troot = (c->tree_mode == RT_TREE_SCENE && c->anim_ids.empty()) ? c->st_root : kNoChild;
         // production shape on a dispatch that records no tile work: the counter-free kernel
-        if (kfn == k_accel<false, false, true> && !k2.tile_cost) kfn = k_accel<false, false, true, false>;
+
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
                           c->boxes_finite};
+        // compaction: bounces >= tail_from of the rays still alive run in k_accel_tail
+        k2.tail_queue = nullptr;
+        // RT_TAIL_AUTO: from bounce 2 on scenes of many scene-tree items (measured: config 5's
+        // incoherent bounces -5 %; on the car's 1,302 items the extra kernel costs +18 %)
+        const int tail_from = c->tail_from != RT_TAIL_AUTO
+                                  ? c->tail_from
+                                  : (c->accel.st.item_ref.size() >= kTailAutoItems ? 2 : 0);
+        const bool tail = tail_from > 0 && tail_from < k2.maxBounces && !c->persistent;
+        const int rx = (k2.tiles_x + 7) / 8, regions = rx * ((k2.tiles / k2.tiles_x + 7) / 8);
+        if (tail) {
+            const size_t need = static_cast<size_t>(regions) * kTailRegion;
+            if (need > c->tail_cap) {
+                hipFree(c->tail_queue);
+                c->tail_queue = nullptr;
+                c->tail_cap = 0;
+                if (hipMalloc(&c->tail_queue, need * 4 * sizeof(float4)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                c->tail_cap = need;
+            }
+            if (regions > c->tail_regions_cap) {
+                hipFree(c->tail_counts);
+                c->tail_counts = nullptr;
+                c->tail_regions_cap = 0;
+                if (hipMalloc(&c->tail_counts, 2 * static_cast<size_t>(regions) * sizeof(int)) != hipSuccess)
+                    return RT_ERR_NO_MEMORY;
+                HIP_TRY(hipMemsetAsync(c->tail_counts, 0, 2 * static_cast<size_t>(regions) * sizeof(int), c->stream));
+                c->tail_regions_cap = regions;
+            }
+            k2.tail_queue = c->tail_queue;
+            k2.tail_count = c->tail_counts + c->tail_parity * c->tail_regions_cap;
+            k2.tail_count_next = c->tail_counts + (1 - c->tail_parity) * c->tail_regions_cap;
+            k2.tail_from = tail_from;
+            k2.tail_rx = rx;
+            k2.tail_regions = regions;
+            k2.tail_counters = c->tail_regions_cap;
+            k2.tail_max_lanes = c->tail_max_lanes;
+        }
+        if (kfn == k_accel<false, false, true>) {
+            // production shape: the counter-free kernel on a dispatch that records no tile
+            // work; the queueing kernel when the tail runs (other shapes: no compaction)
+            if (tail) kfn = k2.tile_cost ? k_accel<false, false, true, true, true> : k_accel<false, false, true, false, true>;
+            else if (!k2.tile_cost) kfn = k_accel<false, false, true, false>;
+        } else if (tail) {
+            k2.tail_queue = nullptr;
+        }
+        const bool tail_on = k2.tail_queue != nullptr;
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
+        if (tail_on) {
+            const size_t tlds = static_cast<size_t>(k2.lane_stack) * 64 * 6;
+            hipLaunchKernelGGL(spec ? k_accel_tail<true> : k_accel_tail<false>, dim3(c->cu_count * 16), dim3(64), tlds,
+                               c->stream, A, c->mat, k2);
+            c->tail_parity = 1 - c->tail_parity;
+        }
         if (k2.tile_cost) {
             // the next frame's order; stream-ordered after this dispatch (and after its
             // end event, so rt_kernel_times is the render kernel alone), before the next
@@ -2366,6 +2538,8 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->img);
     hipFree(c->stats_dev);
     hipFree(c->tile_counter);
+    hipFree(c->tail_queue);
+    hipFree(c->tail_counts);
     hipFree(c->tile_times);
     hipFree(c->tile_order);
     hipFree(c->sched_cost);
@@ -2814,6 +2988,19 @@ extern "C" int rt_debug_scene_stack(rt_ctx* c, int n) {
 
 // Diagnostics: override the per-lane LDS stack depth of k_accel (0 = computed
 // bound). A value below the bound can drop stack entries: timing studies only.
+// Diagnostics: only waves with at most `lanes` rays alive hand them to the tail kernel.
+extern "C" int rt_debug_tail_lanes(rt_ctx* c, int lanes) {
+    if (!c || lanes < 0 || lanes > 64) return RT_ERR_INVALID;
+    c->tail_max_lanes = lanes;
+    return RT_OK;
+}
+
+extern "C" int rt_set_tail(rt_ctx* c, int from_bounce) {
+    if (!c || from_bounce < RT_TAIL_AUTO) return RT_ERR_INVALID;
+    c->tail_from = from_bounce;
+    return RT_OK;
+}
+
 // Diagnostics: re-derive the cost order every `period` dispatches (1: every one).
 extern "C" int rt_debug_sched_period(rt_ctx* c, int period) {
     if (!c || period < 1) return RT_ERR_INVALID;

@@ -199,6 +199,7 @@ RT_SYMBOLS = {
     "rt_scene_size": (_I, [_P, _P, _P, _P]),
     "rt_read_indices": (_I, [_P, _P, _I]),
     "rt_set_schedule": (_I, [_P, _I]),
+    "rt_set_tail": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
 
@@ -519,6 +520,15 @@ class ComputeShader:
     def set_tree(self, mode):
         """TREE_SCENE (default): one SAH tree over the reference leaves where exact; TREE_REFERENCE: the reference tree."""
         self._chk(self._lib.rt_set_tree(self._h, int(mode)), "rt_set_tree")
+
+    def set_tail(self, from_bounce):
+        """Bounces >= from_bounce of the rays still alive run compacted in a second kernel; 0 = off."""
+        self._chk(self._lib.rt_set_tail(self._h, int(from_bounce)), "rt_set_tail")
+
+    def debug_tail_lanes(self, lanes):
+        fn = self._lib.rt_debug_tail_lanes
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(lanes)), "rt_debug_tail_lanes")
 
     def set_schedule(self, mode):
         """SCHED_COST (default): tiles start longest-first by their last duration; SCHED_ROWS: row-major."""

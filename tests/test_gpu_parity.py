@@ -599,3 +599,33 @@ def test_device_refit_equals_host_path(ctx):
         ctx.set_animated(np.array([0, 0], np.int32))  # duplicates
     with pytest.raises(rtamd.RTError):
         ctx.set_animated(np.array([len(fs.shapes)], np.int32))
+
+
+@pytest.mark.parametrize("tail", [0, 1, 2, 3])
+def test_ray_compaction_exact(ctx, tail):
+    """rt_set_tail: bounces of the rays still alive run compacted in k_accel_tail;
+    the frame is the uncompacted one bit for bit, across dispatches whose tile
+    (and region) counts change, and the oracle's on a band."""
+    W, H = 960, 540
+    fs = rtamd.generate(3, 0, W, H)
+    p = oracle.params(W, H, 3)
+    ctx.set_tail(0)
+    try:
+        ref = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+        ctx.set_tail(tail)
+        for _ in range(2):
+            img = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+            assert np.array_equal(img, ref), f"tail {tail}: {int((img != ref).any(axis=-1).sum())} pixels differ"
+            band = gpu_rows(ctx, fs, W, H, p, y0=200, rows=40, kernel=rtamd.KERNEL_ACCEL)  # fewer regions
+            assert np.array_equal(band, ref[200:240])
+        o, _ = oracle.render(fs, W, H, p, y0=256, out_rows=16)
+        check(img[256:272], o, f"tail {tail} vs oracle")
+        fs5 = rtamd.generate(5, 0, 640, 360)
+        p5 = oracle.params(640, 360, 3)
+        ctx.set_tail(0)
+        a = gpu_rows(ctx, fs5, 640, 360, p5, kernel=rtamd.KERNEL_ACCEL)
+        ctx.set_tail(tail)
+        b = gpu_rows(ctx, fs5, 640, 360, p5, kernel=rtamd.KERNEL_ACCEL)
+        assert np.array_equal(a, b)
+    finally:
+        ctx.set_tail(-1)
