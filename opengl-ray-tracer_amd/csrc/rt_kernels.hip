@@ -1235,7 +1235,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
     w0 = wc;
     c0 = COUNT ? clock64() : 0;
-    if (lane_mode)
+    if (depth >= kp.shadow_lane_from)
         lane_walk<true, COST || COUNT, COUNT, SPEC>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
     else
         packet_walk<true, COST || COUNT, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
@@ -2386,9 +2386,14 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             ++c->sched_frame;
         }
         k2.lane_from_depth = c->lane_from_depth;
+        // big scenes (the RT_TAIL_AUTO criterion): camera rays' shadow walks per lane too
+        // (measured on config 5: -3.7 %; on the car the packet walk is faster)
+        const bool big = c->accel.st.item_ref.size() >= kTailAutoItems;
+        k2.shadow_lane_from = big && c->lane_from_depth <= 1 ? 0 : c->lane_from_depth;
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
-        const size_t lds =
-            k2.lane_from_depth < k2.maxBounces ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6 : 0;
+        const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces
+                               ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
+                               : 0;
         // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
         const int troot = (c->tree_mode == RT_TREE_SCENE && c->anim_ids.empty()) ? c->st_root : kNoChild;
         // production shape on a dispatch that records no tile work: the counter-free kernel
