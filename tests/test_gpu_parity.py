@@ -629,3 +629,25 @@ def test_ray_compaction_exact(ctx, tail):
         assert np.array_equal(a, b)
     finally:
         ctx.set_tail(-1)
+
+
+def test_alternating_dispatches_stay_exact(ctx):
+    """State carried between dispatches (cost order sets, counter-free dispatches,
+    compaction counters by parity and region count) across changing dispatch
+    shapes, scenes and compaction settings: every frame equals its first render."""
+    shapes = [(640, 360, 0, None), (640, 360, 96, 64), (320, 180, 0, None), (640, 360, 8, 200)]
+    refs = {}
+    for it in range(3):
+        for cfg in (5, 3):
+            fs = rtamd.generate(cfg, 0, 640, 360)
+            for k, (W, H, y0, rows) in enumerate(shapes):
+                for tail in (-1, 2, 0):
+                    ctx.set_tail(tail)
+                    p = oracle.params(W, H, 3)
+                    img = gpu_rows(ctx, fs, W, H, p, y0=y0, rows=rows, kernel=rtamd.KERNEL_ACCEL)
+                    key = (cfg, k)
+                    if key not in refs:
+                        refs[key] = img
+                    bad = int((img != refs[key]).any(axis=-1).sum())
+                    assert bad == 0, f"iteration {it} config {cfg} shape {k} tail {tail}: {bad} pixels differ"
+    ctx.set_tail(-1)
