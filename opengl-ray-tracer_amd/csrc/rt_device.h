@@ -92,6 +92,8 @@ struct KParams {
     unsigned* __restrict__ sched_hist;       // with tile_cost: work-bucket histogram copies of this frame
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane
     int shadow_lane_from;                    // k_accel: shadow walks of bounces >= this walk per lane
+    int root_ok;                             // root_lo/hi hold node N-1's current bounds (k_accel)
+    float root_lo[3], root_hi[3];
     int lane_stack;                          // per-lane LDS stack entries
     // compaction (rt_set_tail): k_accel queues the rays alive after bounce tail_from - 1,
     // k_accel_tail runs their remaining bounces 64 to a wave; tail_queue == nullptr: off

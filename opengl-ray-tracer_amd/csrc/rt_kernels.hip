@@ -1263,6 +1263,18 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     }
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
     bool deferred = false;  // the lane's remaining bounces run in k_accel_tail
+    if (kp.root_ok) {
+        // The root's exact test (gpu_shader.comp:386-395) from the kernel arguments: a camera
+        // ray that misses it hits nothing in any walk (every leaf box lies inside the root's
+        // for the scene tree; the reference walk starts there), so it takes the background
+        // without the walk's dependent loads -- the sky tiles of a frame.
+        const bool in = ray_aabb(ray.o, inv_dir(ray.d), mk(kp.root_lo[0], kp.root_lo[1], kp.root_lo[2]),
+                                 mk(kp.root_hi[0], kp.root_hi[1], kp.root_hi[2]));
+        if (alive && !in) {
+            acc = background(kp, tile_pixel(kp, tile).y);
+            alive = false;
+        }
+    }
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
         bounce_step<COUNT, SPEC, COST>(A, mat, kp, depth, ray, alive, acc, att,
@@ -2386,6 +2398,20 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             ++c->sched_frame;
         }
         k2.lane_from_depth = c->lane_from_depth;
+        // the root's bounds as kernel arguments while the host copy is current (rt_animate
+        // grows boxes on the device)
+        k2.root_ok = 0;
+        if (kp.N > 0 && kp.useBVH && c->anim_ids.empty() && !c->nodes_on_device_newer &&
+            static_cast<int>(c->host_nodes.size()) == kp.N) {
+            const FlatNode& rn = c->host_nodes[kp.N - 1];
+            k2.root_ok = 1;
+            k2.root_lo[0] = rn.boundsMin.x;
+            k2.root_lo[1] = rn.boundsMin.y;
+            k2.root_lo[2] = rn.boundsMin.z;
+            k2.root_hi[0] = rn.boundsMax.x;
+            k2.root_hi[1] = rn.boundsMax.y;
+            k2.root_hi[2] = rn.boundsMax.z;
+        }
         // big scenes (the RT_TAIL_AUTO criterion): camera rays' shadow walks per lane too
         // (measured on config 5: -3.7 %; on the car the packet walk is faster)
         const bool big = c->accel.st.item_ref.size() >= kTailAutoItems;
