@@ -128,23 +128,26 @@ def test_full_frame_packet_equals_lane(ctx, cfg):
     assert (a[..., 3] == 1).all()
 
 
-def test_full_frame_stripes_reassemble(ctx):
+@pytest.mark.parametrize("cfg,kernel", [(3, rtamd.KERNEL_PACKET), (3, rtamd.KERNEL_ACCEL), (5, rtamd.KERNEL_ACCEL)])
+def test_full_frame_stripes_reassemble(ctx, cfg, kernel):
     """Rendering the 4 interleaved stripe sets of a 4-GPU plan and scattering
     them back gives the single-dispatch frame, bit for bit (the multi-GPU path
-    minus the RCCL gather)."""
+    minus the RCCL gather); for the accelerated kernel also with the cost
+    order, the counter-free dispatches and (config 5) ray compaction."""
     import tiling
-    W, H = 1920, 1080
-    fs = rtamd.generate(3, 0, W, H)
+    W, H = (1920, 1080) if cfg == 3 else (960, 544)
+    fs = rtamd.generate(cfg, 0, W, H)
     p = oracle.params(W, H, 3)
-    full = gpu_rows(ctx, fs, W, H, p)
+    full = gpu_rows(ctx, fs, W, H, p, kernel=kernel)
     plan = tiling.StripePlan(H, 4, 8)
     bufs = torch.zeros((4, plan.rows_max, W, 4), dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
-    for r in range(4):
-        ctx.dispatch_rows(W, H, plan.y0(r), 8, 4, plan.rows(r), bufs[r].data_ptr(), W * 16)
-    ctx.sync()
-    img = tiling.unpermute(bufs, plan).cpu().numpy()
-    assert np.array_equal(img, full)
+    for _ in range(3):  # later rounds reuse the cost order of each stripe set's tile count
+        for r in range(4):
+            ctx.dispatch_rows(W, H, plan.y0(r), 8, 4, plan.rows(r), bufs[r].data_ptr(), W * 16)
+        ctx.sync()
+        img = tiling.unpermute(bufs, plan).cpu().numpy()
+        assert np.array_equal(img, full)
 
 
 def test_deterministic_and_band_equals_crop(ctx):
