@@ -1802,6 +1802,7 @@ struct rt_ctx {
     int* tail_counts = nullptr;  // two sets of per-region counters, alternating by dispatch
     int tail_regions_cap = 0;
     int tail_max_lanes = 64;  // rt_debug_tail_lanes
+    int shadow_walk_override = -1;  // rt_debug_shadow_walk (-1: policy)
     int tail_parity = 0;
     int lane_stack_override = 0;  // diagnostics only (rt_debug_lane_stack): breaks exactness if too small
     int* tile_counter = nullptr;
@@ -2415,7 +2416,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         // big scenes (the RT_TAIL_AUTO criterion): camera rays' shadow walks per lane too
         // (measured on config 5: -3.7 %; on the car the packet walk is faster)
         const bool big = c->accel.st.item_ref.size() >= kTailAutoItems;
-        k2.shadow_lane_from = big && c->lane_from_depth <= 1 ? 0 : c->lane_from_depth;
+        k2.shadow_lane_from = c->shadow_walk_override >= 0 ? c->shadow_walk_override
+                              : (big && c->lane_from_depth <= 1 ? 0 : c->lane_from_depth);
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
         const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces
                                ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
@@ -3019,6 +3021,13 @@ extern "C" int rt_debug_scene_stack(rt_ctx* c, int n) {
 
 // Diagnostics: override the per-lane LDS stack depth of k_accel (0 = computed
 // bound). A value below the bound can drop stack entries: timing studies only.
+// Diagnostics: shadow walks of bounces >= from walk per lane (-1: the default policy).
+extern "C" int rt_debug_shadow_walk(rt_ctx* c, int from) {
+    if (!c || from < -1) return RT_ERR_INVALID;
+    c->shadow_walk_override = from;
+    return RT_OK;
+}
+
 // Diagnostics: only waves with at most `lanes` rays alive hand them to the tail kernel.
 extern "C" int rt_debug_tail_lanes(rt_ctx* c, int lanes) {
     if (!c || lanes < 0 || lanes > 64) return RT_ERR_INVALID;

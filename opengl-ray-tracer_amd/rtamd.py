@@ -525,6 +525,11 @@ class ComputeShader:
         """Bounces >= from_bounce of the rays still alive run compacted in a second kernel; 0 = off."""
         self._chk(self._lib.rt_set_tail(self._h, int(from_bounce)), "rt_set_tail")
 
+    def debug_shadow_walk(self, from_bounce):
+        fn = self._lib.rt_debug_shadow_walk
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(from_bounce)), "rt_debug_shadow_walk")
+
     def debug_tail_lanes(self, lanes):
         fn = self._lib.rt_debug_tail_lanes
         fn.argtypes = [_P, _I]
