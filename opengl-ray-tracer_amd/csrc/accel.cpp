@@ -300,6 +300,13 @@ int log2_ceil(int n) {
 // cone and wide-collapse passes apply). A leaf holds atoms of one reference
 // leaf only (n == 1, or all of one leaf with <= 4 shapes). Splits fall back to
 // the median where the SAH choice would let the height exceed `hmax`.
+#ifndef RT_ITEM_MAX
+#define RT_ITEM_MAX 4
+#endif
+// Shapes of one reference leaf kept together in one scene-tree item (at most; <= 7
+// for the few-leaf item codes).
+constexpr int kItemMax = RT_ITEM_MAX;
+
 struct SceneBuilder {
     AccelHost& T;
     std::vector<Atom> atoms;
@@ -346,7 +353,7 @@ struct SceneBuilder {
             same = same && atoms[i].ref == atoms[b].ref;
             tot += atoms[i].n;
         }
-        if (n == 1 || (same && tot <= 4)) return leaf(b, e);
+        if (n == 1 || (same && tot <= kItemMax)) return leaf(b, e);
         Box3 box = empty_box();
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int i = b; i < e; ++i) {
@@ -493,7 +500,7 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
             sb.ap.insert(sb.ap.end(), ps.begin(), ps.end());
             dst.push_back(at);
         };
-        if (bnd.size() <= 4) {
+        if (bnd.size() <= static_cast<size_t>(kItemMax)) {
             if (!bnd.empty()) {
                 Box3 box = empty_box();
                 std::vector<std::pair<int, int>> ps;
