@@ -19,7 +19,8 @@ collective on the data path: the per-GPU work is fixed as N grows, scaling
 fixed, scaling "strong" (the frame then ends with its slowest pixel paths,
 DESIGN.md §7).
 
-Frames in flight (--inflight F, default 2): frame n of a rank renders on
+Frames in flight (--inflight F, default auto: 2 at 1920x1080, up to 4 for frames
+too small to fill the GPU, e.g. 800x600): frame n of a rank renders on
 context n % F, each with its own HIP stream and output surface (double
 buffering), so one frame's tail -- its slowest tiles, when most of the GPU is
 idle -- overlaps the next frame's start. Every step still renders one whole
@@ -75,7 +76,9 @@ def parse():
     ap.add_argument("--variant", type=int, default=0, help="car road: 0 = 2-triangle quad, 1 = 222 strips")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet", "accel"])
     ap.add_argument("--stripe", type=int, default=8)
-    ap.add_argument("--inflight", type=int, default=2, help="frames in flight per GPU (own context, stream, surface)")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="frames in flight per GPU (own context, stream, surface); 0 = auto: 2, or up to 4 "
+                         "while a frame has fewer than 16k 8x8 tiles (too few waves to fill the GPU)")
     ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
                     help="N > 1: weak = one frame per GPU (orbit), strong = one frame split over the GPUs + gather")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
@@ -175,7 +178,8 @@ def main():
     fs = sc.serializeScene()
 
     # strong mode gathers one shared buffer per step: one frame in flight there
-    F = 1 if strong else max(1, a.inflight)
+    tiles = ((W + 7) // 8) * ((H + 7) // 8)
+    F = 1 if strong else (a.inflight if a.inflight > 0 else min(4, max(2, -(-16384 // tiles) + 1)))
     main_stream = torch.cuda.current_stream()
     streams = [main_stream] + [torch.cuda.Stream() for _ in range(F - 1)]
     ctxs = []
