@@ -1174,6 +1174,12 @@ constexpr int kTileRec = 24;
 // Ray compaction (rt_set_tail): queue entries per 64x64-pixel region.
 constexpr int kTailRegion = 64 * 64;
 constexpr size_t kTailAutoItems = 8192;  // RT_TAIL_AUTO threshold
+#ifndef RT_TAIL_ONESHOT
+#define RT_TAIL_ONESHOT 1
+#endif
+// k_accel_tail grid: one wave per possible chunk (64 per region), each taking one, or a
+// resident grid striding over the chunks.
+constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
 
 // Cost-ordered dispatch (rt_set_schedule, k_tile_order): 32 half-octave
 // buckets of a tile's work; the render kernel counts them per group of
@@ -1444,6 +1450,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
                                             [&]() { return image_row(kp, r); }, stk, stt, kp.lane_stack, wc, nullptr);
         }
         if (have) store_px(kp, r, x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+        if (kTailOneShot) break;  // one chunk per wave: no loop-carried state
     }
     if (blockIdx.x == 0)
         for (int b = threadIdx.x; b < kp.tail_counters; b += blockDim.x) kp.tail_count_next[b] = 0;
@@ -2477,7 +2484,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
         if (tail_on) {
             const size_t tlds = static_cast<size_t>(k2.lane_stack) * 64 * 6;
-            hipLaunchKernelGGL(spec ? k_accel_tail<true> : k_accel_tail<false>, dim3(c->cu_count * 16), dim3(64), tlds,
+            const int tgrid = kTailOneShot ? regions * (kTailRegion / 64) : c->cu_count * 16;
+            hipLaunchKernelGGL(spec ? k_accel_tail<true> : k_accel_tail<false>, dim3(tgrid), dim3(64), tlds,
                                c->stream, A, c->mat, k2);
             c->tail_parity = 1 - c->tail_parity;
         }
