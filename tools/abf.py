@@ -71,6 +71,7 @@ for _ in range(F):
             k, v = kv.split("=")
             {"schedule": lambda x: c.set_schedule(x), "launch": lambda x: c.set_launch(x, False),
              "persistent": lambda x: c.set_launch(1, bool(x)), "period": lambda x: c.debug_sched_period(x), "tail": lambda x: c.set_tail(x), "tlanes": lambda x: c.debug_tail_lanes(x), "shwalk": lambda x: c.debug_shadow_walk(x),
+             "spec": lambda x: c.debug_spec(x), "stack": lambda x: c.debug_lane_stack(x),
              "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x)}[k](int(v))
     ctxs.append((c, s))
     bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
