@@ -9,4 +9,4 @@ timeout -k 10 600 python -m pytest tests -m gpu -q -rf > gpurun_out/pytest_gpu.l
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err; rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench_$TAG.json
 [ $rc -eq 0 ] || exit $rc
-bash tools/profile.sh ${TAG}_c3 --steps 20 --warmup 3
+bash tools/profile.sh ${TAG}_c3 --steps 20 --warmup 3 --inflight 1
