@@ -268,7 +268,12 @@ __device__ __forceinline__ GeoRec load_rec(const float4* __restrict__ base, int 
 // Writes the pixel for output row r, column x.
 __device__ __forceinline__ void store_px(const KParams& kp, int r, int x, float4 v) {
     float4* row = reinterpret_cast<float4*>(kp.dst + static_cast<size_t>(r) * kp.pitch);
-    row[x] = v;
+    // streaming store (one global_store_dwordx4 ... nt): the kernel never reads the image
+    // back, so it should not displace the scene records from L2 (config 3 -1.1 %, config 2 -1.7 %)
+    __builtin_nontemporal_store(v.x, &row[x].x);
+    __builtin_nontemporal_store(v.y, &row[x].y);
+    __builtin_nontemporal_store(v.z, &row[x].z);
+    __builtin_nontemporal_store(v.w, &row[x].w);
 }
 
 }  // namespace rtd
