@@ -1,73 +1,73 @@
 #!/usr/bin/env python3
 """bench.py — frames/s and Mrays/s of the MI355X ray tracer (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--kernel auto]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 3] [--mode auto|frames|strong|weak]
 
-A step is one frame of the reference's GPU render loop (src/main.cpp:325-370)
-per GPU: per-frame camera + light upload (SSBO 2/1), the render dispatch and
-its completion (one process per GPU, launched by torch.distributed.run).
-Default workload: config 3, the car scene (4,022 triangles + 100 spheres,
-reference BVH with the 2-triangle road), 1920x1080, maxBounces 3, barycentric,
-no Fresnel.
+A step is one frame of the reference's GPU render loop (src/main.cpp:325-370):
+the per-frame camera + light upload (SSBO 2/1), the render dispatch and its
+completion. Default workload: config 3, the car scene (4,022 triangles + 100
+spheres, reference BVH with the 2-triangle road), 1920x1080, maxBounces 3,
+barycentric, no Fresnel.
 
-Multi-GPU (--mode): frames are independent units, so by default (weak) every
-rank renders its own 1920x1080 frame per step -- frame r of a camera orbit
-around the car, 1 degree per frame, rank 0 = the config's camera -- with no
-collective on the data path: the per-GPU work is fixed as N grows, scaling
-"weak". --mode strong instead splits ONE frame per step across the ranks
-(interleaved 8-row stripes) and gathers it to rank 0 over RCCL: total work
-fixed, scaling "strong" (the frame then ends with its slowest pixel paths,
-DESIGN.md §7).
+--gpus N: one process per GPU. Without torch.distributed.run's environment and
+N > 1, bench.py starts `python -m torch.distributed.run --nproc-per-node N` as a
+CHILD process (before touching the GPU) and exits with its return code; under
+torchrun it checks that WORLD_SIZE == N.
 
-Frames in flight (--inflight F, default auto: 2 at 1920x1080, up to 4 for frames
-too small to fill the GPU, e.g. 800x600): frame n of a rank renders on
-context n % F, each with its own HIP stream and output surface (double
-buffering), so one frame's tail -- its slowest tiles, when most of the GPU is
-idle -- overlaps the next frame's start. Every step still renders one whole
-frame; ms_per_step is the sustained time per frame. The same K frames are also
-timed with one frame in flight (serial_ms_per_step, the single-frame latency
-regime), and kernel_ms_mean / kernel_ms_median are the device durations of the
-individual dispatches in that one-frame pass (the kernel alone on the GPU: the
-roofline's denominator; rocprof's kernel-trace average of `bench.py --inflight 1`
-is the matching profile); kernel_ms_mean_inflight is the same events' mean with
-frames in flight, where a dispatch's span includes waiting for the other frame.
+Modes (--mode auto = frames at N = 1, strong at N > 1):
+  frames  one GPU renders whole frames (frames in flight: --inflight, auto 2 at
+          1080p, up to 4 for frames too small to fill the GPU);
+  strong  the north star's multi-GPU frame: every step renders ONE
+          1920x1080 frame split over the N GPUs by interleaved 8-row stripes and
+          gathers it to rank 0 through the C ABI's rt_group (ncclGather over
+          xGMI, then k_unstripe into rank 0's image) — total work fixed,
+          scaling "strong". Frames in flight = several groups, dealt
+          round-robin, each with its own streams, buffers and communicator;
+  weak    each rank renders its own whole frame per step (frame r of a 1-degree
+          camera orbit about the config's look-at point), no collective.
 
 value = Mrays/s = (closest-hit + shadow rays of the frame, counted on the
 reference walk by the counting kernel) x frames / s, summed over the job.
-Rank 0 prints one JSON line with the roofline of the render kernel and the CPU
-baseline (the oracle, OpenMP on host cores, on a bounded row sample).
+Rank 0 prints one JSON line with the render kernel's roofline and the CPU
+baseline (N = 1 only: the oracle, OpenMP on the host's cores, on a bounded row
+sample of the same frame; plus the reference's 1-core cpuRayTracer).
+
+roofline: the render kernel is bound by dependent-fetch latency, not by HBM
+(DESIGN.md §5). `achieved` = HBM bytes per launch measured by rocprofv3
+(FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_summary.json, the same command) /
+the kernel's mean device time in THIS run (HIP events on the renderer's
+stream, one frame in flight); `frac` = achieved / 8 TB/s. Without a PMC entry
+for the workload it falls back to the compulsory bytes (image + the kernel's
+device records once). The reference-walk bytes of SURVEY §8(d) are reported
+as `reference_equivalent_GBps` (work the accelerator skips; not a bandwidth).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import platform
+import socket
+import subprocess
 import sys
 import time
 
-import numpy as np
-import torch
-import torch.distributed as dist
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
-import rtamd  # noqa: E402
-import tiling  # noqa: E402
-
 METRIC = "Mrays/sec + FPS @1920x1080, car scene (4122 shapes), 1/2/4/8 GPUs"
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
-# config -> (scene generator config, width, height, maxBounces, description)
+# config -> (scene generator config, width, height, maxBounces, description, camera look-at target)
+# The targets are the generators' LookAt points (csrc/scene.cpp: gen_monkey :472, gen_car :549,
+# gen_random :570), about which the weak mode's camera orbit turns.
 WORKLOADS = {
-    2: (2, 800, 600, 1, "monkey stand-in (1,240 shapes), 800x600, primary + shadow"),
-    3: (3, 1920, 1080, 3, "car stand-in (4,022 triangles + 100 spheres), 1920x1080, reflection depth 3"),
-    4: (3, 3840, 2160, 3, "car stand-in, 3840x2160"),
-    5: (5, 1920, 1080, 3, "100k random triangles, deep BVH, 1920x1080"),
+    2: (2, 800, 600, 1, "monkey stand-in (1,240 shapes), 800x600, primary + shadow", (0.0, 10.0, -8.0)),
+    3: (3, 1920, 1080, 3, "car stand-in (4,022 triangles + 100 spheres), 1920x1080, reflection depth 3",
+        (0.0, 0.0, 0.0)),
+    4: (3, 3840, 2160, 3, "car stand-in, 3840x2160", (0.0, 0.0, 0.0)),
+    5: (5, 1920, 1080, 3, "100k random triangles, deep BVH, 1920x1080", (0.0, 0.0, 0.0)),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
@@ -77,19 +77,51 @@ def parse():
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet", "accel"])
     ap.add_argument("--stripe", type=int, default=8)
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU (own context, stream, surface); 0 = auto: 2, or up to 4 "
-                         "while a frame has fewer than 16k 8x8 tiles (too few waves to fill the GPU)")
-    ap.add_argument("--mode", default="weak", choices=["weak", "strong"],
-                    help="N > 1: weak = one frame per GPU (orbit), strong = one frame split over the GPUs + gather")
+                    help="frames in flight per GPU; 0 = auto: 2, or up to 4 while the GPU's share of a frame "
+                         "has fewer than 16k 8x8 tiles (too few waves to fill it)")
+    ap.add_argument("--mode", default="auto", choices=["auto", "frames", "strong", "weak"])
+    ap.add_argument("--gather", default="auto", choices=["auto", "rt", "torch"],
+                    help="strong mode's fan-in: rt = rt_group (RCCL ncclGather, C ABI); torch = "
+                         "torch.distributed.gather (gloo rehearsals); auto = rt on nccl, torch on gloo")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's cores (nproc)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with every rank on one GPU")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(fs, W, H, mb, seconds, threads):
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(a):
+    """--gpus N > 1 outside torchrun: run torchrun as a child and return its exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def host_cores():
+    """What `nproc` reports: OMP_NUM_THREADS if set, else the CPUs this process may run on."""
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    return int(omp) if omp.isdigit() and int(omp) > 0 else len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(rtamd, fs, W, H, mb, seconds, threads):
     """The oracle (oracle/rt_oracle.c, the GLSL restated, OpenMP) on a band of
     rows through the middle of the same frame; the band grows until the
     measurement takes roughly `seconds`."""
@@ -107,13 +139,13 @@ def cpu_baseline(fs, W, H, mb, seconds, threads):
         rows = min(H, max(rows * 2, int(rows * seconds / max(dt, 1e-3) * 0.9)))
     rays = st["closest_rays"] + st["shadow_rays"]
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (GLSL restated, OpenMP) rows [{y0},{y0 + rows}) of the same {W}x{H} frame: "
-                      f"{rows * W} pixels, {rays} rays in {dt:.2f} s",
+            "sample": f"oracle (GLSL restated, OpenMP, {threads} threads) rows [{y0},{y0 + rows}) of the same "
+                      f"{W}x{H} frame: {rows * W} pixels, {rays} rays in {dt:.2f} s",
             "ms_per_frame_equiv": dt * 1e3 * H / rows,
-            "cpu": platform.processor() or platform.machine()}
+            "cpu": cpu_model(), "cpus_visible": os.cpu_count(), "cpus_affinity": len(os.sched_getaffinity(0))}
 
 
-def cpu_reference_1core(seconds):
+def cpu_reference_1core(rtamd, seconds):
     """BASELINE.md "CPU-ref": the reference's own CPU path, cpuRayTracer
     (src/main.cpp:848-894: brute force over every shape, primary rays only, CPU
     phong) restated in oracle/rt_oracle.c, on ONE core as the reference runs it.
@@ -137,7 +169,7 @@ def cpu_reference_1core(seconds):
         if dt >= seconds * 0.5 or rows >= 64:
             break
         rows = min(64, max(rows * 2, int(rows * seconds / max(dt, 1e-3) * 0.9)))
-    return {"kind": "port", "path": "cpuRayTracer (src/main.cpp:848-894)", "cores": 1,
+    return {"kind": "port", "path": "cpuRayTracer (src/main.cpp:848-894)", "cores": 1, "cpu": cpu_model(),
             "config1_ms_per_frame": ms1, "config1_mrays_primary_per_s": 800 * 600 / ms1 / 1e3,
             "config3_primary_only_mrays_per_s": rows * 1920 / dt / 1e6,
             "config3_primary_only_ms_per_frame_equiv": dt * 1e3 * 1080 / rows,
@@ -145,12 +177,56 @@ def cpu_reference_1core(seconds):
                       f"whole 800x600 frames; config 3 rows [{y0},{y0 + rows}) of 1920x1080 in {dt:.2f} s"}
 
 
+def pmc_entry(key):
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f).get(key)
+
+
+def roofline(info, kname, k_ms, pixels, b_ref, pmc):
+    """The render kernel against the HBM roofline (see the module docstring)."""
+    compulsory = 16.0 * pixels + float(info.get("record_bytes", 0))
+    k_s = k_ms * 1e-3
+    measured = pmc["bytes"] if pmc else None
+    achieved = (measured if measured else compulsory) / k_s / 1e9
+    out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": achieved / HBM_PEAK_GBS,
+           "basis": ("measured DRAM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                     f"{pmc['source']}) / this run's mean kernel time") if measured else
+                    "compulsory bytes per launch (16 B/pixel image store + the kernel's device records once) "
+                    "/ this run's mean kernel time (no PMC entry for this workload)",
+           "traffic": measured,
+           "algorithmic_bytes_per_launch": compulsory,
+           "algorithmic_GBps": compulsory / k_s / 1e9,
+           "reference_equivalent_bytes_per_launch": b_ref,
+           "reference_equivalent_GBps": b_ref / k_s / 1e9,
+           "kernel": kname, "kernel_ms": k_ms}
+    if pmc and "issue" in pmc:
+        out["issue"] = pmc["issue"]
+    return out
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(spawn_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 and a.backend == "gloo":
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
+    import rtamd  # noqa: E402
+    import tiling  # noqa: E402
+
+    gloo = a.backend == "gloo"
+    if world > 1 and gloo:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo")
     elif world > 1:
@@ -159,62 +235,78 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    # One non-default stream shared by torch (RCCL waits on it) and the renderer.
+    mode = a.mode if a.mode != "auto" else ("strong" if world > 1 else "frames")
+    if mode == "frames" and world > 1:
+        mode = "weak"
+    strong = mode == "strong"
+    use_group = strong and (a.gather == "rt" or (a.gather == "auto" and not gloo))
+    if use_group and gloo:
+        raise SystemExit("--gather rt needs the nccl backend (one GPU per rank)")
+    # torch's work (gathers on the torch path, the stats all_reduce) on one non-default stream
     torch.cuda.set_stream(torch.cuda.Stream())
 
-    cfg, W, H, mb, desc = WORKLOADS[a.config]
+    cfg, W, H, mb, desc, target = WORKLOADS[a.config]
     sc = rtamd.Scene().generate(cfg, a.variant, W / H)
     sc_stats = sc.bvh_stats()
-    strong = a.mode == "strong" and world > 1
-    if not strong and rank > 0:
-        # frame `rank` of the orbit: the camera turned about the vertical axis through
-        # the look-at point (the origin) by `rank` degrees
-        cam0 = sc.serializeScene().camera
-        p = cam0["Position"][0].astype(np.float64)
-        ang = np.radians(float(rank))
-        pos = (p[0] * np.cos(ang) + p[2] * np.sin(ang), p[1], -p[0] * np.sin(ang) + p[2] * np.cos(ang))
-        sc.set_camera(pos, float(cam0["fov"][0]), float(cam0["aspectRatio"][0]))
-        sc.LookAt((0.0, 0.0, 0.0))
+    if mode == "weak" and rank > 0:
+        sc.orbit(target, float(rank))  # frame `rank` of the orbit: `rank` degrees about the look-at point
     fs = sc.serializeScene()
+    kernel_id = {"auto": 0, "lane": 1, "packet": 2, "accel": 3}[a.kernel]
 
-    # strong mode gathers one shared buffer per step: one frame in flight there
-    tiles = ((W + 7) // 8) * ((H + 7) // 8)
-    F = 1 if strong else (a.inflight if a.inflight > 0 else min(4, max(2, -(-16384 // tiles) + 1)))
-    main_stream = torch.cuda.current_stream()
-    streams = [main_stream] + [torch.cuda.Stream() for _ in range(F - 1)]
-    ctxs = []
-    for s_ in streams:
-        c_ = rtamd.ComputeShader(torch.cuda.current_device())
-        c_.set_stream(s_.cuda_stream)
-        c_.upload(fs)
-        c_.set_params(W, H, mb, True, False, False)
-        c_.set_kernel({"auto": 0, "lane": 1, "packet": 2, "accel": 3}[a.kernel])
-        ctxs.append(c_)
-    ctx = ctxs[0]
-
-    # strong: this rank's interleaved stripes of the one frame; weak: the rank's whole frame
     plan = tiling.StripePlan(H, world if strong else 1, a.stripe)
     prank = rank if strong else 0
     rows = plan.rows(prank)
-    bufs = [torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev) for _ in range(F)]
+    tiles = ((W + 7) // 8) * ((rows + 7) // 8)
+    F = a.inflight if a.inflight > 0 else min(4, max(2, -(-16384 // tiles) + 1))
+    if strong and not use_group:
+        F = 1  # the torch path gathers one shared buffer per step
+
+    # F frames in flight: F renderers per GPU (contexts or groups), each with its own stream
+    groups, ctxs, bufs = [], [], []
+    if use_group:
+        for _ in range(F):
+            uid = [rtamd.group_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            g = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local)
+            g.upload(fs)
+            g.set_params(W, H, mb, True, False, False)
+            g.members[0].set_kernel(kernel_id)
+            groups.append(g)
+            ctxs.append(g.members[0])
+    else:
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
+        for s_ in streams:
+            c_ = rtamd.ComputeShader(torch.cuda.current_device())
+            c_.set_stream(s_.cuda_stream)
+            c_.upload(fs)
+            c_.set_params(W, H, mb, True, False, False)
+            c_.set_kernel(kernel_id)
+            ctxs.append(c_)
+            bufs.append(torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev))
+    ctx = ctxs[0]
 
     # Work of this rank's rows on the reference walk (counting kernel, untimed).
     st = ctx.collect_stats(W, H, plan.y0(prank), a.stripe, plan.world, rows)
     mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, rows * W), st["hits"]],
-                        dtype=torch.float64, device=dev)
+                        dtype=torch.float64, device="cpu" if gloo else dev)
     total = mine.clone()
     if world > 1:
-        total = total.cpu() if a.backend == "gloo" else total
         dist.all_reduce(total)
     rays_step = float(total[0] + total[1])  # all ranks' rays of one step
-    b_alg_rank = float(mine[2])
+    b_ref_rank = float(mine[2])
 
     cam, light = fs.camera, fs.light
 
     def frame(i, inflight):
+        if use_group:
+            g = groups[i % inflight]
+            g.set_camera(cam)    # SSBO 2 (src/main.cpp:328-330)
+            g.set_light(light)   # SSBO 1 (:332-334)
+            g.dispatch(W, H, a.stripe)  # this rank's stripes + ncclGather + unstripe on rank 0
+            return
         c_ = ctxs[i % inflight]
-        c_.set_camera(cam)   # SSBO 2 (src/main.cpp:328-330)
-        c_.set_light(light)  # SSBO 1 (:332-334)
+        c_.set_camera(cam)
+        c_.set_light(light)
         buf = bufs[i % inflight]
         c_.dispatch_rows(W, H, plan.y0(prank), a.stripe, plan.world, rows, buf.data_ptr(), W * 16)
         if strong:
@@ -233,11 +325,10 @@ def main():
         t0 = time.perf_counter()
         for i in range(a.steps):
             frame(i, inflight)
-        torch.cuda.synchronize()
+        torch.cuda.synchronize()  # the device: every renderer stream, RCCL and unstripe included
         if world > 1:
             dist.barrier()
-        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                          device="cpu" if a.backend == "gloo" else dev)
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cpu" if gloo else dev)
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el[0])
@@ -246,7 +337,7 @@ def main():
     serial_kt = ctx.kernel_times() if F > 1 else None
     elapsed = timed(F)
 
-    kt_if = np.concatenate([c_.kernel_times() for c_ in ctxs]) if F > 1 else ctx.kernel_times()
+    kt_if = np.concatenate([c_.kernel_times() for c_ in ctxs])
     # The render kernel's duration is taken where it runs alone (the one-frame-in-flight
     # pass): with frames in flight a dispatch's events also span the time it waits for
     # the other frame's waves to leave the CUs.
@@ -257,14 +348,13 @@ def main():
     k_med = float(np.median(kt)) if len(kt) else float("nan")
 
     if rank == 0:
-        frames = a.steps * (1 if strong or world == 1 else world)
+        frames = a.steps * (world if mode == "weak" else 1)
         fps = frames / elapsed
-        achieved = b_alg_rank / (k_ms * 1e-3) / 1e9
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                traffic = json.load(f).get(f"config{a.config}_n{world}_{a.kernel}")
+        gather = None
+        if strong:
+            gather = ("rt_group: ncclGather to rank 0 (RCCL over xGMI) + k_unstripe, C ABI (include/rt_group.h)"
+                      if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
+        pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}") if not strong or world == 1 else None
         out = {
             "metric": METRIC,
             "value": rays_step * a.steps / elapsed / 1e6,
@@ -281,38 +371,33 @@ def main():
             "dtype": "f32",
             "data": "synthetic (procedural stand-in meshes, fixed seed; the reference's .obj assets are absent)",
             "backend": a.backend if world > 1 else None,
+            "mode": mode,
+            "ranks_seen": world,
             "config": {"workload": f"config {a.config}: {desc}" + (" (222-strip road)" if a.variant else ""),
                        "width": W, "height": H, "maxBounces": mb, "useBVH": 1, "useFresnel": 0,
                        "triangle_test": "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
                        "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel,
-                       "parallelism": (f"row-stripes{a.stripe}x{world}+rccl-gather" if strong else
-                                       f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)")},
+                       "parallelism": (f"row-stripes{a.stripe}x{world}+gather" if strong else
+                                       f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"
+                                       if mode == "weak" else "1 GPU")},
+            "gather": gather,
             "fps": fps,
             "mrays_primary_per_s": W * H * fps / 1e6,
             "rays_per_step": rays_step,
             "kernel_ms_mean": k_ms,
             "kernel_ms_median": k_med,
             "kernel_ms_mean_inflight": float(np.mean(kt_if)) if len(kt_if) else float("nan"),
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                # the same bytes over the sustained frame time (frames overlap when F > 1)
-                "aggregate_achieved": b_alg_rank * a.steps / elapsed / 1e9,
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": b_alg_rank,
-                "kernel": kname,
-            },
+            "roofline": roofline(info, kname, k_ms, rows * W, b_ref_rank, pmc),
             "accel": info,
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu:
-            thr = a.cpu_threads or min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(fs, W, H, mb, a.cpu_seconds, thr)
-            out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(a.cpu_seconds / 2)
+            thr = a.cpu_threads or host_cores()
+            out["cpu_baseline"] = cpu_baseline(rtamd, fs, W, H, mb, a.cpu_seconds, thr)
+            out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2)
         print(json.dumps(out), flush=True)
+    for g in groups:
+        g.close()
     for c_ in ctxs:
         c_.close()
     if world > 1:

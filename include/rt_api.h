@@ -32,7 +32,8 @@ enum rt_status {
     RT_ERR_NO_MEMORY = -3, /* device allocation failed                               */
     RT_ERR_NO_SCENE = -4,  /* dispatch before rt_upload_scene / camera / light       */
     RT_ERR_BVH = -5,       /* node/index arrays are out of range or too deep         */
-    RT_ERR_NO_DEVICE = -6  /* no HIP device with that ordinal                        */
+    RT_ERR_NO_DEVICE = -6, /* no HIP device with that ordinal                        */
+    RT_ERR_COMM = -7       /* an RCCL call failed (rt_group.h)                       */
 };
 
 /* Uniforms of gpu_shader.comp:126-130, set by src/main.cpp:357-361.
@@ -69,6 +70,8 @@ typedef struct rt_accel_info {
     int scene_items;         /* its leaves (shapes of one reference leaf each)         */
     int scene_height;        /* its binary height                                      */
     int tree_nested;         /* the reference tree's child boxes lie in their parents' */
+    int record_bytes;        /* device records the accelerated kernel reads: nodes,   */
+                             /* items, shapes, materials (its compulsory scene bytes)  */
 } rt_accel_info;
 
 /* Work counted on the reference's own traversal (gpu_shader.comp:380-430 and
@@ -158,8 +161,10 @@ int rt_dispatch_rows(struct rt_ctx* ctx, int width, int height, int y0, int stri
 /* glMemoryBarrier + wait: blocks until the context's stream is drained. */
 int rt_sync(struct rt_ctx* ctx);
 
-/* Read the context surface back to host memory (rows [0,height), `pitch` bytes). */
-int rt_read_image(struct rt_ctx* ctx, float* host_dst, size_t pitch);
+/* Read the context surface back to host memory: `height` rows of `pitch` bytes.
+ * width/height state the destination's size and must equal the surface's (the
+ * last rt_dispatch's W x H), so a short buffer is refused, never overrun. */
+int rt_read_image(struct rt_ctx* ctx, float* host_dst, size_t pitch, int width, int height);
 
 /* Device pointer and pitch of the context surface (zero-copy hand-off). */
 int rt_device_image(struct rt_ctx* ctx, void** ptr, size_t* pitch);

@@ -1,0 +1,97 @@
+/*
+ * rt_group.h — one frame split over several GPUs, gathered to rank 0
+ * (librtamd.so).
+ *
+ * The reference renders a frame with one glDispatchCompute(W, H, 1) on one GPU
+ * (src/main.cpp:352-354). Pixels are independent (gpu_shader.comp:434-623
+ * reads no other pixel), so a group splits the frame's rows over its ranks:
+ * rank r of P renders the interleaved stripe set
+ *     { image row y : (y / stripe) mod P == r }
+ * (rt_dispatch_rows with y0 = r*stripe, step = P) into a compact buffer of
+ * rows_max = max over ranks of its row count. One fan-in per frame brings the
+ * P buffers to rank 0 — ncclGather over xGMI (RCCL) or device copies — and a
+ * kernel on rank 0 scatters the stripes back into image order in rank 0's
+ * pitched RGBA32F surface. Interleaving balances sky rows against rows through
+ * the car without any per-frame planning; no other collective runs.
+ *
+ * Two ways to build a group:
+ *  - rt_group_create: ONE process drives every device (ncclCommInitAll, the
+ *    single-process plan of SURVEY §7 step 7). Devices must be distinct for
+ *    RCCL; a device list with repeats uses the copy transport.
+ *  - rt_group_create_rank: one process per GPU (torch.distributed.run, the
+ *    bench's launch); each process holds its one member, rank `rank` of
+ *    `nranks`, and the ranks meet through the 128-byte id that rank 0 makes
+ *    with rt_group_unique_id and sends to the others (ncclCommInitRank).
+ *
+ * Frames in flight: a group renders one frame at a time (its members' streams
+ * order frame k+1's render after frame k's gather). A caller that wants
+ * several frames in flight makes several groups and deals frames round-robin.
+ * Every call returns an rt_status (rt_api.h); RT_ERR_COMM for RCCL failures
+ * (and for RCCL forced on a device list with repeats).
+ */
+#ifndef RT_GROUP_H
+#define RT_GROUP_H
+
+#include <stddef.h>
+#include "rt_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+struct rt_group; /* opaque */
+
+#define RT_GROUP_ID_BYTES 128
+
+enum rt_gather {
+    RT_GATHER_AUTO = 0,  /* RCCL when the ranks' devices are distinct, copies otherwise */
+    RT_GATHER_RCCL = 1,  /* ncclGather to rank 0 on the members' streams                */
+    RT_GATHER_COPY = 2   /* hipMemcpyPeerAsync into rank 0's staging (one process only) */
+};
+
+/* ncclGetUniqueId: rank 0 of a multi-process group makes it, every rank passes
+ * it to rt_group_create_rank. `cap` >= RT_GROUP_ID_BYTES. */
+int rt_group_unique_id(void* id, size_t cap);
+
+/* One process, member k = rank k on devices[k] (n >= 1). */
+int rt_group_create(struct rt_group** out, const int* devices, int n, int transport);
+
+/* One process per GPU: this process's member is rank `rank` of `nranks`, on
+ * HIP device `device`. Always RCCL (ncclCommInitRank). */
+int rt_group_create_rank(struct rt_group** out, const void* id, int nranks, int rank, int device);
+
+int rt_group_destroy(struct rt_group* g);
+
+/* nranks, members driven by this process, transport in use (RT_GATHER_RCCL/COPY). */
+int rt_group_info(struct rt_group* g, int* nranks, int* nlocal, int* transport);
+
+/* The context of local member k (0 <= k < nlocal), for per-context settings
+ * (rt_set_kernel, rt_set_walk, rt_kernel_times, ...). Owned by the group. */
+int rt_group_member(struct rt_group* g, int k, struct rt_ctx** ctx);
+
+/* rt_upload_scene / rt_set_camera / rt_set_light / rt_set_params on every
+ * local member (the scene is replicated: < 1 MB for the car, 28 MB at 100k). */
+int rt_group_upload_scene(struct rt_group* g, const FlatShape* shapes, int num_shapes, const FlatNode* nodes,
+                          int num_nodes, const int* indices, int num_indices);
+int rt_group_set_camera(struct rt_group* g, const FlatCamera* camera);
+int rt_group_set_light(struct rt_group* g, const FlatLight* light);
+int rt_group_set_params(struct rt_group* g, const rt_params* params);
+
+/* Render the W x H frame split into `stripe`-row stripes over the ranks and
+ * gather it into rank 0's surface. Stream-ordered and asynchronous; every rank
+ * calls it for every frame, in the same order. */
+int rt_group_dispatch(struct rt_group* g, int width, int height, int stripe);
+
+/* Wait until this process's members have finished their last frame. */
+int rt_group_sync(struct rt_group* g);
+
+/* Rank 0's surface (RT_ERR_INVALID in a process without rank 0). read_image
+ * copies the whole frame; width/height must equal the last dispatch's. */
+int rt_group_read_image(struct rt_group* g, float* host_dst, size_t pitch, int width, int height);
+int rt_group_device_image(struct rt_group* g, void** ptr, size_t* pitch);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_GROUP_H */

@@ -1772,6 +1772,7 @@ struct rt_ctx {
     int nfew = 0;              // few-leaf mode (AccelPtrs::nfew)
     int* prim_idx_dev = nullptr;
     bool accel_ok = false;
+    size_t record_bytes = 0;   // device records k_accel reads (rt_accel_info::record_bytes)
     int boxes_finite = 0;
     rta::AccelHost accel;
     // frame constants
@@ -2094,6 +2095,8 @@ int build_upload_accel(rt_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host vectors die here
     c->st_root = use_st ? static_cast<int>(kLocal | static_cast<unsigned>(nw + T.wroot)) : kNoChild;
     c->accel_ok = true;
+    c->record_bytes = (an.size() + ln.size() + wn.size() + tl.size() + ti.size() + 5 * P + 2 * static_cast<size_t>(c->S)) *
+                      sizeof(float4);
     return RT_OK;
 }
 
@@ -2531,6 +2534,7 @@ const char* rt_status_string(int s) {
         case RT_ERR_NO_SCENE: return "scene, camera or light not uploaded";
         case RT_ERR_BVH: return "node/index arrays out of range or deeper than the 64-entry stack";
         case RT_ERR_NO_DEVICE: return "no such HIP device";
+        case RT_ERR_COMM: return "RCCL call failed";
         default: return "unknown status";
     }
 }
@@ -2904,8 +2908,10 @@ int rt_sync(rt_ctx* c) {
     return RT_OK;
 }
 
-int rt_read_image(rt_ctx* c, float* dst, size_t pitch) {
-    if (!c || !dst || !c->img || pitch < static_cast<size_t>(c->img_w) * 16) return RT_ERR_INVALID;
+int rt_read_image(rt_ctx* c, float* dst, size_t pitch, int width, int height) {
+    if (!c || !dst || !c->img || width != c->img_w || height != c->img_h ||
+        pitch < static_cast<size_t>(c->img_w) * 16)
+        return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     HIP_TRY(hipMemcpy2DAsync(dst, pitch, c->img, c->img_pitch, static_cast<size_t>(c->img_w) * 16, c->img_h,
                              hipMemcpyDeviceToHost, c->stream));
@@ -2995,6 +3001,7 @@ extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
     out->scene_items = static_cast<int>(c->accel.st.item_ref.size());
     out->scene_height = c->accel.st.height;
     out->tree_nested = c->accel.st.nested;
+    out->record_bytes = c->accel_ok ? static_cast<int>(std::min<size_t>(c->record_bytes, 0x7fffffff)) : 0;
     return RT_OK;
 }
 

@@ -83,7 +83,7 @@ class rt_params(C.Structure):
 class rt_accel_info(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("built", "local_nodes", "local_leaves", "bounded_prims", "always_prims",
                                        "max_stack", "last_kernel", "scene_tree", "scene_nodes", "scene_items",
-                                       "scene_height", "tree_nested")]
+                                       "scene_height", "tree_nested", "record_bytes")]
 
 
 class rt_stats(C.Structure):
@@ -116,7 +116,7 @@ def algorithmic_bytes(st: dict, pixels_written: int, use_mt: bool = False) -> in
 
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
           -4: "scene, camera or light not uploaded", -5: "node/index arrays out of range or deeper than the 64-entry stack",
-          -6: "no such HIP device"}
+          -6: "no such HIP device", -7: "RCCL call failed"}
 
 
 class RTError(RuntimeError):
@@ -186,7 +186,7 @@ RT_SYMBOLS = {
     "rt_set_params": (_I, [_P, _P]), "rt_set_kernel": (_I, [_P, _I]),
     "rt_dispatch": (_I, [_P, _I, _I, _I, _I]),
     "rt_dispatch_rows": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t]),
-    "rt_sync": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t]),
+    "rt_sync": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
     "rt_device_image": (_I, [_P, _P, _P]),
     "rt_collect_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
     "rt_last_kernel_ms": (_I, [_P, _P]),
@@ -202,6 +202,25 @@ RT_SYMBOLS = {
     "rt_set_tail": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
+
+# include/rt_group.h (also in librtamd.so)
+GROUP_SYMBOLS = {
+    "rt_group_unique_id": (_I, [_P, C.c_size_t]),
+    "rt_group_create": (_I, [_P, _P, _I, _I]),
+    "rt_group_create_rank": (_I, [_P, _P, _I, _I, _I]),
+    "rt_group_destroy": (_I, [_P]),
+    "rt_group_info": (_I, [_P, _P, _P, _P]),
+    "rt_group_member": (_I, [_P, _I, _P]),
+    "rt_group_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
+    "rt_group_set_camera": (_I, [_P, _P]), "rt_group_set_light": (_I, [_P, _P]),
+    "rt_group_set_params": (_I, [_P, _P]),
+    "rt_group_dispatch": (_I, [_P, _I, _I, _I]),
+    "rt_group_sync": (_I, [_P]),
+    "rt_group_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
+    "rt_group_device_image": (_I, [_P, _P, _P]),
+}
+GATHER_AUTO, GATHER_RCCL, GATHER_COPY = 0, 1, 2
+GROUP_ID_BYTES = 128
 
 
 def _bind(lib, table, partial=False):
@@ -225,7 +244,7 @@ def scene_lib():
 def rt_lib():
     global _rt_lib
     if _rt_lib is None:
-        _rt_lib = _bind(_load("librtamd.so"), RT_SYMBOLS)
+        _rt_lib = _bind(_bind(_load("librtamd.so"), RT_SYMBOLS), GROUP_SYMBOLS)
     return _rt_lib
 
 
@@ -324,6 +343,24 @@ class Scene:
 
     def set_light(self, position, color=(1, 1, 1), intensity=1.0):
         self._chk(self._lib.rts_set_light(self._h, _f3(position), _f3(color), intensity), "set_light")
+
+    def camera(self):
+        """serializeCamera (src/main.cpp:806-816) alone."""
+        cam = np.zeros(1, CAMERA_DTYPE)
+        self._chk(self._lib.rts_serialize(self._h, None, None, None, _ptr(cam), None), "serializeCamera")
+        return cam
+
+    def orbit(self, target, degrees):
+        """Turn the camera `degrees` about the vertical axis through `target` and
+        look at `target` again (the weak bench mode's per-rank frames of an orbit).
+        The rotation is done in float64 on the serialised position."""
+        cam = self.camera()
+        p = cam["Position"][0].astype(np.float64) - np.asarray(target, np.float64)
+        ang = np.radians(float(degrees))
+        q = (p[0] * np.cos(ang) + p[2] * np.sin(ang), p[1], -p[0] * np.sin(ang) + p[2] * np.cos(ang))
+        self.set_camera(np.asarray(q) + np.asarray(target, np.float64), float(cam["fov"][0]),
+                        float(cam["aspectRatio"][0]))
+        self.LookAt(target)
 
     def buildBVH(self, maxDepth=15):
         self._chk(self._lib.rts_build_bvh(self._h, maxDepth), "buildBVH")
@@ -466,7 +503,7 @@ class ComputeShader:
 
     def read_image(self, width, height):
         out = np.empty((height, width, 4), np.float32)
-        self._chk(self._lib.rt_read_image(self._h, _ptr(out), width * 16), "rt_read_image")
+        self._chk(self._lib.rt_read_image(self._h, _ptr(out), width * 16, width, height), "rt_read_image")
         return out
 
     def render(self, width, height, y0=0, y1=None):
@@ -603,3 +640,107 @@ class ComputeShader:
         ms = C.c_float()
         self._chk(self._lib.rt_last_kernel_ms(self._h, C.byref(ms)), "rt_last_kernel_ms")
         return ms.value
+
+
+# ---------------------------------------------------------------------------
+def group_unique_id() -> bytes:
+    """ncclGetUniqueId for rt_group_create_rank (rank 0 makes it, the others receive it)."""
+    buf = (C.c_char * GROUP_ID_BYTES)()
+    rc = rt_lib().rt_group_unique_id(buf, GROUP_ID_BYTES)
+    if rc != 0:
+        raise RTError("rt_group_unique_id", rc)
+    return bytes(buf)
+
+
+class _Member(ComputeShader):
+    """A group member's context: owned (and destroyed) by its Group."""
+
+    def __init__(self, lib, handle, device):
+        self._lib = lib
+        self._h = handle
+        self.device = device
+
+    def close(self):
+        self._h = None
+
+
+class Group:
+    """One frame over several GPUs (include/rt_group.h): interleaved row stripes
+    per rank, gathered to rank 0 by ncclGather (RCCL) or device copies.
+
+    Group(devices=[0, 1, ...])            one process drives every device
+    Group(uid=..., nranks=P, rank=r, device=d)   one process per GPU
+    """
+
+    def __init__(self, devices=None, transport=GATHER_AUTO, uid=None, nranks=None, rank=None, device=None):
+        self._lib = rt_lib()
+        h = C.c_void_p()
+        if uid is not None:
+            idb = (C.c_char * GROUP_ID_BYTES).from_buffer_copy(uid)
+            self._chk(self._lib.rt_group_create_rank(C.byref(h), idb, int(nranks), int(rank), int(device)),
+                      "rt_group_create_rank")
+        else:
+            d = np.ascontiguousarray(devices, np.int32)
+            self._chk(self._lib.rt_group_create(C.byref(h), _ptr(d), len(d), int(transport)), "rt_group_create")
+        self._h = h
+        n, nl, tr = C.c_int(), C.c_int(), C.c_int()
+        self._chk(self._lib.rt_group_info(h, C.byref(n), C.byref(nl), C.byref(tr)), "rt_group_info")
+        self.nranks, self.nlocal, self.transport = n.value, nl.value, tr.value
+        self.members = []
+        for k in range(self.nlocal):
+            c = C.c_void_p()
+            self._chk(self._lib.rt_group_member(h, k, C.byref(c)), "rt_group_member")
+            self.members.append(_Member(self._lib, c, device if uid is not None else int(devices[k])))
+
+    @staticmethod
+    def _chk(rc, what):
+        if rc != 0:
+            raise RTError(what, rc)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            for m in self.members:
+                m.close()
+            self._lib.rt_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def upload(self, fs: FlatScene):
+        self._keep = fs
+        self._chk(self._lib.rt_group_upload_scene(self._h, _ptr(fs.shapes), len(fs.shapes), _ptr(fs.nodes),
+                                                  len(fs.nodes), _ptr(fs.indices), len(fs.indices)),
+                  "rt_group_upload_scene")
+        self.set_camera(fs.camera)
+        self.set_light(fs.light)
+
+    def set_camera(self, cam):
+        cam = as_records(cam, CAMERA_DTYPE)
+        self._chk(self._lib.rt_group_set_camera(self._h, _ptr(cam)), "rt_group_set_camera")
+
+    def set_light(self, light):
+        light = as_records(light, LIGHT_DTYPE)
+        self._chk(self._lib.rt_group_set_light(self._h, _ptr(light)), "rt_group_set_light")
+
+    def set_params(self, resX, resY, maxBounces=3, useBVH=True, useFresnel=False, useMollerTrumbore=False):
+        p = rt_params(float(resX), float(resY), int(maxBounces), int(bool(useBVH)), int(bool(useFresnel)),
+                      int(bool(useMollerTrumbore)))
+        self._chk(self._lib.rt_group_set_params(self._h, C.byref(p)), "rt_group_set_params")
+
+    def dispatch(self, width, height, stripe=8):
+        self._chk(self._lib.rt_group_dispatch(self._h, width, height, stripe), "rt_group_dispatch")
+
+    def sync(self):
+        self._chk(self._lib.rt_group_sync(self._h), "rt_group_sync")
+
+    def read_image(self, width, height):
+        out = np.empty((height, width, 4), np.float32)
+        self._chk(self._lib.rt_group_read_image(self._h, _ptr(out), width * 16, width, height),
+                  "rt_group_read_image")
+        return out
+
+    def render(self, width, height, stripe=8):
+        self.dispatch(width, height, stripe)
+        self.sync()
+        return self.read_image(width, height)

@@ -1,0 +1,148 @@
+// group_check.cpp — a C++ host (no Python, no torch) drives the multi-GPU
+// entry points of librtamd.so (include/rt_group.h) and checks that the
+// gathered frame equals the single-dispatch frame bit for bit.
+//
+//   group_check W H [config [ranks]]   exit 0 = every case identical
+//
+// Cases run on whatever devices the box has:
+//   * copy transport, 1..ranks (default 4) ranks all on device 0 (stripes + peer copies + unstripe);
+//   * RCCL transport, one rank per distinct device (ncclCommInitAll + ncclGather),
+//     which on a 1-GPU box is the 1-rank communicator;
+//   * on >= 2 devices, RCCL over the first 2 and all devices.
+// The scene is the config's own (rts_generate: the reference's builder and
+// serialisers), uploaded as the reference uploads its SSBOs (src/main.cpp:256-275).
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/rt_api.h"
+#include "../../include/rt_group.h"
+#include "../../include/rt_scene.h"
+
+#define CHECK(x)                                                                         \
+    do {                                                                                 \
+        int rc__ = (x);                                                                  \
+        if (rc__ != RT_OK) {                                                             \
+            std::fprintf(stderr, "%s:%d %s -> %d (%s)\n", __FILE__, __LINE__, #x, rc__,  \
+                         rt_status_string(rc__));                                        \
+            std::exit(2);                                                                \
+        }                                                                                \
+    } while (0)
+
+struct Scene {
+    std::vector<FlatShape> shapes;
+    std::vector<FlatNode> nodes;
+    std::vector<int> idx;
+    FlatCamera cam;
+    FlatLight light;
+};
+
+static Scene make_scene(int config, int W, int H) {
+    Scene s;
+    rts_scene* h = rts_new();
+    if (!h || rts_generate(h, config, 0, static_cast<float>(W) / static_cast<float>(H)) < 0) std::exit(3);
+    int S = 0, N = 0, I = 0;
+    rts_counts(h, &S, &N, &I);
+    s.shapes.resize(S);
+    s.nodes.resize(N);
+    s.idx.resize(I);
+    if (rts_serialize(h, s.shapes.data(), s.nodes.data(), s.idx.data(), &s.cam, &s.light) < 0) std::exit(3);
+    rts_free(h);
+    return s;
+}
+
+static int compare(const char* what, const std::vector<float>& ref, const std::vector<float>& img) {
+    size_t bad = 0;
+    for (size_t i = 0; i < ref.size(); ++i) bad += std::memcmp(&ref[i], &img[i], 4) != 0;
+    std::printf("%-44s %s (%zu of %zu floats differ)\n", what, bad ? "DIFFERS" : "identical", bad, ref.size());
+    return bad ? 1 : 0;
+}
+
+static int run_group(const char* what, const Scene& s, const rt_params& p, int W, int H, int stripe,
+                     const int* devs, int n, int transport, const std::vector<float>& ref) {
+    rt_group* g = nullptr;
+    const int rc = rt_group_create(&g, devs, n, transport);
+    if (rc != RT_OK) {
+        std::printf("%-44s create failed: %s\n", what, rt_status_string(rc));
+        return 1;
+    }
+    CHECK(rt_group_upload_scene(g, s.shapes.data(), static_cast<int>(s.shapes.size()), s.nodes.data(),
+                                static_cast<int>(s.nodes.size()), s.idx.data(), static_cast<int>(s.idx.size())));
+    CHECK(rt_group_set_camera(g, &s.cam));
+    CHECK(rt_group_set_light(g, &s.light));
+    CHECK(rt_group_set_params(g, &p));
+    // three frames: the buffers are reused across frames, as in a render loop
+    for (int f = 0; f < 3; ++f) CHECK(rt_group_dispatch(g, W, H, stripe));
+    CHECK(rt_group_sync(g));
+    std::vector<float> img(static_cast<size_t>(W) * H * 4);
+    CHECK(rt_group_read_image(g, img.data(), static_cast<size_t>(W) * 16, W, H));
+    int nr = 0, nl = 0, tr = 0;
+    CHECK(rt_group_info(g, &nr, &nl, &tr));
+    char label[96];
+    std::snprintf(label, sizeof label, "%s [%d ranks, %s]", what, nr, tr == RT_GATHER_RCCL ? "rccl" : "copy");
+    // a short destination is refused, not overrun
+    const int short_rc = rt_group_read_image(g, img.data(), static_cast<size_t>(W) * 16, W, H - 1);
+    CHECK(rt_group_destroy(g));
+    if (short_rc != RT_ERR_INVALID) {
+        std::printf("%s: short read_image returned %d\n", label, short_rc);
+        return 1;
+    }
+    return compare(label, ref, img);
+}
+
+int main(int argc, char** argv) {
+    const int W = argc > 1 ? std::atoi(argv[1]) : 480;
+    const int H = argc > 2 ? std::atoi(argv[2]) : 270;
+    const int config = argc > 3 ? std::atoi(argv[3]) : 3;
+    const int max_ranks = argc > 4 ? std::atoi(argv[4]) : 4;
+    int ndev = 0;  // devices, probed through the C ABI (rt_create refuses an absent ordinal)
+    for (rt_ctx* probe = nullptr; rt_create(&probe, ndev) == RT_OK; ++ndev) rt_destroy(probe);
+    if (ndev < 1) {
+        std::fprintf(stderr, "no HIP device\n");
+        return 4;
+    }
+    std::printf("%d HIP device(s)\n", ndev);
+    const Scene s = make_scene(config, W, H);
+    const rt_params p{static_cast<float>(W), static_cast<float>(H), 3, 1, 0, 0};
+
+    // the single-dispatch frame (rt_dispatch of the whole image on device 0)
+    rt_ctx* c = nullptr;
+    CHECK(rt_create(&c, 0));
+    CHECK(rt_upload_scene(c, s.shapes.data(), static_cast<int>(s.shapes.size()), s.nodes.data(),
+                          static_cast<int>(s.nodes.size()), s.idx.data(), static_cast<int>(s.idx.size())));
+    CHECK(rt_set_camera(c, &s.cam));
+    CHECK(rt_set_light(c, &s.light));
+    CHECK(rt_set_params(c, &p));
+    CHECK(rt_dispatch(c, W, H, 0, H));
+    CHECK(rt_sync(c));
+    std::vector<float> ref(static_cast<size_t>(W) * H * 4);
+    CHECK(rt_read_image(c, ref.data(), static_cast<size_t>(W) * 16, W, H));
+    CHECK(rt_destroy(c));
+
+    int fails = 0;
+    const std::vector<int> zeros(max_ranks > 3 ? max_ranks : 3, 0);
+    for (int n = 1; n <= max_ranks; ++n) {
+        char what[64];
+        std::snprintf(what, sizeof what, "config %d %dx%d, stripes of 8", config, W, H);
+        fails += run_group(what, s, p, W, H, 8, zeros.data(), n, RT_GATHER_COPY, ref);
+    }
+    fails += run_group("stripes of 5 (ragged last stripe)", s, p, W, H, 5, zeros.data(), 3, RT_GATHER_COPY, ref);
+    fails += run_group("stripe taller than the frame", s, p, W, H, H + 3, zeros.data(), 2, RT_GATHER_COPY, ref);
+    fails += run_group("rccl, one rank per device", s, p, W, H, 8, zeros.data(), 1, RT_GATHER_RCCL, ref);
+    {
+        rt_group* g = nullptr;
+        const int rc = rt_group_create(&g, zeros.data(), 2, RT_GATHER_RCCL);
+        std::printf("%-44s %s\n", "rccl forced on a repeated device", rc == RT_ERR_COMM ? "refused" : "NOT refused");
+        fails += rc == RT_ERR_COMM ? 0 : 1;
+        if (g) rt_group_destroy(g);
+    }
+    if (ndev >= 2) {
+        std::vector<int> all(ndev);
+        for (int d = 0; d < ndev; ++d) all[d] = d;
+        fails += run_group("rccl over 2 devices", s, p, W, H, 8, all.data(), 2, RT_GATHER_RCCL, ref);
+        fails += run_group("rccl over every device", s, p, W, H, 8, all.data(), ndev, RT_GATHER_RCCL, ref);
+    }
+    std::printf("%s\n", fails ? "FAIL" : "OK");
+    return fails ? 1 : 0;
+}

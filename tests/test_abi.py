@@ -18,20 +18,24 @@ def declared(header):
     return sorted(set(DECL.findall(text)))
 
 
-@pytest.mark.parametrize("header,lib", [("rt_api.h", "librtamd.so"), ("rt_scene.h", "librtscene.so")])
-def test_exports(header, lib):
+TABLES = {"rt_api.h": ("librtamd.so", rtamd.RT_SYMBOLS), "rt_group.h": ("librtamd.so", rtamd.GROUP_SYMBOLS),
+          "rt_scene.h": ("librtscene.so", rtamd.SCENE_SYMBOLS)}
+
+
+@pytest.mark.parametrize("header", sorted(TABLES))
+def test_exports(header):
+    lib, table = TABLES[header]
     names = declared(header)
     assert len(names) >= 12, names
     so = C.CDLL(os.path.join(rtamd.LIBDIR, lib))
     missing = [n for n in names if not hasattr(so, n)]
     assert not missing, missing
-    table = rtamd.RT_SYMBOLS if lib == "librtamd.so" else rtamd.SCENE_SYMBOLS
     assert sorted(table) == names, "binding table out of sync with the header"
 
 
 def test_status_strings():
     lib = rtamd.rt_lib()
-    for code in range(0, -7, -1):
+    for code in range(0, -8, -1):
         assert lib.rt_status_string(code).decode() == rtamd.STATUS[code]
 
 

@@ -1,0 +1,79 @@
+"""bench.py's host logic on CPU: --gpus N launches torchrun as a child, a
+WORLD_SIZE that disagrees with --gpus is refused before any GPU work, the
+CPU baseline sizes itself to the host, the weak mode's orbit camera turns
+about the config's own look-at point, and the roofline never claims more
+than the HBM peak from the bytes it is given."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import bench
+import rtamd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_gpus_spawns_torchrun_child(monkeypatch):
+    seen = {}
+
+    def fake_call(cmd):
+        seen["cmd"] = cmd
+        return 7
+
+    monkeypatch.setattr(bench.subprocess, "call", fake_call)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "5"])
+    assert bench.spawn_ranks(bench.parse(["--gpus", "4", "--steps", "5"])) == 7
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
+    assert cmd[-4:] == ["--gpus", "4", "--steps", "5"]
+
+
+def test_world_size_mismatch_is_refused():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0
+    assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_cpu_threads_follow_the_host(monkeypatch):
+    monkeypatch.setenv("OMP_NUM_THREADS", "16")
+    assert bench.host_cores() == 16
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.host_cores() == len(os.sched_getaffinity(0))
+    assert bench.cpu_model() != ""
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_orbit_turns_about_the_look_at_point(cfg):
+    _, W, H, _, _, target = bench.WORKLOADS[cfg]
+    sc = rtamd.Scene().generate(cfg, 0, W / H)
+    c0 = sc.camera()
+    sc.orbit(target, 1.0)
+    c1 = sc.camera()
+    t = np.asarray(target, np.float64)
+    p0 = c0["Position"][0].astype(np.float64) - t
+    p1 = c1["Position"][0].astype(np.float64) - t
+    assert p1[1] == pytest.approx(p0[1])  # about the vertical axis
+    assert np.linalg.norm(p1) == pytest.approx(np.linalg.norm(p0), rel=1e-6)
+    turn = np.degrees(np.arctan2(p0[0], p0[2]) - np.arctan2(p1[0], p1[2]))
+    assert abs(abs(turn) - 1.0) < 1e-4
+    # rank r's camera still looks at the same point as rank 0's
+    for c, p in ((c0, p0), (c1, p1)):
+        f = c["Front"][0].astype(np.float64)
+        assert np.allclose(f, -p / np.linalg.norm(p), atol=1e-5)
+
+
+def test_roofline_fraction_is_physical():
+    info = {"record_bytes": 1_000_000}
+    r = bench.roofline(info, "k_accel", 0.3, 1920 * 1080, 8.5e11, {"bytes": 45e6, "source": "x"})
+    assert r["frac"] == pytest.approx(45e6 / 0.3e-3 / 1e9 / 8000)
+    assert r["frac"] < 1 and r["traffic"] == 45e6
+    assert r["reference_equivalent_GBps"] > 8000  # the skipped reference work is reported, not claimed
+    r2 = bench.roofline(info, "k_accel", 0.3, 1920 * 1080, 8.5e11, None)
+    assert r2["achieved"] == pytest.approx((16 * 1920 * 1080 + 1e6) / 0.3e-3 / 1e9)
+    assert r2["traffic"] is None

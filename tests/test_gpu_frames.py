@@ -1,0 +1,205 @@
+"""Whole-frame and multi-GPU-path parity on the GPU (-m gpu; needs an MI355X).
+
+* Full frames of configs 2, 3 and 5 at their BASELINE sizes against the
+  OpenMP oracle (not bands): every pixel within 1e-4 per channel.
+* Camera diversity on the production kernel: the weak bench mode's orbit
+  cameras, a camera inside the car's body, grazing views along the road,
+  and axis-aligned views whose centre rays have exactly-zero direction
+  components (the slab test's inf/NaN path, gpu_shader.comp:364-377).
+* Config 4 (3840x2160): oracle bands at the top, through the car and at the
+  bottom for the accelerated and the packet kernel; the 8-rank stripe set
+  reassembled by rt_group (copy transport on one GPU) equals the single
+  dispatch bit for bit; the 1-rank RCCL group (ncclCommInitRank + ncclGather)
+  equals it too.
+* tests/native/group_check: a C++ host that links librtamd.so through the C
+  ABI alone and checks every group case bit for bit (1080p-class and 4K).
+
+Tolerance 1e-4 per channel (BASELINE.json north_star); measured 0.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+import rtamd
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = rtamd.ComputeShader(0)
+    yield c
+    c.close()
+
+
+def check(img, ref, what):
+    diff = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    bad = int((diff > TOL).any(axis=-1).sum())
+    assert np.isfinite(img).all() == np.isfinite(ref).all(), what
+    assert bad == 0, f"{what}: {bad} pixels over {TOL}, max diff {np.nanmax(diff):.3g}"
+
+
+def render(ctx, fs, W, H, mb, kernel=rtamd.KERNEL_AUTO, y0=0, rows=None):
+    rows = H - y0 if rows is None else rows
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True, False, False)
+    ctx.set_kernel(kernel)
+    out = torch.full((rows, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows(W, H, y0, 1, 1, rows, out.data_ptr(), W * 16)
+    ctx.sync()
+    return out.cpu().numpy()
+
+
+# --------------------------------------------------------------------------
+# Full frames against the oracle
+
+@pytest.mark.parametrize("cfg,W,H,mb", [(2, 800, 600, 1), (3, 1920, 1080, 3), (5, 1920, 1080, 3)],
+                         ids=["config2_800x600", "config3_1920x1080", "config5_1920x1080"])
+def test_full_frame_vs_oracle(ctx, cfg, W, H, mb):
+    fs = rtamd.generate(cfg, 0, W, H)
+    img = render(ctx, fs, W, H, mb)
+    assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, mb))
+    check(img, ref, f"config {cfg} full frame")
+
+
+# --------------------------------------------------------------------------
+# Camera diversity (production kernel vs oracle, reduced size)
+
+def _camera_scene(cfg, W, H, pos=None, target=None, orbit=None, basis=None):
+    sc = rtamd.Scene().generate(cfg, 0, W / H)
+    if orbit is not None:
+        sc.orbit(orbit[0], orbit[1])
+    if pos is not None and target is not None:
+        sc.set_camera(pos, 60.0, W / H)
+        sc.LookAt(target)
+    fs = sc.serializeScene()
+    if basis is not None:
+        # an exact axis-aligned camera record (LookAt's trigonometry leaves ~1e-8 residues)
+        front, up, right = basis
+        fs.camera["Position"] = pos
+        fs.camera["Front"] = front
+        fs.camera["Up"] = up
+        fs.camera["Right"] = right
+    return fs
+
+
+CAMERAS = {
+    # weak-mode orbit frames (bench.py: rank r turns r degrees about the look-at point)
+    "orbit1_car": (3, dict(orbit=((0.0, 0.0, 0.0), 1.0))),
+    "orbit7_car": (3, dict(orbit=((0.0, 0.0, 0.0), 7.0))),
+    "orbit3_monkey": (2, dict(orbit=((0.0, 10.0, -8.0), 3.0))),
+    "orbit5_random": (5, dict(orbit=((0.0, 0.0, 0.0), 5.0))),
+    # inside the car body (ellipsoid about (0,-3.4,0)), looking along +x and back at the cabin
+    "inside_car": (3, dict(pos=(0.0, -3.4, 0.0), target=(10.0, -3.0, 1.0))),
+    "inside_car_up": (3, dict(pos=(1.0, -3.0, 0.5), target=(1.5, -9.0, 0.2))),
+    # grazing views along the road plane y = 0 (just above it: y is down)
+    "grazing_road": (3, dict(pos=(0.0, -0.05, 45.0), target=(0.0, -0.02, 0.0))),
+    "grazing_road_side": (3, dict(pos=(60.0, -0.2, 3.0), target=(-10.0, -0.1, -2.0))),
+    # axis-aligned: front exactly -z / -x, so the centre column/row rays have zero components
+    "axis_minus_z": (3, dict(pos=(0.0, -2.0, 40.0), basis=((0, 0, -1), (0, 1, 0), (1, 0, 0)))),
+    "axis_minus_x": (3, dict(pos=(60.0, -2.0, 0.0), basis=((-1, 0, 0), (0, 1, 0), (0, 0, -1)))),
+    "axis_random_cloud": (5, dict(pos=(0.0, 0.0, 60.0), basis=((0, 0, -1), (0, 1, 0), (1, 0, 0)))),
+    "axis_down_car": (3, dict(pos=(0.0, -30.0, 0.0), basis=((0, 1, 0), (0, 0, -1), (1, 0, 0)))),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CAMERAS))
+def test_camera_vs_oracle(ctx, name):
+    cfg, kw = CAMERAS[name]
+    W, H = 480, 270  # even: the centre column/row have NDC exactly 0
+    fs = _camera_scene(cfg, W, H, **kw)
+    mb = 3
+    img = render(ctx, fs, W, H, mb)
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, mb))
+    check(img, ref, name)
+    if name.startswith("axis"):
+        _, d = oracle.get_ray(fs.camera, 0.0, 0.0)
+        assert (d == 0).sum() == 2, d  # the centre ray runs along an axis: two zero components
+
+
+# --------------------------------------------------------------------------
+# Config 4: 3840x2160
+
+W4, H4 = 3840, 2160
+BANDS4 = {"top": (0, 16), "car": (1040, 24), "bottom": (2144, 16)}
+
+
+@pytest.fixture(scope="module")
+def car4k():
+    return rtamd.generate(3, 0, W4, H4)
+
+
+@pytest.mark.parametrize("kernel", [rtamd.KERNEL_ACCEL, rtamd.KERNEL_PACKET], ids=["accel", "packet"])
+@pytest.mark.parametrize("band", sorted(BANDS4))
+def test_config4_bands_vs_oracle(ctx, car4k, band, kernel):
+    y0, rows = BANDS4[band]
+    img = render(ctx, car4k, W4, H4, 3, kernel, y0, rows)
+    ref, _ = oracle.render(car4k, W4, H4, oracle.params(W4, H4, 3), y0=y0, out_rows=rows)
+    check(img, ref, f"4K {band}")
+    if band == "car":
+        assert (np.abs(img[..., :3] - img[:1, :1, :3]) > 0).any()  # the band really crosses the scene
+
+
+@pytest.fixture(scope="module")
+def frame4k(ctx, car4k):
+    return render(ctx, car4k, W4, H4, 3)
+
+
+@pytest.mark.parametrize("kernel", [rtamd.KERNEL_AUTO, rtamd.KERNEL_PACKET], ids=["auto", "packet"])
+def test_config4_group_of_8_reassembles(frame4k, car4k, kernel):
+    """The 8-GPU plan of config 4 (8-row stripes, rank r = stripes r, r+8, ...),
+    run as 8 group members on this GPU: the gathered frame is the single dispatch."""
+    g = rtamd.Group([0] * 8, rtamd.GATHER_COPY)
+    try:
+        assert (g.nranks, g.nlocal, g.transport) == (8, 8, rtamd.GATHER_COPY)
+        g.upload(car4k)
+        g.set_params(W4, H4, 3)
+        for m in g.members:
+            m.set_kernel(kernel)
+        for _ in range(2):
+            img = g.render(W4, H4, 8)
+            assert np.array_equal(img, frame4k)
+        with pytest.raises(rtamd.RTError):
+            g.read_image(W4, H4 - 8)  # a short destination is refused
+    finally:
+        g.close()
+
+
+def test_rccl_rank_group_equals_single_dispatch(ctx):
+    """rt_group_create_rank with one rank: ncclCommInitRank + ncclGather + unstripe."""
+    W, H = 640, 360
+    fs = rtamd.generate(3, 0, W, H)
+    ref = render(ctx, fs, W, H, 3)
+    g = rtamd.Group(uid=rtamd.group_unique_id(), nranks=1, rank=0, device=0)
+    try:
+        assert g.transport == rtamd.GATHER_RCCL
+        g.upload(fs)
+        g.set_params(W, H, 3)
+        for _ in range(3):
+            img = g.render(W, H, 8)
+            assert np.array_equal(img, ref)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("args", [["480", "270", "3"], ["800", "600", "2", "6"], ["3840", "2160", "3", "8"]],
+                         ids=["car_480x270", "monkey_800x600", "car_3840x2160_8ranks"])
+def test_native_group_host(args):
+    """C++ host through the C ABI only (tests/native/group_check.cpp)."""
+    exe = os.path.join(ROOT, "tests", "native", "build", "group_check")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "native")], check=True)
+    r = subprocess.run([exe] + args, capture_output=True, text=True, timeout=100)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "OK" in r.stdout.splitlines()[-1]
