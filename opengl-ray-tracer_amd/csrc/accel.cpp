@@ -87,8 +87,9 @@ struct LocalBuilder {
             Box3 bb[kBins];
             for (auto& x : bb) x = empty_box();
             auto bin_of = [&](const Item& it) {
-                int k = static_cast<int>((it.c[axis] - clo[axis]) / ext * kBins);
-                return std::min(kBins - 1, std::max(0, k));
+                const float f = (it.c[axis] - clo[axis]) / ext * kBins;
+                if (!(f >= 1.0f)) return 0;  // NaN never converts to int
+                return f >= static_cast<float>(kBins - 1) ? kBins - 1 : static_cast<int>(f);
             };
             for (int i = b; i < e; ++i) {
                 int k = bin_of(items[i]);
@@ -373,8 +374,10 @@ struct SceneBuilder {
         constexpr int kBins = kMaxBins;
         auto bin_of = [&](const Atom& it, int ax) {
             const float ext = chi[ax] - clo[ax];
-            int k = static_cast<int>((it.c[ax] - clo[ax]) / ext * kBins);
-            return std::min(kBins - 1, std::max(0, k));
+            const float f = (it.c[ax] - clo[ax]) / ext * kBins;
+            // non-finite centres (inf - inf, x / inf) go to bin 0; never convert NaN to int
+            if (!(f >= 1.0f)) return 0;
+            return f >= static_cast<float>(kBins - 1) ? kBins - 1 : static_cast<int>(f);
         };
         float best = INFINITY;
         int best_k = -1, best_axis = -1;
