@@ -12,7 +12,7 @@
  *   FlatNode      48 B   src/flatStructures.hpp:94-106 ≡ gpu_shader.comp:74-86
  *
  * Every size and field offset is pinned by static assertions below and, in
- * tests/test_oracle_golden.py (test_layout_matches_reference), against the offsets printed by the reference header
+ * tests/test_oracle_golden.py (test_layout_matches_reference_header), against the offsets printed by the reference header
  * itself (compiled from /root/reference by oracle/Makefile, fixture
  * tests/golden/ref_layout.json).
  *
