@@ -104,6 +104,8 @@ struct KParams {
     int tail_rx, tail_regions;               // 64x64-pixel regions: per row, total (one counter each)
     int tail_counters;                       // counters per set (>= tail_regions; all zeroed for the next)
     int tail_max_lanes;                      // a wave queues its rays only if at most this many are alive
+    float shadow_off;                        // k_accel's shadow-ray offset: 1e-3 (BVH branch, gpu_shader.comp:469);
+                                             // 1e-5 when it renders the brute branch (:565, rt_ctx::brute)
 };
 
 // Row mapping of rt_dispatch_rows (include/rt_api.h).

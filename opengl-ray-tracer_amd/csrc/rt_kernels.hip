@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <new>
 #include <vector>
 
@@ -1234,7 +1235,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     float ld = 0.f;
     if (alive) {
         const V hn = shape_normal(load_rec(A.prims, best.slot), best.p);
-        sr = Ray{best.p + hn * 1e-3f, normalize(kp.light_pos - best.p)};
+        sr = Ray{best.p + hn * kp.shadow_off, normalize(kp.light_pos - best.p)};
         ld = dist(kp.light_pos, best.p);
     }
     bool shadow = false;
@@ -1835,6 +1836,16 @@ struct rt_ctx {
     int n_dirty = 0;
     int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
+    // The brute-force branch (useBVH = 0, gpu_shader.comp:523-620) tests every shape in
+    // index order, keeps the strict-< first minimum and stops shadows at the first
+    // occluder: exactly the BVH branch walking a tree of ONE leaf that lists shapes
+    // 0..S-1 in order under an infinite box (which every ray with a non-NaN slab passes,
+    // and for which a NaN ray gets no hit in either branch), except for the shadow
+    // offset, 1e-5 instead of 1e-3 (:565 vs :469). `brute` is that second context: the
+    // same shapes over the one-leaf tree, with its own accelerator, on this stream.
+    rt_ctx* brute = nullptr;
+    bool brute_stale = true;            // shapes changed since brute's upload
+    int brute_accel = 1;                // rt_set_brute_accel
 };
 
 namespace {
@@ -2332,6 +2343,94 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step,
     kp.out_rows = out_rows;
     kp.dst = reinterpret_cast<char*>(dst);
     kp.pitch = pitch;
+    kp.shadow_off = 1e-3f;
+    return RT_OK;
+}
+
+bool accel_usable(const rt_ctx* c, const KParams& kp) {
+    const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
+    return c->accel_ok && kp.useBVH && !kp.useMT && cmag <= c->accel.origin_lim;
+}
+
+int launch(rt_ctx* c, const KParams& kp, bool stats);
+
+// The brute branch through `brute` (rt_ctx::brute): the same shapes under one
+// leaf listing 0..S-1 with an infinite box, built on first use after the
+// shapes change. nullptr: render the branch literally (k_packet).
+rt_ctx* brute_ctx(rt_ctx* c, const KParams& kp) {
+    if (!c->brute_accel || kp.useBVH || kp.useMT || !c->anim_ids.empty() || c->S <= 0 ||
+        (c->kernel != RT_KERNEL_AUTO && c->kernel != RT_KERNEL_ACCEL))
+        return nullptr;
+    if (!c->brute) {
+        if (rt_create(&c->brute, c->device) != RT_OK) return nullptr;
+        hipStreamDestroy(c->brute->stream);
+        c->brute->stream = c->stream;
+        c->brute->own_stream = false;
+        c->brute_stale = true;
+    }
+    rt_ctx* b = c->brute;
+    if (c->brute_stale) {
+        FlatNode leaf;
+        std::memset(&leaf, 0, sizeof leaf);
+        const float inf = std::numeric_limits<float>::infinity();
+        leaf.boundsMin = rt_vec3{-inf, -inf, -inf};
+        leaf.boundsMax = rt_vec3{inf, inf, inf};
+        leaf.leftChild = leaf.rightChild = -1;
+        leaf.startShapeIdx = 0;
+        leaf.numShapes = c->S;
+        std::vector<int> order(c->S);
+        for (int i = 0; i < c->S; ++i) order[i] = i;
+        if (rt_upload_scene(b, c->host_shapes.data(), c->S, &leaf, 1, order.data(), c->S) != RT_OK) return nullptr;
+        c->brute_stale = false;
+    }
+    b->cam = c->cam;
+    b->light = c->light;
+    b->have_cam = b->have_light = true;
+    b->params = c->params;
+    b->params.useBVH = 1;
+    b->kernel = RT_KERNEL_ACCEL;
+    b->waves_per_block = c->waves_per_block;
+    b->persistent = c->persistent;
+    b->lane_from_depth = c->lane_from_depth;
+    b->cone_cull = c->cone_cull;
+    b->spec_mode = c->spec_mode;
+    b->schedule = c->schedule;
+    b->sched_period = c->sched_period;
+    b->tail_from = c->tail_from;
+    b->tail_max_lanes = c->tail_max_lanes;
+    b->shadow_walk_override = c->shadow_walk_override;
+    b->tree_mode = c->tree_mode;
+    b->scene_stack = c->scene_stack;
+    b->lane_stack_override = c->lane_stack_override;
+    const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
+    return b->accel_ok && cmag <= b->accel.origin_lim ? b : nullptr;
+}
+
+// rt_dispatch_rows' render: the brute branch on `brute` when it applies, timed
+// by this context's events (rt_kernel_times) like any other dispatch.
+int render(rt_ctx* c, const KParams& kp) {
+    rt_ctx* b = brute_ctx(c, kp);
+    if (!b) return launch(c, kp, false);
+    KParams kb;
+    int rc = fill_kparams(b, kp.width, kp.height, kp.y0, kp.stripe, kp.step, kp.out_rows,
+                          reinterpret_cast<float*>(kp.dst), kp.pitch, kb);
+    if (rc != RT_OK) return rc;
+    kb.shadow_off = 1e-5f;  // gpu_shader.comp:565
+    hipEvent_t e0 = c->ev0, e1 = c->ev1;
+    if (c->ring_used < static_cast<int>(c->ring0.size())) {
+        e0 = c->ring0[c->ring_used];
+        e1 = c->ring1[c->ring_used];
+    }
+    HIP_TRY(hipEventRecord(e0, c->stream));
+    rc = launch(b, kb, false);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(hipEventRecord(e1, c->stream));
+    c->last0 = e0;
+    c->last1 = e1;
+    if (c->ring_used < static_cast<int>(c->ring0.size())) ++c->ring_used;
+    c->timed = true;
+    c->last_kind = b->last_kind;
+    b->ring_used = 0;  // its own records are not read
     return RT_OK;
 }
 
@@ -2340,10 +2439,9 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     dim3 grid((kp.width + kTileW - 1) / kTileW, (kp.out_rows + kTileH - 1) / kTileH);
     if (grid.y > 65535u) return RT_ERR_INVALID;
     int kind = c->kernel;
-    const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
-    const bool accel_usable = c->accel_ok && kp.useBVH && !kp.useMT && cmag <= c->accel.origin_lim;
-    if (kind == RT_KERNEL_AUTO) kind = accel_usable ? RT_KERNEL_ACCEL : RT_KERNEL_PACKET;
-    if (kind == RT_KERNEL_ACCEL && !accel_usable) kind = RT_KERNEL_PACKET;  // same image either way
+    const bool usable = accel_usable(c, kp);
+    if (kind == RT_KERNEL_AUTO) kind = usable ? RT_KERNEL_ACCEL : RT_KERNEL_PACKET;
+    if (kind == RT_KERNEL_ACCEL && !usable) kind = RT_KERNEL_PACKET;  // same image either way
     const size_t lds = static_cast<size_t>(kp.max_stack) * kBlock * sizeof(int);
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (!stats && c->ring_used < static_cast<int>(c->ring0.size())) {
@@ -2576,6 +2674,8 @@ int rt_destroy(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->brute) rt_destroy(c->brute);  // it runs on this context's stream
+    c->brute = nullptr;
     free_scene(c);
     hipFree(c->staging_shapes);
     hipFree(c->staging_nodes);
@@ -2615,6 +2715,10 @@ int rt_set_stream(rt_ctx* c, void* s) {
     } else {
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
+    }
+    if (c->brute) {  // the brute-branch context runs on this context's stream (synchronised above)
+        c->brute->stream = c->stream;
+        c->brute->own_stream = false;
     }
     return RT_OK;
 }
@@ -2661,6 +2765,7 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->have_scene = true;
     c->nodes_on_device_newer = false;
     c->anim_ids.clear();  // ids refer to the previous scene
+    c->brute_stale = true;
     return upload_accel(c);
 }
 
@@ -2678,6 +2783,7 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));  // glBufferSubData semantics: the host array may be reused
     std::copy(shapes, shapes + count, c->host_shapes.begin() + first);
+    c->brute_stale = true;
     return upload_accel(c);  // moved shapes change the conservative bounds
 }
 
@@ -2780,6 +2886,7 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
                            c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr);
     HIP_TRY(hipGetLastError());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
+    c->brute_stale = true;
     c->nodes_on_device_newer = true;
     c->st_root = kNoChild;  // the scene tree's bounds are not refit: stale until the next build
     if (!rebuild) return RT_OK;
@@ -2876,7 +2983,7 @@ int rt_dispatch_rows(rt_ctx* c, int width, int height, int y0, int stripe, int s
     int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, dst, pitch, kp);
     if (rc != RT_OK) return rc;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    return launch(c, kp, false);
+    return render(c, kp);
 }
 
 int rt_dispatch(rt_ctx* c, int width, int height, int y0, int y1) {

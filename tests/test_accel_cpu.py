@@ -332,3 +332,35 @@ def test_scene_tree_off_when_boxes_do_not_nest(check_lib):
     o, d = np.concatenate([o, o2]), np.concatenate([d, d2])
     info = compare(check_lib, fs2, o, d, rng.uniform(1, 80, len(o)), 1)
     assert info[11] == 0 and info[9] == 0 and info[10] == 0
+
+
+def one_leaf(fs):
+    """The brute-force branch's tree (rt_ctx::brute): one leaf listing shapes 0..S-1
+    in order under an infinite box, so the reference walk IS the brute scan
+    (gpu_shader.comp:535-552: every shape, index order, strict-< first minimum)."""
+    nodes = np.zeros(1, rtamd.NODE_DTYPE)
+    nodes["boundsMin"], nodes["boundsMax"] = -np.inf, np.inf
+    nodes["leftChild"] = nodes["rightChild"] = -1
+    nodes["numShapes"] = len(fs.shapes)
+    return rtamd.FlatScene(fs.shapes, nodes, np.arange(len(fs.shapes), dtype=np.int32), fs.camera, fs.light)
+
+
+@pytest.mark.parametrize("src", ["car", "monkey", "soup1", "soup2"])
+def test_accel_brute_branch_tree(check_lib, src):
+    """The accelerator over the brute branch's one-leaf tree picks the brute
+    scan's shape for every ray (camera, random and axis-aligned rays)."""
+    if src.startswith("soup"):
+        import test_gpu_parity as tg
+        fs = tg._soup(int(src[-1]))
+    else:
+        fs = rtamd.generate(3 if src == "car" else 2, 0, 96, 54)
+    fs1 = one_leaf(fs)
+    rng = np.random.default_rng(len(src))
+    o, d = camera_rays(fs1, 64, 36)
+    o2, d2 = random_rays(rng, 4000)
+    d3 = np.zeros((500, 3))
+    d3[np.arange(500), rng.integers(0, 3, 500)] = rng.choice([-1.0, 1.0], 500)
+    o3 = rng.uniform(-20, 20, (500, 3))
+    O, D = np.concatenate([o, o2, o3]), np.concatenate([d, d2, d3])
+    info = compare(check_lib, fs1, O, D, rng.uniform(1, 80, len(O)))
+    assert info[9] == 1  # the one-leaf tree nests trivially: rays take the scene tree

@@ -203,3 +203,60 @@ def test_native_group_host(args):
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "OK" in r.stdout.splitlines()[-1]
+
+
+# --------------------------------------------------------------------------
+# The brute-force branch (useBVH = 0, gpu_shader.comp:523-620) on the accelerator
+
+def render_p(ctx, fs, W, H, mb, bvh, kernel, y0=0, rows=None, fresnel=False):
+    rows = H - y0 if rows is None else rows
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, bvh, fresnel, False)
+    ctx.set_kernel(kernel)
+    out = torch.full((rows, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows(W, H, y0, 1, 1, rows, out.data_ptr(), W * 16)
+    ctx.sync()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("cfg,W,H,mb,fresnel", [(2, 800, 600, 1, False), (2, 400, 300, 4, True),
+                                                (3, 1920, 1080, 3, False), (5, 240, 136, 3, False)],
+                         ids=["config2", "config2_fresnel_b4", "config3_1080p", "config5_240x136"])
+def test_brute_branch_accelerated_equals_scan(ctx, cfg, W, H, mb, fresnel):
+    """useBVH = 0 through the accelerated one-leaf context equals the literal
+    brute scan (k_packet) bit for bit, frame after frame."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    scan = render_p(ctx, fs, W, H, mb, False, rtamd.KERNEL_PACKET, fresnel=fresnel)
+    assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_PACKET
+    ctx.kernel_times()
+    for _ in range(2):
+        fast = render_p(ctx, fs, W, H, mb, False, rtamd.KERNEL_AUTO, fresnel=fresnel)
+        assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL
+        assert np.array_equal(fast, scan)
+    assert len(ctx.kernel_times()) == 2  # timed on the context's own events
+
+
+def test_brute_branch_vs_oracle_band(ctx):
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    img = render_p(ctx, fs, W, H, 3, False, rtamd.KERNEL_AUTO, 520, 16)
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, False), y0=520, out_rows=16)
+    check(img, ref, "brute band")
+
+
+def test_brute_branch_follows_shape_updates(ctx):
+    """rt_update_shapes rebuilds the brute context's copy before the next brute frame."""
+    W, H = 320, 180
+    fs = rtamd.generate(3, 0, W, H)
+    render_p(ctx, fs, W, H, 3, False, rtamd.KERNEL_AUTO)
+    moved = fs.shapes[-100:].copy()
+    moved["sphereCenter"] += np.float32(2.5)
+    ctx.update_shapes(len(fs.shapes) - 100, moved)
+    out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+    ctx.sync()
+    fs2 = rtamd.FlatScene(np.concatenate([fs.shapes[:-100], moved]), fs.nodes, fs.indices, fs.camera, fs.light)
+    ref, _ = oracle.render(fs2, W, H, oracle.params(W, H, 3, False))
+    check(out.cpu().numpy(), ref, "brute after update_shapes")
