@@ -76,6 +76,9 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=0, help="car road: 0 = 2-triangle quad, 1 = 222 strips")
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "packet", "accel"])
     ap.add_argument("--stripe", type=int, default=8)
+    ap.add_argument("--brute", action="store_true", help="useBVH = 0: the brute-force branch (gpu_shader.comp:523-620)")
+    ap.add_argument("--mt", action="store_true", help="useMollerTrumbore = 1 (gpu_shader.comp:170-195)")
+    ap.add_argument("--fresnel", action="store_true", help="useFresnel = 1 (gpu_shader.comp:500-509)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU; 0 = auto: 2, or up to 4 while the GPU's share of a frame "
                          "has fewer than 16k 8x8 tiles (too few waves to fill it)")
@@ -121,13 +124,13 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(rtamd, fs, W, H, mb, seconds, threads):
+def cpu_baseline(rtamd, fs, W, H, mb, seconds, threads, toggles=(True, False, False)):
     """The oracle (oracle/rt_oracle.c, the GLSL restated, OpenMP) on a band of
     rows through the middle of the same frame; the band grows until the
     measurement takes roughly `seconds`."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (cpu_baseline leg only)
-    p = oracle.params(W, H, mb)
+    p = oracle.params(W, H, mb, *toggles)
     rows = 8
     while True:
         y0 = max(0, H // 2 - rows // 2)
@@ -269,7 +272,7 @@ def main():
             dist.broadcast_object_list(uid, src=0)
             g = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local)
             g.upload(fs)
-            g.set_params(W, H, mb, True, False, False)
+            g.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             g.members[0].set_kernel(kernel_id)
             groups.append(g)
             ctxs.append(g.members[0])
@@ -279,7 +282,7 @@ def main():
             c_ = rtamd.ComputeShader(torch.cuda.current_device())
             c_.set_stream(s_.cuda_stream)
             c_.upload(fs)
-            c_.set_params(W, H, mb, True, False, False)
+            c_.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             c_.set_kernel(kernel_id)
             ctxs.append(c_)
             bufs.append(torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev))
@@ -287,7 +290,8 @@ def main():
 
     # Work of this rank's rows on the reference walk (counting kernel, untimed).
     st = ctx.collect_stats(W, H, plan.y0(prank), a.stripe, plan.world, rows)
-    mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, rows * W), st["hits"]],
+    mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, rows * W, a.mt),
+                         st["hits"]],
                         dtype=torch.float64, device="cpu" if gloo else dev)
     total = mine.clone()
     if world > 1:
@@ -354,7 +358,8 @@ def main():
         if strong:
             gather = ("rt_group: ncclGather to rank 0 (RCCL over xGMI) + k_unstripe, C ABI (include/rt_group.h)"
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
-        pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}") if not strong or world == 1 else None
+        toggles = (a.brute, a.mt, a.fresnel, a.variant)
+        pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}") if not any(toggles) and not strong else None
         out = {
             "metric": METRIC,
             "value": rays_step * a.steps / elapsed / 1e6,
@@ -374,8 +379,8 @@ def main():
             "mode": mode,
             "ranks_seen": world,
             "config": {"workload": f"config {a.config}: {desc}" + (" (222-strip road)" if a.variant else ""),
-                       "width": W, "height": H, "maxBounces": mb, "useBVH": 1, "useFresnel": 0,
-                       "triangle_test": "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
+                       "width": W, "height": H, "maxBounces": mb, "useBVH": int(not a.brute),
+                       "useFresnel": int(a.fresnel), "triangle_test": "moller-trumbore" if a.mt else "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
                        "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel,
                        "parallelism": (f"row-stripes{a.stripe}x{world}+gather" if strong else
                                        f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"
@@ -393,7 +398,8 @@ def main():
         }
         if world == 1 and not a.no_cpu:
             thr = a.cpu_threads or host_cores()
-            out["cpu_baseline"] = cpu_baseline(rtamd, fs, W, H, mb, a.cpu_seconds, thr)
+            out["cpu_baseline"] = cpu_baseline(rtamd, fs, W, H, mb, a.cpu_seconds, thr,
+                                               (not a.brute, a.fresnel, a.mt))
             out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2)
         print(json.dumps(out), flush=True)
     for g in groups:

@@ -1824,11 +1824,16 @@ struct rt_ctx {
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
     size_t anim_maps_cap = 0;
     AnimMaps anim{};
-    void* anim_pinned = nullptr;        // per-frame upload: FlatShape[count] then int flags[count]
-    size_t anim_pinned_cap = 0;
-    char* anim_frame = nullptr;         // its device copy
+    // Per-frame upload, FlatShape[count] then int flags[count]: a ring of pinned host
+    // buffers, so rt_animate waits only for the copy kAnimRing frames back (not for the
+    // previous frame's render, which the previous copy is stream-ordered behind).
+    static constexpr int kAnimRing = 3;
+    void* anim_pinned[kAnimRing] = {nullptr, nullptr, nullptr};
+    size_t anim_pinned_cap[kAnimRing] = {0, 0, 0};
+    hipEvent_t anim_copied[kAnimRing] = {nullptr, nullptr, nullptr};  // that slot's upload has completed
+    int anim_slot = 0;
+    char* anim_frame = nullptr;         // the device copy (stream-ordered reuse)
     size_t anim_frame_cap = 0;
-    hipEvent_t anim_copied = nullptr;   // the last upload from anim_pinned has completed
     float4* anim_sbox = nullptr;        // per animated shape boxes (AnimOut::sbox)
     size_t anim_sbox_cap = 0;
     float4* pbox = nullptr;             // per prim conservative box (AnimOut::pbox)
@@ -2693,8 +2698,10 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->anim_maps);
     hipFree(c->anim_frame);
     hipFree(c->anim_sbox);
-    if (c->anim_pinned) hipHostFree(c->anim_pinned);
-    if (c->anim_copied) hipEventDestroy(c->anim_copied);
+    for (int k = 0; k < rt_ctx::kAnimRing; ++k) {
+        if (c->anim_pinned[k]) hipHostFree(c->anim_pinned[k]);
+        if (c->anim_copied[k]) hipEventDestroy(c->anim_copied[k]);
+    }
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
     if (c->ev0) hipEventDestroy(c->ev0);
@@ -2848,25 +2855,27 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
         flags[i] = (cls == rta::BOUNDED ? AF_BOUNDED : 0) | (cone ? AF_CONE : 0);
     }
     const size_t bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
-    if (!c->anim_copied) {
-        HIP_TRY(hipEventCreateWithFlags(&c->anim_copied, hipEventDisableTiming));
+    const int slot = c->anim_slot;
+    c->anim_slot = (slot + 1) % rt_ctx::kAnimRing;
+    if (!c->anim_copied[slot]) {
+        HIP_TRY(hipEventCreateWithFlags(&c->anim_copied[slot], hipEventDisableTiming));
     } else {
-        HIP_TRY(hipEventSynchronize(c->anim_copied));  // the last upload has left the pinned buffer
+        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // this slot's last upload has left it
     }
-    if (c->anim_pinned_cap < bytes) {
-        if (c->anim_pinned) hipHostFree(c->anim_pinned);
-        c->anim_pinned = nullptr;
-        c->anim_pinned_cap = 0;
-        if (hipHostMalloc(&c->anim_pinned, bytes) != hipSuccess) return RT_ERR_NO_MEMORY;
-        c->anim_pinned_cap = bytes;
+    if (c->anim_pinned_cap[slot] < bytes) {
+        if (c->anim_pinned[slot]) hipHostFree(c->anim_pinned[slot]);
+        c->anim_pinned[slot] = nullptr;
+        c->anim_pinned_cap[slot] = 0;
+        if (hipHostMalloc(&c->anim_pinned[slot], bytes) != hipSuccess) return RT_ERR_NO_MEMORY;
+        c->anim_pinned_cap[slot] = bytes;
     }
     int rc = ensure_staging(c->anim_frame, c->anim_frame_cap, bytes);
     if (rc != RT_OK) return rc;
-    char* pin = static_cast<char*>(c->anim_pinned);
+    char* pin = static_cast<char*>(c->anim_pinned[slot]);
     std::memcpy(pin, shapes, n * sizeof(FlatShape));
     std::memcpy(pin + n * sizeof(FlatShape), flags.data(), n * sizeof(int));
     HIP_TRY(hipMemcpyAsync(c->anim_frame, pin, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipEventRecord(c->anim_copied, c->stream));
+    HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));
     const bool acc = c->accel_ok;
     const size_t P = c->accel.prim_shape.size();
     const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat,
