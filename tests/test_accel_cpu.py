@@ -364,3 +364,34 @@ def test_accel_brute_branch_tree(check_lib, src):
     O, D = np.concatenate([o, o2, o3]), np.concatenate([d, d2, d3])
     info = compare(check_lib, fs1, O, D, rng.uniform(1, 80, len(O)))
     assert info[9] == 1  # the one-leaf tree nests trivially: rays take the scene tree
+
+
+def test_mt_hits_stray_beyond_barycentric_padding():
+    """Why Moller-Trumbore frames are not accelerated with the barycentric
+    bounds: the reference's MT test (gpu_shader.comp:170-195) accepts a hit when
+    |a| >= 1e-5 (an absolute threshold), and on grazing rays from afar its u, v
+    and t carry errors of order u * |s| * |e1||e2| / |a|, so an accepted hit
+    point can lie a triangle-size away from the triangle. The barycentric test
+    checks its own hit point and never strays like that. Pinned here on the
+    car's triangles with origins inside the accelerator's origin bound: a
+    conservative box for MT would need that stray as padding."""
+    fs = rtamd.generate(3, 0, 96, 54)
+    rng = np.random.default_rng(0)
+    idx = np.where(fs.shapes["type"] == 3)[0]
+    worst = 0.0
+    for _ in range(20000):
+        tri = fs.shapes[idx[rng.integers(len(idx))]]
+        p1, p2, p3 = [tri[k].astype(np.float64) for k in ("triP1", "triP2", "triP3")]
+        n = np.cross(p2 - p1, p3 - p1)
+        n /= np.linalg.norm(n)
+        lo, hi = np.minimum(np.minimum(p1, p2), p3), np.maximum(np.maximum(p1, p2), p3)
+        x = rng.dirichlet([1, 1, 1]) @ np.stack([p1, p2, p3])
+        t = np.cross(n, rng.normal(size=3))
+        d = t / np.linalg.norm(t) + rng.choice([1, -1]) * 10 ** rng.uniform(-5, -3) * n
+        d /= np.linalg.norm(d)
+        o = (x - d * rng.uniform(100, 220)).astype(np.float32)
+        kind, hit = oracle.intersect(tri, o, d.astype(np.float32), use_mt=True)
+        if kind == 1:  # INNER
+            worst = max(worst, float(np.maximum(0, np.maximum(lo - hit, hit - hi)).max()))
+    extent = 0.6  # the car's triangles are about half a unit across
+    assert worst > 0.1 * extent, worst  # far beyond the 1e-3 * (size + magnitude) padding of the bounds
