@@ -180,7 +180,86 @@ Cone merge(const Cone& x, const Cone& y) {
 
 }  // namespace
 
+// Moller-Trumbore: the unit normal of e1 x e2 (edges as the device computes
+// them, float), either orientation (|cos| decides); `none` for other shapes.
+bool mt_normal(const FlatShape& s, double n[3]) {
+    if (s.type != RT_TRIANGLE) return false;
+    const float e1[3] = {s.triP2.x - s.triP1.x, s.triP2.y - s.triP1.y, s.triP2.z - s.triP1.z};
+    const float e2[3] = {s.triP3.x - s.triP1.x, s.triP3.y - s.triP1.y, s.triP3.z - s.triP1.z};
+    const double c[3] = {static_cast<double>(e1[1]) * e2[2] - static_cast<double>(e1[2]) * e2[1],
+                         static_cast<double>(e1[2]) * e2[0] - static_cast<double>(e1[0]) * e2[2],
+                         static_cast<double>(e1[0]) * e2[1] - static_cast<double>(e1[1]) * e2[0]};
+    const double l = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    if (!(l > 0) || !std::isfinite(l)) return false;
+    for (int i = 0; i < 3; ++i) n[i] = c[i] / l;
+    return true;
+}
+
+// Grazing cones (AccelHost::mt): per node the axis and half angle of the
+// triangle normals below, orientation-free (each normal is flipped towards the
+// running axis before merging).
+struct GCone {
+    double a[3] = {0, 0, 0};
+    double theta = -1;  // < 0: no triangle below
+};
+
+GCone gmerge(const GCone& x, const GCone& y) {
+    if (x.theta < 0) return y;
+    if (y.theta < 0) return x;
+    if (x.theta >= 1.5 || y.theta >= 1.5) return GCone{{0, 0, 0}, 10.0};
+    double ya[3] = {y.a[0], y.a[1], y.a[2]};
+    if (x.a[0] * ya[0] + x.a[1] * ya[1] + x.a[2] * ya[2] < 0)
+        for (double& v : ya) v = -v;
+    double a[3] = {x.a[0] + ya[0], x.a[1] + ya[1], x.a[2] + ya[2]};
+    double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    if (!(l > 1e-6)) return GCone{{0, 0, 0}, 10.0};
+    for (double& v : a) v /= l;
+    auto ang = [&](const double* b) {
+        double c = a[0] * b[0] + a[1] * b[1] + a[2] * b[2];
+        return std::acos(std::max(-1.0, std::min(1.0, c)));
+    };
+    return GCone{{a[0], a[1], a[2]}, std::max(ang(x.a) + x.theta, ang(ya) + y.theta)};
+}
+
+void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
+    const size_t M = A.lbox.size();
+    A.lcone.assign(4 * M, 0.f);
+    std::vector<GCone> cones(M);
+    std::vector<char> done(M, 0);
+    std::function<const GCone&(size_t)> get = [&](size_t j) -> const GCone& {
+        if (done[j]) return cones[j];
+        GCone c;
+        if (A.la[j] < 0) {
+            const int st = -A.la[j] - 1, n = A.lb[j];
+            for (int i = 0; i < n; ++i) {
+                GCone one;
+                if (mt_normal(shapes[A.prim_shape[st + i]], one.a)) one.theta = 0.0;
+                c = gmerge(c, one);
+            }
+        } else {
+            c = gmerge(get(static_cast<size_t>(A.la[j])), get(static_cast<size_t>(A.lb[j] & 0x3fffffff)));
+        }
+        cones[j] = c;
+        done[j] = 1;
+        return cones[j];
+    };
+    const double psi = std::asin(kMtCos);
+    for (size_t j = 0; j < M; ++j) {
+        const GCone& c = get(j);
+        float* o = &A.lcone[4 * j];
+        const double t = c.theta + psi + kConeMargin;
+        o[0] = static_cast<float>(c.a[0]);
+        o[1] = static_cast<float>(c.a[1]);
+        o[2] = static_cast<float>(c.a[2]);
+        o[3] = c.theta < 0 ? -1.f : (t >= 1.5707 ? 2.f : static_cast<float>(std::sin(t)));
+    }
+}
+
 void build_cones(const FlatShape* shapes, AccelHost& A) {
+    if (A.mt) {
+        build_cones_mt(shapes, A);
+        return;
+    }
     const size_t M = A.lbox.size();
     A.lcone.assign(4 * M, 0.f);
     std::vector<Cone> cones(M, full_cone());
@@ -470,6 +549,7 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
     }
     st.nested = 1;
     AccelHost T;
+    T.mt = out.mt;  // the scene tree's cones follow the accelerator's triangle test
     SceneBuilder sb{T, {}, {}, {}, kSceneHeight, 0};
     std::vector<Atom> unb;
     const Box3 inf_box{{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}};
@@ -601,9 +681,10 @@ static int build_wide(AccelHost& A, const std::vector<int>& ref_depth, int cap) 
 }
 
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
-                 int leaf_threshold, int stack_cap, AccelHost& out) {
+                 int leaf_threshold, int stack_cap, AccelHost& out, bool mt) {
     (void)I;
     out = AccelHost();
+    out.mt = mt;
     out.content.assign(N, empty_box());
     out.flags.assign(N, 0);
     out.plain_start.assign(N, 0);
@@ -614,13 +695,13 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     std::vector<Box3> sbox(S);
     std::vector<int> scls(S);
     for (int i = 0; i < S; ++i) {
-        scls[i] = classify(shapes[i], sbox[i], 0.0);
+        scls[i] = classify(shapes[i], sbox[i], 0.0, mt);
         if (scls[i] == BOUNDED)
             for (int a = 0; a < 3; ++a)
                 out.scene_mag = std::max({out.scene_mag, std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
     }
-    out.origin_lim = static_cast<float>(kOriginRel * (out.scene_mag + 1.0));
-    for (int i = 0; i < S; ++i) scls[i] = classify(shapes[i], sbox[i], out.origin_lim);
+    out.origin_lim = static_cast<float>((mt ? kOriginRelMt : kOriginRel) * (out.scene_mag + 1.0));
+    for (int i = 0; i < S; ++i) scls[i] = classify(shapes[i], sbox[i], out.origin_lim, mt);
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).
@@ -671,7 +752,7 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
             bounded.push_back(it);
         }
         out.content[k] = content;
-        out.flags[k] = unb ? 0 : 8;
+        out.flags[k] = (unb || mt) ? 0 : 8;  // MT boxes hold for non-grazing rays only: no content culling
         if (static_cast<int>(bounded.size()) <= leaf_threshold) {
             for (const Item& it : bounded) plain.push_back({it.shape, it.seq});
             std::sort(plain.begin(), plain.end(), [](auto& a, auto& b) { return a.second < b.second; });

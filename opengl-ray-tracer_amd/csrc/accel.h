@@ -93,14 +93,21 @@ struct AccelHost {
     // its cones are in st_cone (4 per binary node, as lcone).
     SceneTree st;
     std::vector<float> st_cone;
+    // Built for the Moller-Trumbore triangle test (build_accel mt): triangle boxes
+    // from classify_mt_triangle, no back-face culling, and the cones of lcone /
+    // st_cone are GRAZING cones: a ray with |dot(axis, d/|d|)| < thr might meet a
+    // triangle below at |cos| < kMtCos, where its box does not hold, so the walk
+    // enters the subtree whatever its box says (thr = -1: no triangle below, 2:
+    // any ray). Reference-node content boxes are not used (flags bit 3 clear).
+    bool mt = false;
 };
 
 // Builds the accelerator for a validated reference tree (see check_tree).
 // leaf_threshold: leaves with more shapes than this get a local BVH.
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
-                 int leaf_threshold, int stack_cap, AccelHost& out);
+                 int leaf_threshold, int stack_cap, AccelHost& out, bool mt = false);
 
-// Back-face cones of the local nodes (fills A.lcone).
+// Back-face cones of the local nodes (fills A.lcone; grazing cones when A.mt).
 void build_cones(const FlatShape* shapes, AccelHost& A);
 
 constexpr int kWide = 4;

@@ -44,6 +44,22 @@ constexpr double kCosRef = 0.5;      // below it the padding scales with 1/cos
 constexpr double kSphereErr = 4e-6;  // k of the sphere-root error above, with room
 constexpr double kOriginRel = 4.0;   // origin_lim = kOriginRel * (scene magnitude + 1)
 constexpr double kOriginErr = 4e-6;  // padding per unit of origin_lim (origin-relative error above)
+// Moller-Trumbore bounds (classify with mt): they hold for rays whose direction
+// makes |cos| >= kMtCos with the triangle's normal; the walk enters every
+// subtree holding a triangle such a ray might graze (accel.h, the MT cones).
+#ifndef RTA_MT_COS
+#define RTA_MT_COS 0.02
+#endif
+#ifndef RTA_MT_ORIGIN_REL
+#define RTA_MT_ORIGIN_REL 1.5
+#endif
+constexpr double kMtCos = RTA_MT_COS;
+constexpr double kMtSafety = 2.0;
+// Origin bound of an MT accelerator (in place of kOriginRel): the error of the
+// MT hit point grows with |o - p1|; rays from farther take the always-enter
+// mode and a camera beyond it renders the frame on k_packet.
+constexpr double kOriginRelMt = RTA_MT_ORIGIN_REL;
+constexpr double kU = 5.9604644775390625e-08;  // 2^-24
 
 enum { UNBOUNDED = 0, BOUNDED = 1, NEVER = 2 };
 
@@ -106,11 +122,58 @@ RTA_HD Box3 finish(const BoxAcc& acc, double origin_lim, double amp = 1.0) {
     return acc.padded(amp * (kPadRel * (acc.extent() + acc.mag() + 1.0) + kOriginErr * origin_lim) + 1e-6);
 }
 
+// The Moller-Trumbore test (gpu_shader.comp:170-195) accepts a hit when
+// |a| = |e1 . (d x e2)| >= 1e-5, an absolute threshold, and reports o + t d with
+// t, u, v each computed through f = 1/a. With |d| in [0.5, 2] (the padded
+// walk's range, accel_math.h), |o_i| <= L = origin_lim, s = o - p1 and
+// u = 2^-24 (first-order float error bounds of the dot and cross products):
+//   |da|  <= 7u D |e1||e2|                       (a, D = max |d| = 2)
+//   eps_u <= (9u D |s| |e2| + 1.5 * 7u D |e1||e2|) / A,  eps_v likewise with |e1|
+//   |t - t*| <= ((9 |s| + 7 D T) u |e1||e2|) / A + 2u T
+// where A = |a| - |da| and T bounds t*. The exact hit X* = p1 + u* e1 + v* e2
+// then lies within eps_u |e1| + eps_v |e2| of the triangle and the reported
+// point within D |t - t*| + 2u(|o| + D T) of X*. For grazing rays A can be as
+// small as 1e-5 and the stray reaches a triangle-size (measured: 0.5 units on
+// the car's half-unit triangles, tests/test_accel_cpu.py); the bound is
+// therefore taken for |cos(d, n)| >= kMtCos, A >= 0.5 |e1 x e2| kMtCos, and the
+// walk enters every subtree such a ray might graze regardless of its box.
+RTA_HD int classify_mt_triangle(const FlatShape& s, Box3& out, double origin_lim) {
+    const float e1f[3] = {s.triP2.x - s.triP1.x, s.triP2.y - s.triP1.y, s.triP2.z - s.triP1.z};
+    const float e2f[3] = {s.triP3.x - s.triP1.x, s.triP3.y - s.triP1.y, s.triP3.z - s.triP1.z};
+    const D3 p1 = d3(s.triP1), e1{e1f[0], e1f[1], e1f[2]}, e2{e2f[0], e2f[1], e2f[2]};
+    if (!finite3(p1) || !finite3(e1) || !finite3(e2)) return UNBOUNDED;
+    const double E1 = sqrt(dot(e1, e1)), E2 = sqrt(dot(e2, e2)), cr = sqrt(dot(cross(e1, e2), cross(e1, e2)));
+    if (!(cr > 0) || !isfinite(cr)) return UNBOUNDED;
+    const double D = 2.0;
+    const double A = fmax(1e-5, 0.5 * cr * kMtCos) - 7 * kU * D * E1 * E2;
+    if (!(A > 0.5e-5)) return UNBOUNDED;
+    const double Sm = sqrt(3.0) * origin_lim + sqrt(dot(p1, p1));
+    const double eu = (9 * kU * D * Sm * E2 + 1.5 * 7 * kU * D * E1 * E2) / A;
+    const double ev = (9 * kU * D * Sm * E1 + 1.5 * 7 * kU * D * E1 * E2) / A;
+    if (!(eu < 0.5 && ev < 0.5)) return UNBOUNDED;
+    const double T = 2.0 * (Sm + (1 + eu) * E1 + (1 + ev) * E2);
+    const double dt = 1.01 * ((9 * Sm + 7 * D * T) * kU * E1 * E2 / A + 2 * kU * T);
+    const double pad = kMtSafety * (eu * E1 + ev * E2 + D * dt + 2 * kU * (sqrt(3.0) * origin_lim + D * (T + dt)));
+    if (!isfinite(pad) || pad > 1e3 * (E1 + E2 + 1.0)) return UNBOUNDED;
+    BoxAcc acc;
+    acc.add(p1);
+    acc.add(p1 + e1);
+    acc.add(p1 + e2);
+    out = finish(acc, origin_lim);
+    for (int i = 0; i < 3; ++i) {
+        out.lo[i] = nextafterf(static_cast<float>(static_cast<double>(out.lo[i]) - pad), -INFINITY);
+        out.hi[i] = nextafterf(static_cast<float>(static_cast<double>(out.hi[i]) + pad), INFINITY);
+    }
+    return BOUNDED;
+}
+
 // UNBOUNDED: no finite bound; BOUNDED: `out` is set; NEVER: the reference test
 // never returns INNER. origin_lim: largest |coordinate| of a ray origin the
 // bound must hold for (0 for the build's first pass, which only measures the
-// scene's magnitude).
-RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim) {
+// scene's magnitude). mt: triangles take the Moller-Trumbore test
+// (classify_mt_triangle; the other shapes' tests do not depend on it).
+RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim, bool mt = false) {
+    if (mt && s.type == RT_TRIANGLE) return classify_mt_triangle(s, out, origin_lim);
     BoxAcc acc;
     switch (s.type) {
         case RT_SPHERE: {

@@ -567,9 +567,37 @@ __device__ __forceinline__ bool lex_better(float d, int seq, const Best& b) {
 // the hit point and distance are computed exactly as the reference does, and
 // the remaining (wall / barycentric) checks only run when the candidate could
 // win. Same result as testing first and comparing after.
+// Moller-Trumbore (gpu_shader.comp:170-195) with the same float operations as
+// intersect(): t > 0 gives INNER at o + t d, whatever the triangle's facing.
+__device__ __forceinline__ bool mt_hit(const float* f, const Ray& r, V& p) {
+    const V p1 = mk(f[4], f[5], f[6]), e1 = mk(f[7], f[8], f[9]), e2 = mk(f[10], f[11], f[12]);
+    const V hh = cross(r.d, e2);
+    const float a = dot(e1, hh);
+    if (__builtin_fabsf(a) < 1e-5f) return false;
+    const float fi = 1.0f / a;
+    const V s = r.o - p1;
+    const float u = fi * dot(s, hh);
+    if (u < 0.0f || u > 1.0f) return false;
+    const V q = cross(s, e1);
+    const float v = fi * dot(r.d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    const float t = fi * dot(e2, q);
+    if (!(t > 0.0f)) return false;
+    p = r.o + t * r.d;
+    return true;
+}
+
+template <bool MT = false>
 __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray& r, Best& b) {
     const float* f = g.f;
     const int seq = __float_as_int(f[17]);
+    if (MT && g.type == 3) {
+        V p;
+        if (!mt_hit(f, r, p)) return;
+        const float d = dist(r.o, p);
+        if (lex_better(d, seq, b)) b = Best{d, seq, p, slot};
+        return;
+    }
     if (g.type == 0) {
         V c = mk(f[0], f[1], f[2]);
         V oc = r.o - c;
@@ -618,8 +646,13 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
 }
 
 // Shadow candidate: an INNER hit nearer than lim (gpu_shader.comp:473-480).
+template <bool MT = false>
 __device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float lim) {
     const float* f = g.f;
+    if (MT && g.type == 3) {
+        V p;
+        return mt_hit(f, r, p) && dist(r.o, p) < lim;
+    }
     if (g.type == 0) {
         V c = mk(f[0], f[1], f[2]);
         V oc = r.o - c;
@@ -791,6 +824,10 @@ __device__ __forceinline__ void cas(Kids4& k, int i, int j) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
+// MT (AccelHost::mt): the cone is a grazing cone; a child the ray might graze
+// (|dot| < thr) is entered at parameter 0 whatever its box, and nothing is culled
+// by facing (Moller-Trumbore has no back-face test).
+template <bool MT = false>
 __device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f2 ly, f2 lz, f2 hx, f2 hy, f2 hz,
                                           f2 ax, f2 ay, f2 az, f2 th, float& t0, float& t1, bool& h0, bool& h1) {
     const f2 ix = {c.ix, c.ix}, iy = {c.iy, c.iy}, iz = {c.iz, c.iz};
@@ -810,12 +847,21 @@ __device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f
         tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), fminf(fmaxf(z0[k], z1[k]), np ? INFINITY : tl));
         te[k] = np ? 0.0f : tn[k];
     }
+    if (MT) {
+        const bool g0 = __builtin_fabsf(dn[0]) < th[0] + rta::kConeEps, g1 = __builtin_fabsf(dn[1]) < th[1] + rta::kConeEps;
+        t0 = g0 ? 0.0f : te[0];
+        t1 = g1 ? 0.0f : te[1];
+        h0 = (tn[0] <= tf[0]) | g0;
+        h1 = (tn[1] <= tf[1]) | g1;
+        return;
+    }
     t0 = te[0];
     t1 = te[1];
     h0 = (tn[0] <= tf[0]) & !(dn[0] < thr[0]);
     h1 = (tn[1] <= tf[1]) & !(dn[1] < thr[1]);
 }
 
+template <bool MT = false>
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
     const float4* q = A.lnodes + 11 * static_cast<size_t>(uc & 0x3fffffffu);
     const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
@@ -823,10 +869,10 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
     const int cc[4] = {__float_as_int(cd.x), __float_as_int(cd.y), __float_as_int(cd.z), __float_as_int(cd.w)};
     float t[4];
     bool h[4];
-    wide_pair(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y}, (f2){hy.x, hy.y},
+    wide_pair<MT>(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y}, (f2){hy.x, hy.y},
               (f2){hz.x, hz.y}, (f2){ax.x, ax.y}, (f2){ay.x, ay.y}, (f2){az.x, az.y}, (f2){th.x, th.y}, t[0], t[1],
               h[0], h[1]);
-    wide_pair(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w}, (f2){hy.z, hy.w},
+    wide_pair<MT>(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w}, (f2){hy.z, hy.w},
               (f2){hz.z, hz.w}, (f2){ax.z, ax.w}, (f2){ay.z, ay.w}, (f2){az.z, az.w}, (f2){th.z, th.w}, t[2], t[3],
               h[2], h[3]);
     Kids4 k;
@@ -858,7 +904,7 @@ __device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_flo
 // the nearer child in registers and stacking the farther one; the wave then
 // tests all lanes' leaves together. A stacked entry is dropped on pop when a
 // nearer hit has been found since it was pushed.
-template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool SPEC = true>
+template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool SPEC = true, bool MT = false>
 __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
                           int* stk, unsigned short* stt, int stride, int cap, WalkCount& wc) {
     if (A.N <= 0 || !active) return;
@@ -933,7 +979,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     count = static_cast<int>(uc & 0x3fu);
                     if (uc & kItem) count = ((fm >> (count >> 3)) & 1u) ? (count & 7) : 0;  // few-leaf item
                 } else if (uc & kLocal) {
-                    Kids4 w = wide_kids(A, uc, c, tl, true);
+                    Kids4 w = wide_kids<MT>(A, uc, c, tl, true);
                     sort4(w);
 #pragma unroll
                     for (int s2 = 3; s2 >= 1; --s2) {
@@ -975,12 +1021,12 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
             if (COUNT) wc.tests++;
             if (WSTAT && first_active()) wc.wtests++;
             if (SHADOW) {
-                if (try_shadow(g, r, lim_shadow)) {
+                if (try_shadow<MT>(g, r, lim_shadow)) {
                     shadow = true;
                     return;
                 }
             } else {
-                try_closest(g, start + i, r, b);
+                try_closest<MT>(g, start + i, r, b);
             }
         }
         if (!SHADOW) tl = rta::t_limit(b.d, c.rdl);
@@ -991,7 +1037,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
 // (VGPR-resident stack, scalar node loads). The reference's walk order does
 // not depend on the ray, so one walk with masks reproduces every lane's own;
 // the order among children follows the first lane that enters both.
-template <bool SHADOW, bool COUNT = false, bool WSTAT = false>
+template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool MT = false>
 __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b,
                             bool& shadow, WalkCount& wc) {
     unsigned long long m = __ballot(active);
@@ -1066,7 +1112,7 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
         } else if (uc & kLocal) {
             // wide node: children ordered by the entry parameters of the first lane
             // that enters any of them; the rest pushed far to near
-            const Kids4 w = wide_kids(A, uc, c, tl, lane_in(m));
+            const Kids4 w = wide_kids<MT>(A, uc, c, tl, lane_in(m));
             unsigned long long wm[4];
             float key[4];
             int code[4];
@@ -1113,12 +1159,12 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
                 if (live) {
                     if (COUNT) wc.tests++;
                     if (SHADOW) {
-                        if (try_shadow(g, r, lim_shadow)) {
+                        if (try_shadow<MT>(g, r, lim_shadow)) {
                             shadow = true;
                             live = false;
                         }
                     } else {
-                        try_closest(g, start + i, r, b);
+                        try_closest<MT>(g, start + i, r, b);
                     }
                 }
                 if (SHADOW && __ballot(live) == 0) break;
@@ -1211,7 +1257,7 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
 // One bounce of gpu_shader.comp:450-517 for a wave's rays: closest hit, background
 // on a miss, the shadow ray, then Phong and the mirror ray (shade_bounce).
 // bg_y() gives the lane's image row (recomputed, not kept live through the walks).
-template <bool COUNT, bool SPEC, bool COST, class BgY>
+template <bool COUNT, bool SPEC, bool COST, bool MT, class BgY>
 __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp,
                                             int depth, Ray& ray, bool& alive, V& acc, V& att, BgY bg_y, int* stk,
                                             unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
@@ -1221,9 +1267,9 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     WalkCount w0 = wc;
     unsigned long long c0 = COUNT ? clock64() : 0;
     if (lane_mode)
-        lane_walk<false, COST || COUNT, COUNT, SPEC>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
+        lane_walk<false, COST || COUNT, COUNT, SPEC, MT>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
     else
-        packet_walk<false, COST || COUNT, COUNT>(A, ray, alive, 0.f, best, unused, wc);
+        packet_walk<false, COST || COUNT, COUNT, MT>(A, ray, alive, 0.f, best, unused, wc);
     if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
     if (alive && best.slot < 0) {
         acc = acc + mulv(att, background(kp, bg_y()));
@@ -1243,9 +1289,9 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     w0 = wc;
     c0 = COUNT ? clock64() : 0;
     if (depth >= kp.shadow_lane_from)
-        lane_walk<true, COST || COUNT, COUNT, SPEC>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
+        lane_walk<true, COST || COUNT, COUNT, SPEC, MT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
     else
-        packet_walk<true, COST || COUNT, COUNT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
+        packet_walk<true, COST || COUNT, COUNT, MT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
     if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
     if (alive) {
         const GeoRec g = load_rec(A.prims, best.slot);
@@ -1256,7 +1302,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
 
 // Walk counts (node steps, tests) are kept when COST: they are the cost that
 // orders a later dispatch (rt_set_schedule). COUNT adds the per-walk records.
-template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false>
+template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
     // Pixel coordinates and the background are recomputed where needed rather than
@@ -1284,7 +1330,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     }
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
-        bounce_step<COUNT, SPEC, COST>(A, mat, kp, depth, ray, alive, acc, att,
+        bounce_step<COUNT, SPEC, COST, MT>(A, mat, kp, depth, ray, alive, acc, att,
                                        [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec);
         if (TAIL && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
             // Compaction: the rays still alive go to the tail queue (one atomic per wave)
@@ -1325,7 +1371,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 // COST = false: a dispatch that records no tile work (rt_set_schedule reuses the
 // last order), without the walk counters' registers (12 -> 3 spilled VGPRs).
 // TAIL: queue the rays alive after bounce tail_from - 1 for k_accel_tail (rt_set_tail).
-template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true, bool TAIL = false>
+template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false>
 __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
     // per-lane stacks, entry j of lane i at [j * blockDim.x + i]: codes, then bf16 entry parameters
@@ -1345,7 +1391,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         if (kp.tile_order) tile = kp.tile_order[tile];  // dispatch order -> image tile (a permutation)
         WalkCount wc{0u, 0u, 0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
-        accel_tile<TIMED, SPEC, COST, TAIL>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
+        accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1447,7 +1493,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
         WalkCount wc{0u, 0u, 0u, 0u};
         for (int depth = kp.tail_from; depth < kp.maxBounces; ++depth) {
             if (__ballot(alive) == 0) break;
-            bounce_step<false, SPEC, false>(A, mat, kp, depth, ray, alive, acc, att,
+            bounce_step<false, SPEC, false, false>(A, mat, kp, depth, ray, alive, acc, att,
                                             [&]() { return image_row(kp, r); }, stk, stt, kp.lane_stack, wc, nullptr);
         }
         if (have) store_px(kp, r, x, make_float4(acc.x, acc.y, acc.z, 1.0f));
@@ -1851,6 +1897,11 @@ struct rt_ctx {
     rt_ctx* brute = nullptr;
     bool brute_stale = true;            // shapes changed since brute's upload
     int brute_accel = 1;                // rt_set_brute_accel
+    // Moller-Trumbore frames (useMollerTrumbore = 1) render through `mtc`: the same
+    // scene with its accelerator built for the MT test (accel.h AccelHost::mt).
+    rt_ctx* mtc = nullptr;
+    bool mtc_stale = true;              // shapes or nodes changed since mtc's upload
+    bool build_mt = false;              // this context's accelerator is built for MT
 };
 
 namespace {
@@ -1958,7 +2009,7 @@ int build_upload_accel(rt_ctx* c) {
     if (N == 0) return RT_OK;
     rta::AccelHost& A = c->accel;
     if (!rta::build_accel(c->host_shapes.data(), c->S, c->host_nodes.data(), N, c->host_idx.data(), c->I,
-                          kLeafScan, kMaxStack, A))
+                          kLeafScan, kMaxStack, A, c->build_mt))
         return RT_OK;
     if (N >= (1 << 28)) return RT_OK;  // codes carry the node index in 28 bits
     c->boxes_finite = 1;
@@ -2354,45 +2405,29 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step,
 
 bool accel_usable(const rt_ctx* c, const KParams& kp) {
     const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
-    return c->accel_ok && kp.useBVH && !kp.useMT && cmag <= c->accel.origin_lim;
+    return c->accel_ok && kp.useBVH && (kp.useMT != 0) == c->accel.mt && cmag <= c->accel.origin_lim;
 }
 
 int launch(rt_ctx* c, const KParams& kp, bool stats);
 
-// The brute branch through `brute` (rt_ctx::brute): the same shapes under one
-// leaf listing 0..S-1 with an infinite box, built on first use after the
-// shapes change. nullptr: render the branch literally (k_packet).
-rt_ctx* brute_ctx(rt_ctx* c, const KParams& kp) {
-    if (!c->brute_accel || kp.useBVH || kp.useMT || !c->anim_ids.empty() || c->S <= 0 ||
-        (c->kernel != RT_KERNEL_AUTO && c->kernel != RT_KERNEL_ACCEL))
-        return nullptr;
-    if (!c->brute) {
-        if (rt_create(&c->brute, c->device) != RT_OK) return nullptr;
-        hipStreamDestroy(c->brute->stream);
-        c->brute->stream = c->stream;
-        c->brute->own_stream = false;
-        c->brute_stale = true;
+// A sub-context on this context's stream (brute / mtc), created on first use.
+rt_ctx* sub_ctx(rt_ctx* c, rt_ctx*& sub, bool& stale) {
+    if (!sub) {
+        if (rt_create(&sub, c->device) != RT_OK) return nullptr;
+        hipStreamDestroy(sub->stream);
+        sub->stream = c->stream;
+        sub->own_stream = false;
+        stale = true;
     }
-    rt_ctx* b = c->brute;
-    if (c->brute_stale) {
-        FlatNode leaf;
-        std::memset(&leaf, 0, sizeof leaf);
-        const float inf = std::numeric_limits<float>::infinity();
-        leaf.boundsMin = rt_vec3{-inf, -inf, -inf};
-        leaf.boundsMax = rt_vec3{inf, inf, inf};
-        leaf.leftChild = leaf.rightChild = -1;
-        leaf.startShapeIdx = 0;
-        leaf.numShapes = c->S;
-        std::vector<int> order(c->S);
-        for (int i = 0; i < c->S; ++i) order[i] = i;
-        if (rt_upload_scene(b, c->host_shapes.data(), c->S, &leaf, 1, order.data(), c->S) != RT_OK) return nullptr;
-        c->brute_stale = false;
-    }
+    return sub;
+}
+
+// The frame constants and walk settings of `c`, for a sub-context rendering its frame.
+void inherit(rt_ctx* b, const rt_ctx* c) {
     b->cam = c->cam;
     b->light = c->light;
     b->have_cam = b->have_light = true;
     b->params = c->params;
-    b->params.useBVH = 1;
     b->kernel = RT_KERNEL_ACCEL;
     b->waves_per_block = c->waves_per_block;
     b->persistent = c->persistent;
@@ -2407,35 +2442,97 @@ rt_ctx* brute_ctx(rt_ctx* c, const KParams& kp) {
     b->tree_mode = c->tree_mode;
     b->scene_stack = c->scene_stack;
     b->lane_stack_override = c->lane_stack_override;
-    const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
-    return b->accel_ok && cmag <= b->accel.origin_lim ? b : nullptr;
 }
 
-// rt_dispatch_rows' render: the brute branch on `brute` when it applies, timed
-// by this context's events (rt_kernel_times) like any other dispatch.
+bool sub_usable(const rt_ctx* b, const KParams& kp) {
+    const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
+    return b->accel_ok && cmag <= b->accel.origin_lim;
+}
+
+// The brute branch through `brute` (rt_ctx::brute): the same shapes under one
+// leaf listing 0..S-1 with an infinite box, built on first use after the
+// shapes change. nullptr: render the branch literally (k_packet).
+rt_ctx* brute_ctx(rt_ctx* c, const KParams& kp) {
+    if (!c->brute_accel || kp.useBVH || !c->anim_ids.empty() || c->S <= 0 ||
+        (c->kernel != RT_KERNEL_AUTO && c->kernel != RT_KERNEL_ACCEL))
+        return nullptr;
+    rt_ctx* b = sub_ctx(c, c->brute, c->brute_stale);
+    if (!b) return nullptr;
+    if (c->brute_stale) {
+        FlatNode leaf;
+        std::memset(&leaf, 0, sizeof leaf);
+        const float inf = std::numeric_limits<float>::infinity();
+        leaf.boundsMin = rt_vec3{-inf, -inf, -inf};
+        leaf.boundsMax = rt_vec3{inf, inf, inf};
+        leaf.leftChild = leaf.rightChild = -1;
+        leaf.startShapeIdx = 0;
+        leaf.numShapes = c->S;
+        std::vector<int> order(c->S);
+        for (int i = 0; i < c->S; ++i) order[i] = i;
+        if (rt_upload_scene(b, c->host_shapes.data(), c->S, &leaf, 1, order.data(), c->S) != RT_OK) return nullptr;
+        c->brute_stale = false;
+    }
+    inherit(b, c);
+    b->params.useBVH = 1;
+    return b;  // its own MT forwarding (mt_ctx) applies on the next hop
+}
+
+// Moller-Trumbore frames through `mtc` (rt_ctx::mtc): the same shapes and tree,
+// the accelerator built for the MT test.
+rt_ctx* mt_ctx(rt_ctx* c, const KParams& kp) {
+    if (!kp.useBVH || !kp.useMT || c->build_mt || !c->anim_ids.empty() || c->S <= 0 || c->N <= 0 ||
+        (c->kernel != RT_KERNEL_AUTO && c->kernel != RT_KERNEL_ACCEL))
+        return nullptr;
+    rt_ctx* b = sub_ctx(c, c->mtc, c->mtc_stale);
+    if (!b) return nullptr;
+    if (c->mtc_stale) {
+        b->build_mt = true;
+        if (sync_host_nodes(c) != RT_OK ||
+            rt_upload_scene(b, c->host_shapes.data(), c->S, c->host_nodes.data(), c->N, c->host_idx.data(),
+                            c->I) != RT_OK)
+            return nullptr;
+        c->mtc_stale = false;
+    }
+    inherit(b, c);
+    return b;
+}
+
+// rt_dispatch_rows' render: through `brute` (useBVH = 0) and / or `mtc`
+// (Moller-Trumbore) when they apply and their accelerator can take the frame,
+// timed by this context's events (rt_kernel_times) like any other dispatch.
 int render(rt_ctx* c, const KParams& kp) {
-    rt_ctx* b = brute_ctx(c, kp);
-    if (!b) return launch(c, kp, false);
-    KParams kb;
-    int rc = fill_kparams(b, kp.width, kp.height, kp.y0, kp.stripe, kp.step, kp.out_rows,
-                          reinterpret_cast<float*>(kp.dst), kp.pitch, kb);
-    if (rc != RT_OK) return rc;
-    kb.shadow_off = 1e-5f;  // gpu_shader.comp:565
+    rt_ctx* t = c;
+    KParams kt = kp;
+    for (int hop = 0; hop < 2; ++hop) {
+        float off = kt.shadow_off;
+        rt_ctx* nxt = brute_ctx(t, kt);
+        if (nxt) off = 1e-5f;  // gpu_shader.comp:565
+        else nxt = mt_ctx(t, kt);
+        if (!nxt) break;
+        KParams kn;
+        const int rc = fill_kparams(nxt, kt.width, kt.height, kt.y0, kt.stripe, kt.step, kt.out_rows,
+                                    reinterpret_cast<float*>(kt.dst), kt.pitch, kn);
+        if (rc != RT_OK) return rc;
+        kn.shadow_off = off;
+        t = nxt;
+        kt = kn;
+    }
+    if (t == c || !accel_usable(t, kt)) return launch(c, kp, false);
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (c->ring_used < static_cast<int>(c->ring0.size())) {
         e0 = c->ring0[c->ring_used];
         e1 = c->ring1[c->ring_used];
     }
     HIP_TRY(hipEventRecord(e0, c->stream));
-    rc = launch(b, kb, false);
+    const int rc = launch(t, kt, false);
     if (rc != RT_OK) return rc;
     HIP_TRY(hipEventRecord(e1, c->stream));
     c->last0 = e0;
     c->last1 = e1;
     if (c->ring_used < static_cast<int>(c->ring0.size())) ++c->ring_used;
     c->timed = true;
-    c->last_kind = b->last_kind;
-    b->ring_used = 0;  // its own records are not read
+    c->last_kind = t->last_kind;
+    t->ring_used = 0;  // its own records are not read
     return RT_OK;
 }
 
@@ -2578,7 +2675,15 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             k2.tail_counters = c->tail_regions_cap;
             k2.tail_max_lanes = c->tail_max_lanes;
         }
-        if (kfn == k_accel<false, false, true>) {
+        if (c->accel.mt) {
+            // Moller-Trumbore accelerator: its own instances; no compaction
+            k2.tail_queue = nullptr;
+            kfn = spec ? (k2.tile_cost ? k_accel<false, false, true, true, false, true>
+                                       : k_accel<false, false, true, false, false, true>)
+                       : (k2.tile_cost ? k_accel<false, false, false, true, false, true>
+                                       : k_accel<false, false, false, false, false, true>);
+            blocks = (k2.tiles + wpb - 1) / wpb;
+        } else if (kfn == k_accel<false, false, true>) {
             // production shape: the counter-free kernel on a dispatch that records no tile
             // work; the queueing kernel when the tail runs (other shapes: no compaction)
             if (tail) kfn = k2.tile_cost ? k_accel<false, false, true, true, true> : k_accel<false, false, true, false, true>;
@@ -2681,6 +2786,8 @@ int rt_destroy(rt_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     if (c->brute) rt_destroy(c->brute);  // it runs on this context's stream
     c->brute = nullptr;
+    if (c->mtc) rt_destroy(c->mtc);
+    c->mtc = nullptr;
     free_scene(c);
     hipFree(c->staging_shapes);
     hipFree(c->staging_nodes);
@@ -2723,10 +2830,10 @@ int rt_set_stream(rt_ctx* c, void* s) {
         HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         c->own_stream = true;
     }
-    if (c->brute) {  // the brute-branch context runs on this context's stream (synchronised above)
-        c->brute->stream = c->stream;
-        c->brute->own_stream = false;
-    }
+    for (rt_ctx* sub : {c->brute, c->mtc})  // sub-contexts run on this context's stream (synchronised above)
+        if (sub) {
+            rt_set_stream(sub, c->stream);
+        }
     return RT_OK;
 }
 
@@ -2772,7 +2879,7 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->have_scene = true;
     c->nodes_on_device_newer = false;
     c->anim_ids.clear();  // ids refer to the previous scene
-    c->brute_stale = true;
+    c->brute_stale = c->mtc_stale = true;
     return upload_accel(c);
 }
 
@@ -2790,7 +2897,7 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(c->stream));  // glBufferSubData semantics: the host array may be reused
     std::copy(shapes, shapes + count, c->host_shapes.begin() + first);
-    c->brute_stale = true;
+    c->brute_stale = c->mtc_stale = true;
     return upload_accel(c);  // moved shapes change the conservative bounds
 }
 
@@ -2810,6 +2917,7 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host array may be reused after return
     c->host_nodes.assign(nodes, nodes + N);
     c->nodes_on_device_newer = false;
+    c->mtc_stale = true;
     return upload_accel(c);
 }
 
@@ -2895,7 +3003,7 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
                            c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr);
     HIP_TRY(hipGetLastError());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
-    c->brute_stale = true;
+    c->brute_stale = c->mtc_stale = true;
     c->nodes_on_device_newer = true;
     c->st_root = kNoChild;  // the scene tree's bounds are not refit: stale until the next build
     if (!rebuild) return RT_OK;

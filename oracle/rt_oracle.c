@@ -757,10 +757,21 @@ int orc_wall_end(const FlatShape* s, float* e) {
 /* Closest-hit (shape index or -1, distance) and shadow query (any INNER hit
  * nearer than lim) of the reference walk for arbitrary rays: the checker for
  * tests/native/accel_check.cpp. */
+int orc_trace_rays_mt(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                      const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
+                      int* out_shadow, int use_mt);
+
 int orc_trace_rays(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
                    const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
                    int* out_shadow) {
-    rt_params p = {1, 1, 1, 1, 0, 0};
+    return orc_trace_rays_mt(shapes, S, nodes, N, idx, I, o, d, lim, R, out_shape, out_d, out_shadow, 0);
+}
+
+/* The same with the Moller-Trumbore triangle test when use_mt (useMollerTrumbore). */
+int orc_trace_rays_mt(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                      const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
+                      int* out_shadow, int use_mt) {
+    rt_params p = {1, 1, 1, 1, 0, use_mt ? 1 : 0};
     scene_t sc = {shapes, S, nodes, N, idx, I, NULL, NULL, p};
 #pragma omp parallel for schedule(dynamic, 64)
     for (int i = 0; i < R; ++i) {

@@ -28,8 +28,27 @@ V fv(rt_vec3 v) { return {v.x, v.y, v.z}; }
 
 struct Best { float d; int seq; V p; int shape; };
 
-// INNER hit of a shape, GLSL semantics (barycentric), or false.
+bool g_mt = false;  // Moller-Trumbore triangles (out_info[6] = 1)
+
+// INNER hit of a shape, GLSL semantics (barycentric, or Moller-Trumbore when g_mt), or false.
 bool isect(const FlatShape& s, V o, V d, V& p) {
+    if (g_mt && s.type == 3) {  // gpu_shader.comp:170-195, the device's mt_hit operations
+        V p1 = fv(s.triP1), e1 = fv(s.triP2) - p1, e2 = fv(s.triP3) - p1;
+        V hh = cross(d, e2);
+        float a = dot(e1, hh);
+        if (std::fabs(a) < 1e-5f) return false;
+        float fi = 1.0f / a;
+        V sv = o - p1;
+        float u = fi * dot(sv, hh);
+        if (u < 0.0f || u > 1.0f) return false;
+        V q = cross(sv, e1);
+        float v = fi * dot(d, q);
+        if (v < 0.0f || u + v > 1.0f) return false;
+        float t = fi * dot(e2, q);
+        if (!(t > 0.0f)) return false;
+        p = o + t * d;
+        return true;
+    }
     if (s.type == 0) {
         V c = fv(s.sphereCenter), oc = o - c;
         float aa = dot(d, d), bb = 2.0f * dot(d, oc), cc = dot(oc, oc) - s.sphereRadius * s.sphereRadius;
@@ -74,6 +93,12 @@ bool ref_aabb(V o, V inv, const rt_vec3& lo, const rt_vec3& hi) {
 }
 
 // The device walk's conservative tests (accel_math.h), same float operations.
+// MT grazing cone (accel.h, AccelHost::mt): the device's test in wide_pair.
+bool grazing(const rta::RayC& c, const float* k) {
+    const float dn = std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz));
+    return std::fabs(dn) < k[3] + rta::kConeEps;
+}
+
 bool padded(const rta::RayC& c, const rta::Box3& b, float l) {
     float te;
     return rta::box_enter(c, b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2], rta::t_limit(l, c.rdl), te);
@@ -91,7 +116,8 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                 const float* o, const float* d, const float* lim, int R, int* out_shape, float* out_d,
                 int* out_shadow, int* out_info) {
     rta::AccelHost A;
-    if (!rta::build_accel(shapes, S, nodes, N, idx, I, 8, 64, A)) return -1;
+    g_mt = out_info[6] != 0;
+    if (!rta::build_accel(shapes, S, nodes, N, idx, I, 8, 64, A, g_mt)) return -1;
     out_info[0] = static_cast<int>(A.lbox.size());
     out_info[1] = A.always_prims;
     out_info[2] = A.bounded_prims;
@@ -152,8 +178,12 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         const int j = A.st.wchild[rta::kWide * w + s2];
                         if (j < 0) continue;
                         const float* k = &A.st_cone[4 * j];
-                        if (!padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
-                        if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                        if (g_mt) {
+                            if (!grazing(rc, k) && !padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
+                        } else {
+                            if (!padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
+                            if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                        }
                         const int sub = A.st.wsub[rta::kWide * w + s2];
                         if (sub >= 0) {
                             st.push_back(-(sub + 1) - kSceneBase);
@@ -171,7 +201,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         scan(A.plain_start[code], A.plain_count[code]);
                         const int lr = A.local_root[code];
                         if (lr >= 0 && A.wroot[code] >= 0) st.push_back(-(A.wroot[code] + 1));  // wide root
-                        else if (lr >= 0 && padded(rc, A.lbox[lr], l)) scan(-A.la[lr] - 1, A.lb[lr]);
+                        else if (lr >= 0 && (g_mt || padded(rc, A.lbox[lr], l))) scan(-A.la[lr] - 1, A.lb[lr]);
                     } else {
                         st.push_back(nd.leftChild);
                         st.push_back(nd.rightChild);
@@ -182,9 +212,14 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     const int w = -code - 1;
                     for (int s2 = 0; s2 < rta::kWide; ++s2) {
                         const int j = A.wchild[rta::kWide * w + s2];
-                        if (j < 0 || !padded(rc, A.lbox[j], l)) continue;
+                        if (j < 0) continue;
                         const float* k = &A.lcone[4 * j];
-                        if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                        if (g_mt) {
+                            if (!grazing(rc, k) && !padded(rc, A.lbox[j], l)) continue;
+                        } else {
+                            if (!padded(rc, A.lbox[j], l)) continue;
+                            if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                        }
                         if (A.la[j] < 0) scan(-A.la[j] - 1, A.lb[j]);
                         else st.push_back(-(A.wsub[rta::kWide * w + s2] + 1));
                     }

@@ -34,6 +34,8 @@ def check_lib(tmp_path_factory):
     o.orc_trace_rays.restype = C.c_int
     o.orc_trace_rays.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int] + \
         [C.c_void_p] * 3 + [C.c_int] + [C.c_void_p] * 3
+    o.orc_trace_rays_mt.restype = C.c_int
+    o.orc_trace_rays_mt.argtypes = o.orc_trace_rays.argtypes + [C.c_int]
     return lib
 
 
@@ -41,7 +43,7 @@ def _p(a):
     return C.c_void_p(a.ctypes.data) if a.size else None
 
 
-def compare(lib, fs, o, d, lim, tree=1):
+def compare(lib, fs, o, d, lim, tree=1, mt=0):
     fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)  # enforce record layout
     R = len(o)
     o = np.ascontiguousarray(o, np.float32)
@@ -51,10 +53,11 @@ def compare(lib, fs, o, d, lim, tree=1):
     refs = [np.zeros(R, np.int32), np.zeros(R, np.float32), np.zeros(R, np.int32)]
     info = np.zeros(12, np.int32)
     info[8] = tree
+    info[6] = mt
     args = [_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes), _p(fs.indices), len(fs.indices),
             _p(o), _p(d), _p(lim), R]
     assert lib.accel_check(*args, *[_p(x) for x in outs], _p(info)) == 0
-    assert oracle.lib().orc_trace_rays(*args, *[_p(x) for x in refs]) == 0
+    assert oracle.lib().orc_trace_rays_mt(*args, *[_p(x) for x in refs], mt) == 0
     bad = np.where(outs[0] != refs[0])[0]
     assert bad.size == 0, f"{bad.size} closest-hit mismatches, e.g. ray {bad[0]}: {outs[0][bad[0]]} vs {refs[0][bad[0]]}"
     assert np.array_equal(outs[1], refs[1])
@@ -395,3 +398,50 @@ def test_mt_hits_stray_beyond_barycentric_padding():
             worst = max(worst, float(np.maximum(0, np.maximum(lo - hit, hit - hi)).max()))
     extent = 0.6  # the car's triangles are about half a unit across
     assert worst > 0.1 * extent, worst  # far beyond the 1e-3 * (size + magnitude) padding of the bounds
+
+
+def grazing_rays(fs, rng, R, far=(100, 220)):
+    """Rays grazing random triangles of the scene from afar (|a| near the MT threshold)."""
+    idx = np.where(fs.shapes["type"] == 3)[0]
+    o, d = [], []
+    for _ in range(R):
+        tri = fs.shapes[idx[rng.integers(len(idx))]]
+        p = [tri[k].astype(np.float64) for k in ("triP1", "triP2", "triP3")]
+        n = np.cross(p[1] - p[0], p[2] - p[0])
+        n /= np.linalg.norm(n)
+        x = rng.dirichlet([1, 1, 1]) @ np.stack(p)
+        t = np.cross(n, rng.normal(size=3))
+        v = t / np.linalg.norm(t) + rng.choice([1, -1]) * 10 ** rng.uniform(-6, -1) * n
+        v /= np.linalg.norm(v)
+        o.append(x - v * rng.uniform(*far))
+        d.append(v)
+    return np.clip(np.array(o), -220, 220), np.array(d)
+
+
+@pytest.mark.parametrize("tree", [0, 1])
+@pytest.mark.parametrize("src", ["car", "monkey", "random", "soup1", "soup3", "car_one_leaf"])
+def test_accel_mt_matches_reference_walk(check_lib, src, tree):
+    """The Moller-Trumbore accelerator (AccelHost::mt: error-bounded boxes for
+    non-grazing rays, grazing cones that force entry) picks the reference MT
+    walk's shape for camera, random and grazing rays from afar."""
+    if src.startswith("soup"):
+        import test_gpu_parity as tg
+        fs = tg._soup(int(src[-1]))
+    else:
+        fs = rtamd.generate({"car": 3, "monkey": 2, "random": 5, "car_one_leaf": 3}[src], 0, 96, 54)
+        if src == "car_one_leaf":
+            fs = one_leaf(fs)
+    rng = np.random.default_rng(len(src) + tree)
+    o, d = camera_rays(fs, 64, 36)
+    o2, d2 = random_rays(rng, 3000)
+    O, D = [o, o2], [d, d2]
+    if (fs.shapes["type"] == 3).any():
+        o3, d3 = grazing_rays(fs, rng, 3000)
+        o4, d4 = grazing_rays(fs, rng, 1000, far=(1, 30))
+        O += [o3, o4]
+        D += [d3, d4]
+    O, D = np.concatenate(O), np.concatenate(D)
+    compare(check_lib, fs, O, D, rng.uniform(1, 80, len(O)), tree, mt=1)
+    if src == "car":  # camera rays alone: the accelerator still culls (the reference walk tests ~3,100 per ray)
+        info = compare(check_lib, fs, o, d, np.full(len(o), 50.0), tree, mt=1)
+        assert info[4] < 1000, info[4]

@@ -260,3 +260,52 @@ def test_brute_branch_follows_shape_updates(ctx):
     fs2 = rtamd.FlatScene(np.concatenate([fs.shapes[:-100], moved]), fs.nodes, fs.indices, fs.camera, fs.light)
     ref, _ = oracle.render(fs2, W, H, oracle.params(W, H, 3, False))
     check(out.cpu().numpy(), ref, "brute after update_shapes")
+
+
+# --------------------------------------------------------------------------
+# Moller-Trumbore frames (useMollerTrumbore = 1) on the MT accelerator
+
+def render_mt(ctx, fs, W, H, mb, bvh, kernel, y0=0, rows=None, fresnel=False):
+    rows = H - y0 if rows is None else rows
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, bvh, fresnel, True)
+    ctx.set_kernel(kernel)
+    out = torch.full((rows, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows(W, H, y0, 1, 1, rows, out.data_ptr(), W * 16)
+    ctx.sync()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("cfg,W,H,mb,bvh,fresnel", [(2, 800, 600, 1, True, False), (2, 400, 300, 4, True, True),
+                                                    (3, 1920, 1080, 3, True, False), (5, 240, 136, 3, True, False),
+                                                    (2, 200, 150, 3, False, False), (3, 240, 136, 3, False, True)],
+                         ids=["config2", "config2_fresnel_b4", "config3_1080p", "config5_240x136",
+                              "config2_brute", "config3_brute_fresnel"])
+def test_mt_accelerated_equals_literal(ctx, cfg, W, H, mb, bvh, fresnel):
+    """useMollerTrumbore = 1 through the MT accelerator (and, for useBVH = 0, the
+    one-leaf tree's MT accelerator) equals the literal k_packet walk bit for bit."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    lit = render_mt(ctx, fs, W, H, mb, bvh, rtamd.KERNEL_PACKET, fresnel=fresnel)
+    for _ in range(2):
+        fast = render_mt(ctx, fs, W, H, mb, bvh, rtamd.KERNEL_AUTO, fresnel=fresnel)
+        assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL
+        assert np.array_equal(fast, lit)
+
+
+def test_mt_vs_oracle_band(ctx):
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    img = render_mt(ctx, fs, W, H, 3, True, rtamd.KERNEL_AUTO, 520, 16)
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, True, False, True), y0=520, out_rows=16)
+    check(img, ref, "MT band")
+
+
+@pytest.mark.parametrize("name", ["grazing_road", "axis_minus_z", "inside_car", "orbit7_car"])
+def test_mt_cameras_vs_oracle(ctx, name):
+    cfg, kw = CAMERAS[name]
+    W, H = 480, 270
+    fs = _camera_scene(cfg, W, H, **kw)
+    img = render_mt(ctx, fs, W, H, 3, True, rtamd.KERNEL_AUTO)
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, True, False, True))
+    check(img, ref, name)
