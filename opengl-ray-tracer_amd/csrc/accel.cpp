@@ -809,7 +809,12 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     build_cones(shapes, out);
     max_stack = std::max(max_stack, build_wide(out, depth, kLaneStack));
     if (max_stack > stack_cap) return false;
-    build_scene_tree(shapes, nodes, N, idx, reach, seq_base, scls, sbox, std::min(stack_cap, kLaneStack), out);
+    // MT: no scene tree. Its inner boxes bound hits, and an MT hit strays from its
+    // triangle on grazing rays; the reference tree's exact boxes decide which leaves
+    // are tested independently of the triangle test, so MT rays walk those (with the
+    // grazing-cone local BVHs inside large leaves).
+    if (!mt)
+        build_scene_tree(shapes, nodes, N, idx, reach, seq_base, scls, sbox, std::min(stack_cap, kLaneStack), out);
     if (out.st.wroot >= 0) max_stack = std::max(max_stack, out.st.max_stack);
     out.max_stack = max_stack;
     return max_stack <= stack_cap;

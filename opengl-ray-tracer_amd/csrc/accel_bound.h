@@ -48,10 +48,10 @@ constexpr double kOriginErr = 4e-6;  // padding per unit of origin_lim (origin-r
 // makes |cos| >= kMtCos with the triangle's normal; the walk enters every
 // subtree holding a triangle such a ray might graze (accel.h, the MT cones).
 #ifndef RTA_MT_COS
-#define RTA_MT_COS 0.02
+#define RTA_MT_COS 0.03
 #endif
 #ifndef RTA_MT_ORIGIN_REL
-#define RTA_MT_ORIGIN_REL 1.5
+#define RTA_MT_ORIGIN_REL 3.0
 #endif
 constexpr double kMtCos = RTA_MT_COS;
 constexpr double kMtSafety = 2.0;
