@@ -79,6 +79,9 @@ def parse(argv=None):
     ap.add_argument("--brute", action="store_true", help="useBVH = 0: the brute-force branch (gpu_shader.comp:523-620)")
     ap.add_argument("--mt", action="store_true", help="useMollerTrumbore = 1 (gpu_shader.comp:170-195)")
     ap.add_argument("--fresnel", action="store_true", help="useFresnel = 1 (gpu_shader.comp:500-509)")
+    ap.add_argument("--animate", action="store_true",
+                    help="config 3: the four wheels turn every frame (updateWheelAnimations, src/main.cpp:1084-1109) "
+                         "and the tree is refit on the device (rt_animate) inside the timed step")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU; 0 = auto: 2, or up to 4 while the GPU's share of a frame "
                          "has fewer than 16k 8x8 tiles (too few waves to fill it)")
@@ -178,6 +181,30 @@ def cpu_reference_1core(rtamd, seconds):
             "config3_primary_only_ms_per_frame_equiv": dt * 1e3 * 1080 / rows,
             "sample": f"cpuRayTracer restated (oracle/rt_oracle.c orc_cpu_raytracer), 1 thread: config 1 {n1} "
                       f"whole 800x600 frames; config 3 rows [{y0},{y0 + rows}) of 1920x1080 in {dt:.2f} s"}
+
+
+def wheel_frames(fs, n):
+    """Records of the car's 640 wheel triangles for n frames: each wheel turns
+    1 rad/s x 1/60 s per frame about its axle (z through its centre), as
+    updateWheelAnimations does with deltaTime (src/main.cpp:1084-1109); stored
+    normals are left as they were (the reference does not update them)."""
+    import numpy as np
+    ids = np.arange(3380, 3380 + 640, dtype=np.int32)  # gen_car: body (3,380), 4 wheels x 160, road
+    rec = fs.shapes[ids].copy()
+    cen = [np.concatenate([rec[f][160 * w:160 * (w + 1)] for f in ("triP1", "triP2", "triP3")]).astype(np.float64)
+           .mean(0) for w in range(4)]
+    frames = []
+    for _ in range(n):
+        rec = rec.copy()
+        for w in range(4):
+            sl = slice(160 * w, 160 * (w + 1))
+            for f in ("triP1", "triP2", "triP3"):
+                q = rec[f][sl].astype(np.float64) - cen[w]
+                c, s = np.cos(1.0 / 60), np.sin(1.0 / 60)
+                rec[f][sl] = (np.stack([q[:, 0] * c - q[:, 1] * s, q[:, 0] * s + q[:, 1] * c, q[:, 2]], 1)
+                              + cen[w]).astype(np.float32)
+        frames.append(rec)
+    return ids, frames
 
 
 def pmc_entry(key):
@@ -300,6 +327,12 @@ def main():
     b_ref_rank = float(mine[2])
 
     cam, light = fs.camera, fs.light
+    anim = wheel_frames(fs, 64) if a.animate else None
+    if anim is not None:
+        if use_group or a.config not in (3, 4):
+            raise SystemExit("--animate: configs 3/4 on one GPU or weak mode")
+        for c_ in ctxs:
+            c_.set_animated(anim[0])
 
     def frame(i, inflight):
         if use_group:
@@ -311,6 +344,8 @@ def main():
         c_ = ctxs[i % inflight]
         c_.set_camera(cam)
         c_.set_light(light)
+        if anim is not None:
+            c_.animate(anim[1][i % len(anim[1])])  # updateScene + updateBVH on the device
         buf = bufs[i % inflight]
         c_.dispatch_rows(W, H, plan.y0(prank), a.stripe, plan.world, rows, buf.data_ptr(), W * 16)
         if strong:
@@ -358,7 +393,7 @@ def main():
         if strong:
             gather = ("rt_group: ncclGather to rank 0 (RCCL over xGMI) + k_unstripe, C ABI (include/rt_group.h)"
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
-        toggles = (a.brute, a.mt, a.fresnel, a.variant)
+        toggles = (a.brute, a.mt, a.fresnel, a.variant, a.animate)
         pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}") if not any(toggles) and not strong else None
         out = {
             "metric": METRIC,
@@ -380,7 +415,8 @@ def main():
             "ranks_seen": world,
             "config": {"workload": f"config {a.config}: {desc}" + (" (222-strip road)" if a.variant else ""),
                        "width": W, "height": H, "maxBounces": mb, "useBVH": int(not a.brute),
-                       "useFresnel": int(a.fresnel), "triangle_test": "moller-trumbore" if a.mt else "barycentric", "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
+                       "useFresnel": int(a.fresnel), "triangle_test": "moller-trumbore" if a.mt else "barycentric",
+                       "animate": "wheels turn, device refit per frame" if a.animate else None, "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
                        "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel,
                        "parallelism": (f"row-stripes{a.stripe}x{world}+gather" if strong else
                                        f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"

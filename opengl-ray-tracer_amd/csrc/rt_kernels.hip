@@ -1750,6 +1750,27 @@ __global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ di
     }
 }
 
+// Scene-tree wide slots of the unbounded subtree (kNoPrune): their boxes are the
+// reference leaves' padded boxes, which animation grows; while a set is animated
+// they are infinite (entered by every ray; the items' exact boxes still gate).
+__global__ void k_inf_slots(const int* __restrict__ slots, int n, float4* __restrict__ lnodes) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int w = slots[i] >> 2, sl = slots[i] & 3;
+    for (int r = 0; r < 6; ++r) reinterpret_cast<float*>(lnodes + 11 * static_cast<size_t>(w) + r)[sl] = r < 3 ? -INFINITY : INFINITY;
+}
+
+// The scene-tree items' exact boxes (titems) from the grown reference leaves.
+__global__ void k_refresh_items(const FlatNode* __restrict__ src, const int* __restrict__ ref, int n,
+                                float4* __restrict__ titems) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const FlatNode& nd = src[ref[i]];
+    float4* q = titems + 2 * static_cast<size_t>(i);
+    q[0] = make_float4(nd.boundsMin.x, nd.boundsMin.y, nd.boundsMin.z, q[0].w);
+    q[1] = make_float4(nd.boundsMax.x, nd.boundsMax.y, nd.boundsMax.z, q[1].w);
+}
+
 // Re-derives every copy of the node boxes from the staging nodes and the
 // content boxes: the packed nodes (k_packet, k_lane), and the accelerator's
 // exact boxes plus its per-parent child copies (anodes rows 0-1, wnodes).
@@ -1813,6 +1834,10 @@ struct rt_ctx {
     float4 *anodes = nullptr, *lnodes = nullptr, *wnodes = nullptr, *prims = nullptr;
     int4* tleaf = nullptr;
     float4* titems = nullptr;  // scene-tree items (AccelPtrs::titems)
+    int* titem_ref = nullptr;  // per titems record: its reference leaf (k_refresh_items, animation)
+    int n_titems = 0;
+    int* anim_inf_slots = nullptr;  // wide slots whose boxes go infinite while animating (kNoPrune)
+    int n_inf_slots = 0;
     int st_root = 0x7fffffff;  // scene-tree root code, kNoChild if none
     int tree_mode = 1;         // rt_set_tree
     int scene_stack = 0;       // rt_debug_scene_stack (0: the walk's own cap)
@@ -1936,6 +1961,12 @@ void free_accel(rt_ctx* c) {
     hipFree(c->tleaf);
     hipFree(c->titems);
     c->titems = nullptr;
+    hipFree(c->titem_ref);
+    c->titem_ref = nullptr;
+    c->n_titems = 0;
+    hipFree(c->anim_inf_slots);
+    c->anim_inf_slots = nullptr;
+    c->n_inf_slots = 0;
     c->st_root = kNoChild;
     hipFree(c->prims);
     hipFree(c->prim_idx_dev);
@@ -2107,6 +2138,10 @@ int build_upload_accel(rt_ctx* c) {
             for (size_t i = 0; i < few.size(); ++i) put(i, few[i], 0, 0);
         else
             for (size_t i = 0; i < T.item_ref.size(); ++i) put(i, T.item_ref[i], T.item_start[i], T.item_count[i]);
+        const std::vector<int>& refs = few.empty() ? T.item_ref : few;
+        if (hipMalloc(&c->titem_ref, refs.size() * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
+        HIP_TRY(hipMemcpyAsync(c->titem_ref, refs.data(), refs.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        c->n_titems = static_cast<int>(refs.size());
     }
     // wnodes: per reference inner node both children's exact + content boxes;
     // tleaf: per reference leaf its plain range and local root code.
@@ -2278,6 +2313,56 @@ int prepare_animation(rt_ctx* c) {
         std::vector<int4> work;
         for (size_t j = 0; j < M; ++j)
             if (dirty[j]) work.push_back(make_int4(wpos[j], first[j], end[j], 0));
+        // The scene tree (accel.h SceneTree), refit like the local trees: its wide
+        // nodes follow the local ones in lnodes (global slot 4*nw + q), a subtree's
+        // prims are contiguous. Its unbounded part (kNoPrune: boxes are the padded
+        // reference-leaf boxes, which grow) goes infinite while the set is animated;
+        // the items' exact boxes follow the grown leaves (k_refresh_items).
+        std::vector<int> inf_slots;
+        const rta::SceneTree& T = A.st;
+        if (T.wroot >= 0) {
+            const size_t nw = A.wchild.size() / rta::kWide, Ms = T.box.size();
+            std::vector<int> sparent(Ms, -1), swpos(Ms, -1), sfirst(Ms, -1), send(Ms, -1), sleaf(P, -1);
+            for (size_t j = 0; j < Ms; ++j) {
+                if (T.a[j] < 0) {
+                    const int st = -T.a[j] - 1;
+                    sfirst[j] = st;
+                    send[j] = st + T.b[j];
+                    for (int q = 0; q < T.b[j]; ++q) sleaf[st + q] = static_cast<int>(j);
+                } else {
+                    sparent[T.a[j]] = static_cast<int>(j);
+                    sparent[T.b[j] & 0x3fffffff] = static_cast<int>(j);
+                }
+            }
+            std::function<void(int)> range = [&](int j) {
+                if (sfirst[j] >= 0) return;
+                const int l = T.a[j], r = T.b[j] & 0x3fffffff;
+                range(l);
+                range(r);
+                sfirst[j] = sfirst[l];
+                send[j] = send[r];
+            };
+            for (size_t j = 0; j < Ms; ++j) range(static_cast<int>(j));
+            for (size_t q = 0; q < T.wchild.size(); ++q)
+                if (T.wchild[q] >= 0) swpos[T.wchild[q]] = static_cast<int>(4 * nw + q);
+            auto noprune = [&](int j) { return A.st_cone[4 * static_cast<size_t>(j) + 3] <= rta::kNoPrune; };
+            for (size_t j = 0; j < Ms; ++j)
+                if (swpos[j] >= 0 && noprune(static_cast<int>(j))) inf_slots.push_back(swpos[j]);
+            std::vector<int> sstamp(Ms, -1);
+            std::vector<char> sdirty(Ms, 0);
+            for (size_t p = 0; p < P; ++p) {
+                const int i = which[A.prim_shape[p]];
+                if (i < 0 || sleaf[p] < 0) continue;
+                for (int j = sleaf[p]; j >= 0; j = sparent[j])
+                    if (swpos[j] >= 0 && !noprune(j) && sstamp[j] != i) {
+                        sstamp[j] = i;
+                        wpos_of[i].push_back(swpos[j]);
+                        sdirty[j] = 1;
+                    }
+            }
+            for (size_t j = 0; j < Ms; ++j)
+                if (sdirty[j]) work.push_back(make_int4(swpos[j], sfirst[j], send[j], 0));
+        }
         std::vector<float4> pb(2 * (P ? P : 1), make_float4(INFINITY, INFINITY, INFINITY, 0.f));
         for (size_t p = 0; p < P; ++p) {
             rta::Box3 b;
@@ -2301,6 +2386,17 @@ int prepare_animation(rt_ctx* c) {
             HIP_TRY(hipMemcpyAsync(c->refit_dirty, work.data(), work.size() * sizeof(int4), hipMemcpyHostToDevice,
                                    c->stream));
         c->n_dirty = static_cast<int>(work.size());
+        hipFree(c->anim_inf_slots);
+        c->anim_inf_slots = nullptr;
+        c->n_inf_slots = static_cast<int>(inf_slots.size());
+        if (!inf_slots.empty()) {
+            if (hipMalloc(&c->anim_inf_slots, inf_slots.size() * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
+            HIP_TRY(hipMemcpyAsync(c->anim_inf_slots, inf_slots.data(), inf_slots.size() * sizeof(int),
+                                   hipMemcpyHostToDevice, c->stream));
+            hipLaunchKernelGGL(k_inf_slots, dim3((c->n_inf_slots + 255) / 256), dim3(256), 0, c->stream,
+                               c->anim_inf_slots, c->n_inf_slots, c->lnodes);
+            HIP_TRY(hipGetLastError());
+        }
     }
     // one int allocation: ids, then (offsets, list) x 4
     std::vector<int> buf(c->anim_ids);
@@ -2633,7 +2729,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
                                : 0;
         // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
-        const int troot = (c->tree_mode == RT_TREE_SCENE && c->anim_ids.empty()) ? c->st_root : kNoChild;
+        // animated scenes keep it: rt_animate refits its boxes and items (prepare_animation)
+        const int troot = c->tree_mode == RT_TREE_SCENE ? c->st_root : kNoChild;
         // production shape on a dispatch that records no tile work: the counter-free kernel
 
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
@@ -3005,7 +3102,11 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
     c->brute_stale = c->mtc_stale = true;
     c->nodes_on_device_newer = true;
-    c->st_root = kNoChild;  // the scene tree's bounds are not refit: stale until the next build
+    if (acc && c->titem_ref && c->n_titems > 0) {
+        hipLaunchKernelGGL(k_refresh_items, dim3((c->n_titems + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes,
+                           c->titem_ref, c->n_titems, c->titems);
+        HIP_TRY(hipGetLastError());
+    }
     if (!rebuild) return RT_OK;
     ++c->anim_rebuilds;
     return upload_accel(c);  // a bound changed kind: rebuild from the grown nodes

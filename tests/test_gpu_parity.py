@@ -654,3 +654,44 @@ def test_alternating_dispatches_stay_exact(ctx):
                     bad = int((img != refs[key]).any(axis=-1).sum())
                     assert bad == 0, f"iteration {it} config {cfg} shape {k} tail {tail}: {bad} pixels differ"
     ctx.set_tail(-1)
+
+
+@pytest.mark.parametrize("cfg", [3, 2])
+def test_animated_scene_tree_equals_reference_tree(ctx, cfg):
+    """Animated scenes keep the scene tree (rt_animate refits its boxes, items and,
+    for unbounded shapes, opens its kNoPrune part): full frames after each refit
+    equal the reference-tree walk bit for bit, and the oracle on a band. Config 3:
+    the four wheels turn (updateWheelAnimations, src/main.cpp:1084-1109); config 2:
+    its spheres bounce (bounceSphere, :1079-1082) and the floor wall slides."""
+    W, H = (1920, 1080) if cfg == 3 else (800, 600)
+    fs = rtamd.generate(cfg, 0, W, H)
+    if cfg == 3:
+        ids = np.arange(3380, 3380 + 640, dtype=np.int32)
+    else:
+        types = fs.shapes["type"]
+        ids = np.concatenate([np.where(types == 0)[0][:8], np.where(types == 2)[0]]).astype(np.int32)
+    ref = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    ctx.upload(fs)
+    mb = CFG_BOUNCES[cfg]
+    ctx.set_params(W, H, mb, True)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    ctx.set_animated(ids)
+    assert ctx.accel_info()["scene_tree"] == 1
+    out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    for k, rec in enumerate(_animation_steps(fs, ids, 3, renormal=False)):
+        ref.shapes[ids] = rec
+        oracle.update_bvh(ref, ids)
+        ctx.animate(rec)
+        frames = []
+        for tree in (rtamd.TREE_SCENE, rtamd.TREE_REFERENCE):
+            ctx.set_tree(tree)
+            torch.cuda.synchronize()
+            ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+            ctx.sync()
+            frames.append(out.cpu().numpy())
+        ctx.set_tree(rtamd.TREE_SCENE)
+        assert np.array_equal(frames[0], frames[1]), f"step {k}"
+        y0 = H // 2 - 8
+        want, _ = oracle.render(ref, W, H, oracle.params(W, H, mb), y0=y0, out_rows=16)
+        check(frames[0][y0:y0 + 16], want, f"animated step {k}")
+    assert ctx.debug_anim_rebuilds() >= 0
