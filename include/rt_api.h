@@ -158,6 +158,15 @@ int rt_dispatch(struct rt_ctx* ctx, int width, int height, int y0, int y1);
 int rt_dispatch_rows(struct rt_ctx* ctx, int width, int height, int y0, int stripe,
                      int step, int out_rows, float* dst, size_t pitch);
 
+/* rt_dispatch_rows with an output format: RT_FORMAT_RGBA32F (16 B per pixel, as
+ * the reference's image2D rgba32f) or RT_FORMAT_RGB32F (12 B per pixel, packed;
+ * the alpha the reference stores is always 1, gpu_shader.comp:437,623). The
+ * multi-GPU gather (rt_group.h) sends RGB32F: 25 % fewer bytes over xGMI.
+ * pitch >= 12*width and 4-byte aligned for RGB32F. */
+enum rt_format { RT_FORMAT_RGBA32F = 0, RT_FORMAT_RGB32F = 1 };
+int rt_dispatch_rows_fmt(struct rt_ctx* ctx, int width, int height, int y0, int stripe, int step, int out_rows,
+                         float* dst, size_t pitch, int format);
+
 /* glMemoryBarrier + wait: blocks until the context's stream is drained. */
 int rt_sync(struct rt_ctx* ctx);
 

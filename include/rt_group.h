@@ -7,8 +7,9 @@
  * reads no other pixel), so a group splits the frame's rows over its ranks:
  * rank r of P renders the interleaved stripe set
  *     { image row y : (y / stripe) mod P == r }
- * (rt_dispatch_rows with y0 = r*stripe, step = P) into a compact buffer of
- * rows_max = max over ranks of its row count. One fan-in per frame brings the
+ * (rt_dispatch_rows_fmt with y0 = r*stripe, step = P) into a compact packed-RGB
+ * buffer (12 B per pixel: the alpha is always 1) of rows_max = max over ranks of
+ * its row count. One fan-in per frame brings the
  * P buffers to rank 0 — ncclGather over xGMI (RCCL) or device copies — and a
  * kernel on rank 0 scatters the stripes back into image order in rank 0's
  * pitched RGBA32F surface. Interleaving balances sky rows against rows through

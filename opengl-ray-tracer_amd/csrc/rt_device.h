@@ -104,6 +104,7 @@ struct KParams {
     int tail_rx, tail_regions;               // 64x64-pixel regions: per row, total (one counter each)
     int tail_counters;                       // counters per set (>= tail_regions; all zeroed for the next)
     int tail_max_lanes;                      // a wave queues its rays only if at most this many are alive
+    int rgb;                                 // 1: packed RGB32F output, 12 B per pixel (rt_dispatch_rows_fmt)
     float shadow_off;                        // k_accel's shadow-ray offset: 1e-3 (BVH branch, gpu_shader.comp:469);
                                              // 1e-5 when it renders the brute branch (:565, rt_ctx::brute)
 };
@@ -269,6 +270,13 @@ __device__ __forceinline__ GeoRec load_rec(const float4* __restrict__ base, int 
 
 // Writes the pixel for output row r, column x.
 __device__ __forceinline__ void store_px(const KParams& kp, int r, int x, float4 v) {
+    if (kp.rgb) {  // alpha is always 1 (gpu_shader.comp:437,623): the multi-GPU gather sends 12 B per pixel
+        float* p = reinterpret_cast<float*>(kp.dst + static_cast<size_t>(r) * kp.pitch) + 3 * x;
+        __builtin_nontemporal_store(v.x, p);
+        __builtin_nontemporal_store(v.y, p + 1);
+        __builtin_nontemporal_store(v.z, p + 2);
+        return;
+    }
     float4* row = reinterpret_cast<float4*>(kp.dst + static_cast<size_t>(r) * kp.pitch);
     // streaming store (one global_store_dwordx4 ... nt): the kernel never reads the image
     // back, so it should not displace the scene records from L2 (config 3 -1.1 %, config 2 -1.7 %)

@@ -4,12 +4,13 @@
 // The reference's frame is one glDispatchCompute(W, H, 1) (src/main.cpp:352-354)
 // whose invocations read no other pixel (gpu_shader.comp:434-623). Rank r of P
 // renders rows { y : (y / stripe) mod P == r } through rt_dispatch_rows into a
-// compact [rows_max][W] float4 buffer on its own stream. The fan-in is one
-// ncclGather per frame (every rank sends rows_max*W*16 bytes; RCCL moves them
+// compact [rows_max][W] packed-RGB buffer on its own stream (alpha is always 1,
+// so 12 B per pixel). The fan-in is one ncclGather per frame (every rank sends
+// rows_max*W*12 bytes; RCCL moves them
 // over xGMI, each peer on its own link), or, in one process with repeated
 // devices, peer copies into rank 0's staging. k_unstripe then scatters the
 // P slots back into image order in rank 0's pitched surface: one coalesced
-// read and one streaming write per pixel (2 x 33 MB at 1080p, ~10 us).
+// read and one streaming write per pixel (25 + 33 MB at 1080p, ~10 us).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -27,7 +28,7 @@ struct Member {
     int rank = 0, device = 0;
     rt_ctx* ctx = nullptr;
     hipStream_t stream = nullptr;
-    float* buf = nullptr;  // compact stripes, rows_max x W float4
+    float* buf = nullptr;  // compact stripes, rows_max x W packed RGB32F (12 B per pixel)
     size_t buf_cap = 0;    // bytes
     ncclComm_t comm = nullptr;
     hipEvent_t rendered = nullptr;  // copy transport: this member's stripes are in buf
@@ -41,8 +42,9 @@ int stripe_rows(int height, int nranks, int stripe, int rank) {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// out[y][x] = slot k = (y / stripe) % P, its compact row (y / stripe / P) * stripe + y % stripe.
-__global__ __launch_bounds__(256) void k_unstripe(const f4v* __restrict__ staging, int rows_max, int width,
+// out[y][x] = slot k = (y / stripe) % P, its compact row (y / stripe / P) * stripe + y % stripe;
+// the slots hold packed RGB (rt_dispatch_rows_fmt RGB32F), the image RGBA with alpha 1.
+__global__ __launch_bounds__(256) void k_unstripe(const float* __restrict__ staging, int rows_max, int width,
                                                    int stripe, int nranks, f4v* __restrict__ img, size_t pitch_f4) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int y = blockIdx.y;
@@ -50,7 +52,9 @@ __global__ __launch_bounds__(256) void k_unstripe(const f4v* __restrict__ stagin
     const int band = y / stripe;
     const int k = band % nranks;
     const int r = (band / nranks) * stripe + (y - band * stripe);
-    const f4v v = __builtin_nontemporal_load(&staging[(static_cast<size_t>(k) * rows_max + r) * width + x]);
+    const float* p = staging + 3 * ((static_cast<size_t>(k) * rows_max + r) * width + x);
+    const f4v v = {__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2),
+                   1.0f};
     __builtin_nontemporal_store(v, &img[static_cast<size_t>(y) * pitch_f4 + x]);
 }
 
@@ -267,7 +271,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     if (!g || width <= 0 || height <= 0 || stripe <= 0 || height > 65535) return RT_ERR_INVALID;
     const int P = g->nranks;
     const int rows_max = stripe_rows(height, P, stripe, 0);  // rank 0 owns the most rows
-    const size_t slot = static_cast<size_t>(rows_max) * width * 16;
+    const size_t slot = static_cast<size_t>(rows_max) * width * 12;  // packed RGB32F
     // (Re)size the buffers; a resize waits for the frames that still use them.
     bool resize = false;
     for (Member& b : g->m) resize = resize || b.buf_cap < slot;
@@ -305,13 +309,13 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         if (g->transport == RT_GATHER_COPY && g->gathered_valid)
             G_HIP(hipStreamWaitEvent(b.stream, g->gathered, 0));  // root has read the previous frame's buf
         const int rows = stripe_rows(height, P, stripe, b.rank);
-        const int rc = rt_dispatch_rows(b.ctx, width, height, b.rank * stripe, stripe, P, rows, b.buf,
-                                        static_cast<size_t>(width) * 16);
+        const int rc = rt_dispatch_rows_fmt(b.ctx, width, height, b.rank * stripe, stripe, P, rows, b.buf,
+                                            static_cast<size_t>(width) * 12, RT_FORMAT_RGB32F);
         if (rc != RT_OK) return rc;
     }
     // 2. fan-in to rank 0's staging, slot k = rank k
     if (g->transport == RT_GATHER_RCCL) {
-        const size_t count = static_cast<size_t>(rows_max) * width * 4;
+        const size_t count = static_cast<size_t>(rows_max) * width * 3;
         G_NCCL(ncclGroupStart());
         for (Member& b : g->m) {
             const ncclResult_t r = ncclGather(b.buf, b.rank == 0 ? g->staging : nullptr, count, ncclFloat32, 0,
@@ -342,7 +346,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         Member& r = g->m[g->root];
         G_HIP(hipSetDevice(r.device));
         hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, height), dim3(256), 0, r.stream,
-                           reinterpret_cast<const f4v*>(g->staging), rows_max, width, stripe, P,
+                           g->staging, rows_max, width, stripe, P,
                            reinterpret_cast<f4v*>(g->img), g->img_pitch / 16);
         G_HIP(hipGetLastError());
     }

@@ -2456,10 +2456,12 @@ size_t sched_set_words(int tiles) {
 }
 
 int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
-                 size_t pitch, KParams& kp) {
+                 size_t pitch, KParams& kp, int format = RT_FORMAT_RGBA32F) {
     if (!c->have_scene || !c->have_cam || !c->have_light) return RT_ERR_NO_SCENE;
+    const size_t px = format == RT_FORMAT_RGB32F ? 12 : 16, align = format == RT_FORMAT_RGB32F ? 4 : 16;
     if (width <= 0 || height <= 0 || stripe <= 0 || step <= 0 || out_rows < 0 || y0 < 0 || !dst ||
-        pitch < static_cast<size_t>(width) * 16 || (pitch % 16) != 0)
+        (format != RT_FORMAT_RGBA32F && format != RT_FORMAT_RGB32F) || pitch < static_cast<size_t>(width) * px ||
+        (pitch % align) != 0 || (reinterpret_cast<uintptr_t>(dst) % align) != 0)
         return RT_ERR_INVALID;
     std::memset(&kp, 0, sizeof kp);
     kp.geo_leaf = c->geo_leaf;
@@ -2496,6 +2498,7 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step,
     kp.dst = reinterpret_cast<char*>(dst);
     kp.pitch = pitch;
     kp.shadow_off = 1e-3f;
+    kp.rgb = format == RT_FORMAT_RGB32F ? 1 : 0;
     return RT_OK;
 }
 
@@ -2607,7 +2610,8 @@ int render(rt_ctx* c, const KParams& kp) {
         if (!nxt) break;
         KParams kn;
         const int rc = fill_kparams(nxt, kt.width, kt.height, kt.y0, kt.stripe, kt.step, kt.out_rows,
-                                    reinterpret_cast<float*>(kt.dst), kt.pitch, kn);
+                                    reinterpret_cast<float*>(kt.dst), kt.pitch, kn,
+                                    kt.rgb ? RT_FORMAT_RGB32F : RT_FORMAT_RGBA32F);
         if (rc != RT_OK) return rc;
         kn.shadow_off = off;
         t = nxt;
@@ -3196,9 +3200,14 @@ int rt_set_kernel(rt_ctx* c, int kernel) {
 
 int rt_dispatch_rows(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
                      size_t pitch) {
+    return rt_dispatch_rows_fmt(c, width, height, y0, stripe, step, out_rows, dst, pitch, RT_FORMAT_RGBA32F);
+}
+
+int rt_dispatch_rows_fmt(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
+                         size_t pitch, int format) {
     if (!c) return RT_ERR_INVALID;
     KParams kp;
-    int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, dst, pitch, kp);
+    int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, dst, pitch, kp, format);
     if (rc != RT_OK) return rc;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     return render(c, kp);

@@ -186,6 +186,7 @@ RT_SYMBOLS = {
     "rt_set_params": (_I, [_P, _P]), "rt_set_kernel": (_I, [_P, _I]),
     "rt_dispatch": (_I, [_P, _I, _I, _I, _I]),
     "rt_dispatch_rows": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t]),
+    "rt_dispatch_rows_fmt": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I]),
     "rt_sync": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
     "rt_device_image": (_I, [_P, _P, _P]),
     "rt_collect_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
@@ -497,6 +498,11 @@ class ComputeShader:
     def dispatch_rows(self, width, height, y0, stripe, step, out_rows, dst_ptr, pitch):
         self._chk(self._lib.rt_dispatch_rows(self._h, width, height, y0, stripe, step, out_rows,
                                              C.c_void_p(dst_ptr), pitch), "rt_dispatch_rows")
+
+    def dispatch_rows_rgb(self, width, height, y0, stripe, step, out_rows, dst_ptr, pitch):
+        """rt_dispatch_rows_fmt with RT_FORMAT_RGB32F: packed 12-byte pixels."""
+        self._chk(self._lib.rt_dispatch_rows_fmt(self._h, width, height, y0, stripe, step, out_rows,
+                                                 C.c_void_p(dst_ptr), pitch, 1), "rt_dispatch_rows_fmt")
 
     def sync(self):
         self._chk(self._lib.rt_sync(self._h), "rt_sync")

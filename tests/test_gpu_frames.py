@@ -309,3 +309,21 @@ def test_mt_cameras_vs_oracle(ctx, name):
     img = render_mt(ctx, fs, W, H, 3, True, rtamd.KERNEL_AUTO)
     ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, True, False, True))
     check(img, ref, name)
+
+
+def test_rgb_format_equals_rgba(ctx):
+    """rt_dispatch_rows_fmt(RT_FORMAT_RGB32F): packed 12-byte pixels equal the RGBA
+    image's RGB (alpha is always 1); a pitch below 12*W is refused."""
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    rgba = render(ctx, fs, W, H, 3)
+    y0, rows = 400, 136
+    out = torch.full((rows, W * 3), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows_rgb(W, H, y0, 8, 1, rows, out.data_ptr(), W * 12)
+    ctx.sync()
+    got = out.cpu().numpy().reshape(rows, W, 3)
+    assert np.array_equal(got, rgba[y0:y0 + rows, :, :3])
+    assert (rgba[..., 3] == 1).all()
+    with pytest.raises(rtamd.RTError):
+        ctx.dispatch_rows_rgb(W, H, y0, 8, 1, rows, out.data_ptr(), W * 12 - 4)
