@@ -318,7 +318,8 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         const size_t count = static_cast<size_t>(rows_max) * width * 3;
         G_NCCL(ncclGroupStart());
         for (Member& b : g->m) {
-            const ncclResult_t r = ncclGather(b.buf, b.rank == 0 ? g->staging : nullptr, count, ncclFloat32, 0,
+            // recvbuff is only read at the root; the others pass their own buffer (never null)
+            const ncclResult_t r = ncclGather(b.buf, b.rank == 0 ? g->staging : b.buf, count, ncclFloat32, 0,
                                               b.comm, b.stream);
             if (r != ncclSuccess) {
                 ncclGroupEnd();
