@@ -296,7 +296,8 @@ def main():
     if use_group:
         for _ in range(F):
             uid = [rtamd.group_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
+            if world > 1:
+                dist.broadcast_object_list(uid, src=0)
             g = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local)
             g.upload(fs)
             g.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)

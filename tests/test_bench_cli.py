@@ -27,3 +27,17 @@ def test_gpus_2_from_a_plain_invocation(mode):
     assert out["n_gpus"] == 2 and out["ranks_seen"] == 2
     assert out["scaling"] == ("strong" if mode == "strong" else "weak")
     assert out["value"] > 0 and out["roofline"]["frac"] < 1
+
+
+def test_strong_mode_over_rt_group_one_rank():
+    """The N > 1 default's code path (rt_group per frame in flight, ncclCommInitRank,
+    ncclGather, unstripe) with one rank: the 1-GPU rehearsal of what the driver's
+    8-GPU run measures."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "strong", "--steps", "5",
+                        "--warmup", "2", "--no-cpu"], env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert out["mode"] == "strong" and out["scaling"] == "strong" and out["n_gpus"] == 1
+    assert out["gather"].startswith("rt_group") and out["frames_in_flight"] >= 2
+    assert out["value"] > 0
