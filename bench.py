@@ -44,6 +44,8 @@ as `reference_equivalent_GBps` (work the accelerator skips; not a bandwidth).
 from __future__ import annotations
 
 import argparse
+import contextlib
+import ctypes
 import json
 import os
 import socket
@@ -95,6 +97,23 @@ def parse(argv=None):
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo: rehearse the N>1 path with every rank on one GPU")
     return ap.parse_args(argv)
+
+
+@contextlib.contextmanager
+def quiet_stdout():
+    """Route the C-level stdout to stderr while RCCL initialises: it prints a
+    version banner there, and rank 0's stdout must hold only the JSON line."""
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    libc.fflush(None)
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        libc.fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 def free_port():
@@ -261,7 +280,8 @@ def main():
         dist.init_process_group("gloo")
     elif world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        with quiet_stdout():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -298,7 +318,8 @@ def main():
             uid = [rtamd.group_unique_id() if rank == 0 else None]
             if world > 1:
                 dist.broadcast_object_list(uid, src=0)
-            g = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local)
+            with quiet_stdout():
+                g = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local)
             g.upload(fs)
             g.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             g.members[0].set_kernel(kernel_id)

@@ -37,7 +37,9 @@ def test_strong_mode_over_rt_group_one_rank():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "strong", "--steps", "5",
                         "--warmup", "2", "--no-cpu"], env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, lines[:5]  # stdout is the JSON line alone (RCCL's banner goes to stderr)
+    out = json.loads(lines[0])
     assert out["mode"] == "strong" and out["scaling"] == "strong" and out["n_gpus"] == 1
     assert out["gather"].startswith("rt_group") and out["frames_in_flight"] >= 2
     assert out["value"] > 0
