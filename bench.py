@@ -266,6 +266,34 @@ def main():
         raise SystemExit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    gloo = a.backend == "gloo"
+    mode = a.mode if a.mode != "auto" else ("strong" if world > 1 else "frames")
+    if mode == "frames" and world > 1:
+        mode = "weak"
+    strong = mode == "strong"
+    use_group = strong and (a.gather == "rt" or (a.gather == "auto" and not gloo))
+    if use_group and gloo:
+        raise SystemExit("--gather rt needs the nccl backend (one GPU per rank)")
+    cfg, W, H, mb, desc, target = WORKLOADS[a.config]
+    # Frames in flight: enough of this rank's share of a frame to fill the GPU. A rank's
+    # share of a strong-scaled frame is too small (1/8 at 8 GPUs: ~4,000 tiles, its
+    # slowest pixels still ~0.22 ms), so strong mode keeps up to 8 frames in flight,
+    # each group on its own HIP stream; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
+    # queues (default 4) and streams sharing a queue run in order, so the queue count
+    # is raised to F before the runtime starts (measured on one rank's 1/8 share:
+    # 58 us/frame at F = 4 or 8 with 4 queues, 41 us at F = 8 with 8+ queues).
+    share_rows = -(-H // (world if strong else 1))
+    tiles = ((W + 7) // 8) * ((share_rows + 7) // 8)
+    if a.inflight > 0:
+        F = a.inflight
+    elif use_group:
+        F = min(8, max(2, -(-32768 // tiles)))
+    else:
+        F = min(4, max(2, -(-16384 // tiles) + 1))
+    if strong and not use_group:
+        F = 1  # the torch path gathers one shared buffer per step
+    if F > 4:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(F))
 
     import numpy as np
     import torch
@@ -274,7 +302,6 @@ def main():
     import rtamd  # noqa: E402
     import tiling  # noqa: E402
 
-    gloo = a.backend == "gloo"
     if world > 1 and gloo:
         torch.cuda.set_device(0)
         dist.init_process_group("gloo")
@@ -285,17 +312,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    mode = a.mode if a.mode != "auto" else ("strong" if world > 1 else "frames")
-    if mode == "frames" and world > 1:
-        mode = "weak"
-    strong = mode == "strong"
-    use_group = strong and (a.gather == "rt" or (a.gather == "auto" and not gloo))
-    if use_group and gloo:
-        raise SystemExit("--gather rt needs the nccl backend (one GPU per rank)")
     # torch's work (gathers on the torch path, the stats all_reduce) on one non-default stream
     torch.cuda.set_stream(torch.cuda.Stream())
 
-    cfg, W, H, mb, desc, target = WORKLOADS[a.config]
     sc = rtamd.Scene().generate(cfg, a.variant, W / H)
     sc_stats = sc.bvh_stats()
     if mode == "weak" and rank > 0:
@@ -306,10 +325,6 @@ def main():
     plan = tiling.StripePlan(H, world if strong else 1, a.stripe)
     prank = rank if strong else 0
     rows = plan.rows(prank)
-    tiles = ((W + 7) // 8) * ((rows + 7) // 8)
-    F = a.inflight if a.inflight > 0 else min(4, max(2, -(-16384 // tiles) + 1))
-    if strong and not use_group:
-        F = 1  # the torch path gathers one shared buffer per step
 
     # F frames in flight: F renderers per GPU (contexts or groups), each with its own stream
     groups, ctxs, bufs = [], [], []
@@ -426,6 +441,7 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": elapsed / a.steps * 1e3,
             "frames_in_flight": F,
+            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
             "serial_ms_per_step": (serial if serial is not None else elapsed) / a.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
