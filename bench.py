@@ -292,8 +292,9 @@ def main():
         F = min(4, max(2, -(-16384 // tiles) + 1))
     if strong and not use_group:
         F = 1  # the torch path gathers one shared buffer per step
-    if F > 4:
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(F))
+    hwq = os.environ.get("GPU_MAX_HW_QUEUES", "")
+    if F > (int(hwq) if hwq.isdigit() else 4):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(F)  # (the GPU box exports 4, HIP's default)
 
     import numpy as np
     import torch
