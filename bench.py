@@ -60,6 +60,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 # config -> (scene generator config, width, height, maxBounces, description, camera look-at target)
 # The targets are the generators' LookAt points (csrc/scene.cpp: gen_monkey :472, gen_car :549,
 # gen_random :570), about which the weak mode's camera orbit turns.
+SCHEDULES = {"rows": 0, "cost": 1, "xcd": 2}  # rtamd.SCHED_ROWS / SCHED_COST / SCHED_COST_XCD
 WORKLOADS = {
     2: (2, 800, 600, 1, "monkey stand-in (1,240 shapes), 800x600, primary + shadow", (0.0, 10.0, -8.0)),
     3: (3, 1920, 1080, 3, "car stand-in (4,022 triangles + 100 spheres), 1920x1080, reflection depth 3",
@@ -91,6 +92,8 @@ def parse(argv=None):
     ap.add_argument("--gather", default="auto", choices=["auto", "rt", "torch"],
                     help="strong mode's fan-in: rt = rt_group (RCCL ncclGather, C ABI); torch = "
                          "torch.distributed.gather (gloo rehearsals); auto = rt on nccl, torch on gloo")
+    ap.add_argument("--schedule", default="cost", choices=["cost", "xcd", "rows"],
+                    help="tile dispatch order (rt_set_schedule): cost (default), cost dealt to XCDs as bands, rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's cores (nproc)")
@@ -339,6 +342,7 @@ def main():
             g.upload(fs)
             g.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             g.members[0].set_kernel(kernel_id)
+            g.members[0].set_schedule(SCHEDULES[a.schedule])
             groups.append(g)
             ctxs.append(g.members[0])
     else:
@@ -349,6 +353,7 @@ def main():
             c_.upload(fs)
             c_.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             c_.set_kernel(kernel_id)
+            c_.set_schedule(SCHEDULES[a.schedule])
             ctxs.append(c_)
             bufs.append(torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev))
     ctx = ctxs[0]

@@ -207,8 +207,11 @@ int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
  * and the next dispatch with the same tile count starts the tiles in
  * decreasing order of those durations (longest first), so the frame is not
  * left waiting on expensive tiles that started late. The order only changes
- * when pixels are computed, never their values. */
-enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1 };
+ * when pixels are computed, never their values. RT_SCHED_COST_XCD: the same
+ * longest-first order, with each bucket of equal cost split into 8 screen
+ * bands, one per XCD (workgroups are dealt to the XCDs round-robin), so each
+ * XCD's L2 holds the records of one band at a time. */
+enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1, RT_SCHED_COST_XCD = 2 };
 int rt_set_schedule(struct rt_ctx* ctx, int mode);
 
 /* Ray compaction in the accelerated kernel: the rays still alive after bounce

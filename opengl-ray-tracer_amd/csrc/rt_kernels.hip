@@ -1232,6 +1232,7 @@ constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
 // buckets of a tile's work; the render kernel counts them per group of
 // kOrderThreads tiles (one k_tile_order workgroup each).
 constexpr int kOrderBuckets = 32, kOrderThreads = 256;
+constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
 
 __device__ __forceinline__ int work_bucket(unsigned c) {
     if (c < 2u) return 0;
@@ -1527,10 +1528,10 @@ __global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __re
 __global__ __launch_bounds__(kOrderThreads) void k_tile_order(const unsigned* __restrict__ cost, int n,
                                                               const unsigned* __restrict__ hist,
                                                               unsigned* __restrict__ next, int next_words,
-                                                              int* __restrict__ order) {
+                                                              int* __restrict__ order, int xcd) {
     constexpr int kPart = kOrderThreads / kOrderBuckets;  // threads per bucket for the row sums
     __shared__ unsigned tot[kPart][kOrderBuckets], pre[kPart][kOrderBuckets];
-    __shared__ unsigned start[kOrderBuckets], rank[kOrderBuckets];
+    __shared__ unsigned start[kOrderBuckets], rank[kOrderBuckets], base[kOrderBuckets], count[kOrderBuckets];
     const int t = threadIdx.x, j = blockIdx.x, groups = gridDim.x;
     {
         const int b = t % kOrderBuckets, part = t / kOrderBuckets;
@@ -1561,13 +1562,36 @@ __global__ __launch_bounds__(kOrderThreads) void k_tile_order(const unsigned* __
             const unsigned y = __shfl_down(x, off);
             if (t + off < kOrderBuckets) x += y;
         }
-        if (t < kOrderBuckets) start[t] = x - a + p;
+        if (t < kOrderBuckets) {
+            start[t] = x - a + p;
+            base[t] = x - a;
+            count[t] = a;
+        }
     }
     __syncthreads();
     const int i = j * kOrderThreads + t;
     if (i < n) {
         const int b = work_bucket(cost[i]);
-        order[start[b] + atomicAdd(&rank[b], 1u)] = i;
+        const unsigned pos = start[b] + atomicAdd(&rank[b], 1u);
+        if (!xcd) {
+            order[pos] = i;
+        } else {
+            // Workgroups go to the 8 XCDs round-robin (slot s on XCD s mod 8), and each
+            // XCD has its own L2. Deal the bucket's tiles (in group order, i.e. screen
+            // bands) as 8 contiguous chunks, chunk c to the slots base + c, base + 8 + c,
+            // ...: each XCD walks one band of the bucket at a time, and every XCD still
+            // gets an eighth of every bucket (same longest-first balance).
+            const unsigned cnt = count[b], q = cnt / kXcds, rem = cnt % kXcds, pb = pos - base[b];
+            unsigned c, k;
+            if (pb < rem * (q + 1)) {
+                c = pb / (q + 1);
+                k = pb % (q + 1);
+            } else {
+                c = rem + (pb - rem * (q + 1)) / q;
+                k = (pb - rem * (q + 1)) % q;
+            }
+            order[base[b] + kXcds * k + c] = i;
+        }
     }
 }
 
@@ -2682,7 +2706,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         k2.tile_cost = nullptr;
         if (c->tile_order && c->tile_order_n == k2.tiles) {
             k2.tile_order = c->tile_order;
-        } else if (c->schedule == RT_SCHED_COST) {
+        } else if (c->schedule != RT_SCHED_ROWS) {
             if (c->sched_cap < k2.tiles) {
                 hipFree(c->sched_cost);
                 hipFree(c->sched_order);
@@ -2810,7 +2834,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             unsigned* next = c->sched_sets + (1 - c->sched_parity) * sched_set_words(c->sched_cap);
             hipLaunchKernelGGL(k_tile_order, dim3((k2.tiles + kOrderThreads - 1) / kOrderThreads), dim3(kOrderThreads),
                                0, c->stream, c->sched_cost, k2.tiles, set, next,
-                               static_cast<int>(sched_set_words(c->sched_cap)), c->sched_order);
+                               static_cast<int>(sched_set_words(c->sched_cap)), c->sched_order,
+                               c->schedule == RT_SCHED_COST_XCD ? 1 : 0);
             c->sched_parity = 1 - c->sched_parity;
             c->sched_valid = k2.tiles;
         }
@@ -3405,7 +3430,7 @@ extern "C" int rt_debug_lane_stack(rt_ctx* c, int n) {
 }
 
 extern "C" int rt_set_schedule(rt_ctx* c, int mode) {
-    if (!c || (mode != RT_SCHED_ROWS && mode != RT_SCHED_COST)) return RT_ERR_INVALID;
+    if (!c || mode < RT_SCHED_ROWS || mode > RT_SCHED_COST_XCD) return RT_ERR_INVALID;
     c->schedule = mode;
     c->sched_valid = 0;
     return RT_OK;

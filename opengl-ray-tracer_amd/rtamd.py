@@ -70,7 +70,7 @@ LIGHT_DTYPE = np.dtype({
 
 SPHERE, PLANE, WALL, TRIANGLE = 0, 1, 2, 3
 KERNEL_AUTO, KERNEL_LANE, KERNEL_PACKET, KERNEL_ACCEL = 0, 1, 2, 3
-SCHED_ROWS, SCHED_COST = 0, 1
+SCHED_ROWS, SCHED_COST, SCHED_COST_XCD = 0, 1, 2
 TREE_REFERENCE, TREE_SCENE = 0, 1
 
 
@@ -579,7 +579,8 @@ class ComputeShader:
         self._chk(fn(self._h, int(lanes)), "rt_debug_tail_lanes")
 
     def set_schedule(self, mode):
-        """SCHED_COST (default): tiles start longest-first by their last duration; SCHED_ROWS: row-major."""
+        """SCHED_COST (default): tiles start longest-first by their last work; SCHED_COST_XCD: the same
+        order dealt to the 8 XCDs as screen bands; SCHED_ROWS: row-major."""
         self._chk(self._lib.rt_set_schedule(self._h, int(mode)), "rt_set_schedule")
 
     def debug_scene_stack(self, n):

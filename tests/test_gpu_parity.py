@@ -421,20 +421,27 @@ def test_walk_policies_identical(ctx, walk):
 
 
 @pytest.mark.gpu
-def test_cost_schedule_identical_images(ctx):
-    """rt_set_schedule: the cost-ordered dispatch (default) renders the same
-    image as row-major, frame after frame, and across a change of tile count."""
+@pytest.mark.parametrize("sched", [rtamd.SCHED_COST, rtamd.SCHED_COST_XCD])
+def test_cost_schedule_identical_images(ctx, sched):
+    """rt_set_schedule: the cost-ordered dispatch (default) and its XCD-banded
+    variant render the same image as row-major, frame after frame (every pixel
+    written: the surface is NaN before each dispatch), and across a change of
+    tile count."""
     fs = rtamd.generate(3, 0, 320, 180)
     ctx.upload(fs)
     ctx.set_params(320, 180, 3, True)
     ctx.set_kernel(rtamd.KERNEL_ACCEL)
     ctx.set_schedule(rtamd.SCHED_ROWS)
     ref = ctx.render(320, 180)
-    ctx.set_schedule(rtamd.SCHED_COST)
+    ctx.set_schedule(sched)
+    full = torch.empty((180, 320, 4), dtype=torch.float32, device="cuda")
     # dispatch 1 records tile work, 2-8 reuse its order with the counter-free kernel,
     # 9 records again (the order is re-derived every 8th dispatch)
     for _ in range(10):
-        assert np.array_equal(ctx.render(320, 180), ref)
+        full.fill_(float("nan"))
+        ctx.dispatch_rows(320, 180, 0, 1, 1, 180, full.data_ptr(), 320 * 16)
+        ctx.sync()
+        assert np.array_equal(full.cpu().numpy(), ref)
     band = ctx.render(320, 180)[40:120]
     out = torch.zeros((80, 320, 4), dtype=torch.float32, device="cuda")
     for _ in range(2):  # alternate tile counts: the order sets must stay consistent
@@ -443,6 +450,7 @@ def test_cost_schedule_identical_images(ctx):
         assert np.array_equal(out.cpu().numpy(), band)
         assert np.array_equal(ctx.render(320, 180), ref)
     ctx.set_kernel(rtamd.KERNEL_AUTO)
+    ctx.set_schedule(rtamd.SCHED_COST)
 
 
 @pytest.mark.gpu

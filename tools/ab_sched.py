@@ -1,0 +1,87 @@
+"""A/B of tile dispatch schedules in one process (rt_set_schedule): for each
+config, alternate the modes over several rounds (so clock drift hits both),
+with F frames in flight and one at a time, and check that every mode gives
+the same image as SCHED_COST.
+
+    python tools/ab_sched.py [--configs 3,5,2] [--modes 1,2] [--frames 200] [--rounds 4]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
+import rtamd  # noqa: E402
+
+WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 1920, 1080, 3)}
+ap = argparse.ArgumentParser()
+ap.add_argument("--configs", default="3,5,2")
+ap.add_argument("--modes", default="1,2")
+ap.add_argument("--frames", type=int, default=200)
+ap.add_argument("--rounds", type=int, default=4)
+ap.add_argument("--inflight", type=int, default=2)
+a = ap.parse_args()
+modes = [int(m) for m in a.modes.split(",")]
+out = {}
+for cfg in [int(x) for x in a.configs.split(",")]:
+    scene, W, H, mb = WL[cfg]
+    fs = rtamd.generate(scene, 0, W, H)
+    F = a.inflight
+    # one set of F contexts for every mode (modes switch between timed runs), so
+    # that no mode gets streams the others lack
+    ctxs, bufs = [], []
+    for _ in range(F):
+        s = torch.cuda.Stream()
+        c = rtamd.ComputeShader(0)
+        c.set_stream(s.cuda_stream)
+        c.upload(fs)
+        c.set_params(W, H, mb, True)
+        ctxs.append((c, s))
+        bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
+    torch.cuda.synchronize()
+
+    def run(n, f):
+        for i in range(n):
+            c, _ = ctxs[i % f]
+            c.set_camera(fs.camera)
+            c.set_light(fs.light)
+            c.dispatch_rows(W, H, 0, 1, 1, H, bufs[i % f].data_ptr(), W * 16)
+            if f == 1:
+                torch.cuda.synchronize()
+
+    res = {m: {"inflight": [], "serial": []} for m in modes}
+    img = {}
+    for _ in range(a.rounds):
+        for m in modes:
+            torch.cuda.synchronize()
+            for c, _ in ctxs:
+                c.set_schedule(m)
+            run(10 * F, F)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            run(a.frames, F)
+            torch.cuda.synchronize()
+            res[m]["inflight"].append((time.perf_counter() - t0) / a.frames * 1e3)
+            t0 = time.perf_counter()
+            run(a.frames // 2, 1)
+            res[m]["serial"].append((time.perf_counter() - t0) / (a.frames // 2) * 1e3)
+            img[m] = bufs[0].clone()
+    torch.cuda.synchronize()
+    same = {m: bool(torch.equal(img[m], img[modes[0]])) for m in modes}
+    out[cfg] = {
+        m: {
+            "ms_inflight_min": min(r["inflight"]),
+            "ms_inflight_med": sorted(r["inflight"])[len(r["inflight"]) // 2],
+            "ms_serial_min": min(r["serial"]),
+            "ms_serial_med": sorted(r["serial"])[len(r["serial"]) // 2],
+            "image_equal": same[m],
+        }
+        for m, r in res.items()
+    }
+    for c, _ in ctxs:
+        c.close()
+    print(json.dumps({"config": cfg, "F": F, "modes": out[cfg]}), flush=True)
