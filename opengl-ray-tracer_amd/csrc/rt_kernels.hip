@@ -546,6 +546,8 @@ struct AccelPtrs {
     int N;
     float origin_lim;                   // AccelHost::origin_lim
     int boxes_finite;                   // no reference node box holds a NaN (ray_aabb_fast)
+    int split_max;                      // lane_walk_any: split walks of waves with <= this many rays (0: off)
+    int split_g;                        // ... over groups of at most this many lanes (a power of two)
 };
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
@@ -892,6 +894,14 @@ __device__ __forceinline__ void sort4(Kids4& k) {
     cas(k, 1, 2);
 }
 
+// k.code[i] / k.t[i] for a lane-varying i (selects, no indexed registers)
+__device__ __forceinline__ int pick_code(const Kids4& k, int i) {
+    return i == 0 ? k.code[0] : i == 1 ? k.code[1] : i == 2 ? k.code[2] : k.code[3];
+}
+__device__ __forceinline__ float pick_t(const Kids4& k, int i) {
+    return i == 0 ? k.t[0] : i == 1 ? k.t[1] : i == 2 ? k.t[2] : k.t[3];
+}
+
 // Stacked entry parameters are kept as bf16 rounded toward zero: never above
 // the true value (te >= 0), so the pop-time prune only ever drops less.
 __device__ __forceinline__ unsigned short f_bf16_down(float t) {
@@ -904,9 +914,22 @@ __device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_flo
 // the nearer child in registers and stacking the farther one; the wave then
 // tests all lanes' leaves together. A stacked entry is dropped on pop when a
 // nearer hit has been found since it was pushed.
+//
+// Split walks (sg > 1, lane_walk_any): the sg lanes of an aligned group walk one
+// ray. From the root (a prologue before the main loop, so the loop's registers
+// are not raised) they share a path (ss lanes, this lane the si-th) and test
+// its nodes with a fixed limit (tl0), so every lane of the share sees
+// the same children; a node with h hit children hands child p to the lanes
+// si * h / ss == p (h < ss) or lane si the children si, si + ss, ... (h >= ss,
+// its own from then on). Every child is walked by some lane, leaves of the
+// shared part by all of them. The lanes' best distances are pooled after every
+// round of leaf tests (and a shadow hit ends the group's walks); the result is
+// the (distance, rank) minimum over the group, which does not depend on which
+// lane tested which leaf.
 template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool SPEC = true, bool MT = false>
 __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
-                          int* stk, unsigned short* stt, int stride, int cap, WalkCount& wc) {
+                          int* stk, unsigned short* stt, int stride, int cap, WalkCount& wc, int sg = 1,
+                          int si = 0) {
     if (A.N <= 0 || !active) return;
     const V inv = inv_dir(r.d);
     const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
@@ -926,6 +949,64 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
     } else if (A.nfew > 0) {
         fm = few_mask(A, r, inv);
     }
+    int start = 0, count = 0;  // the leaf range this lane holds (reset after each round's tests)
+    if (sg > 1) {
+        // Split: the shared top of the tree, out of the main loop (whose registers it
+        // does not add to). Shared nodes are tested with a fixed limit (tl0), so every
+        // lane of a share (ss lanes, this the si-th) sees the same children.
+        const float tl0 = SHADOW ? tl : INFINITY;
+        int ss = sg;
+        while (have && ss > 1) {
+            const unsigned uc = static_cast<unsigned>(cur);
+            if (uc & (kLeaf | kItem)) break;  // a leaf: the share tests it (and walks on) together
+            if (COUNT) wc.nodes++;
+            if (uc & kTopLeaf) {  // plain range + local root: hold the range, enter the root
+                if (count > 0) break;
+                const int4 lf = A.tleaf[uc & 0x0fffffffu];
+                start = lf.x;
+                count = lf.y;
+                have = lf.z != kNoChild;
+                cur = lf.z;
+            } else if (uc & kLocal) {
+                Kids4 w = wide_kids<MT>(A, uc, c, tl0, true);
+                sort4(w);
+                const int h = (w.t[0] < INFINITY) + (w.t[1] < INFINITY) + (w.t[2] < INFINITY) + (w.t[3] < INFINITY);
+                if (h == 0) {
+                    have = false;
+                } else if (h >= ss) {  // positions si and si + ss (ss >= 2, h <= 4) are this lane's
+                    if (si + ss < h) {
+                        if (sp < pcap) {
+                            stk[sp * stride] = pick_code(w, si + ss);
+                            stt[sp * stride] = f_bf16_down(pick_t(w, si + ss));
+                            ++sp;
+                        } else {
+                            ovf = true;
+                        }
+                    }
+                    cur = pick_code(w, si);
+                    ss = 1;
+                } else {  // child p, shared by the lanes [lo, hi) of this share
+                    const int p = si * h / ss, lo = (p * ss + h - 1) / h, hi = ((p + 1) * ss + h - 1) / h;
+                    cur = pick_code(w, p);
+                    si -= lo;
+                    ss = hi - lo;
+                }
+            } else {
+                const Kids k = ref_kids(A, uc, r, inv, c, tl0, true, fast);
+                if (k.ha && k.hb) {  // two children over ss >= 2 lanes
+                    const bool a_first = !(k.tb < k.ta);
+                    const int p = si * 2 / ss, lo = (p * ss + 1) / 2, hi = ((p + 1) * ss + 1) / 2;
+                    cur = (p == 0) == a_first ? k.ca : k.cb;
+                    si -= lo;
+                    ss = hi - lo;
+                } else if (k.ha || k.hb) {
+                    cur = k.ha ? k.ca : k.cb;
+                } else {
+                    have = false;
+                }
+            }
+        }
+    }
     bool ended = false;
     for (;;) {
         // While-while: a lane descends until it holds a leaf. SPEC (speculative):
@@ -933,7 +1014,6 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
         // for one; a lane that meets a second leaf parks on it (kept for the next
         // round), and the round ends when every walking lane holds a leaf
         // (measured: config 3 -4 %, config 5 -14 %).
-        int start = 0, count = 0;
         if (!ended) {
             for (;;) {
                 if (SPEC ? __ballot(!ended && count == 0) == 0 : count > 0) break;
@@ -1023,13 +1103,92 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
             if (SHADOW) {
                 if (try_shadow<MT>(g, r, lim_shadow)) {
                     shadow = true;
-                    return;
+                    if (sg == 1) return;
+                    ended = true;  // split: the group learns it below
+                    break;
                 }
             } else {
                 try_closest<MT>(g, start + i, r, b);
             }
         }
-        if (!SHADOW) tl = rta::t_limit(b.d, c.rdl);
+        count = 0;
+        if (sg > 1) {  // every lane of the wave's groups is here (the returns above are wave-uniform)
+            if (SHADOW) {
+                int any = shadow ? 1 : 0;
+                for (int o = 1; o < sg; o <<= 1) any |= __shfl_xor(any, o);
+                if (any) {
+                    shadow = true;
+                    ended = true;
+                }
+            } else {
+                float d = b.d;
+                for (int o = 1; o < sg; o <<= 1) d = fminf(d, __shfl_xor(d, o));
+                tl = rta::t_limit(d, c.rdl);
+            }
+        } else if (!SHADOW) {
+            tl = rta::t_limit(b.d, c.rdl);
+        }
+    }
+}
+
+// lane_walk for a wave's rays. A wave with few rays (at most A.split_max, e.g. the
+// reflections of a tile where little is a mirror) gives each ray a group of idle
+// lanes that split its walk (lane_walk, sg > 1): the longest walk of the wave gets
+// shorter, and the wave issues fewer rounds. The group's result is the lexicographic
+// (distance, rank) minimum of its lanes' -- the same hit as one lane's whole walk.
+// One lane_walk either way (one copy of the walk in the kernel). b must hold the
+// same value in every lane (bounce_step's fresh best); on return it holds each
+// active lane's result and r each active lane's own ray (both are rebuilt from the
+// group, so neither is live across the walk).
+// SPLIT = false compiles the plain walk alone: the split's registers spill in the
+// car's production kernel (+8 % per frame there, r02m), so only the kernels of
+// big scenes (the compacting k_accel instance and k_accel_tail) carry it.
+template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool SPEC = true, bool MT = false, bool SPLIT = true>
+__device__ __forceinline__ void lane_walk_any(const AccelPtrs& A, Ray& r, bool active, float lim_shadow, Best& b,
+                                              bool& shadow, int* stk, unsigned short* stt, int stride, int cap,
+                                              WalkCount& wc) {
+    if (!SPLIT) {  // the plain walk, without the split's registers
+        lane_walk<SHADOW, COUNT, WSTAT, SPEC, MT>(A, r, active, lim_shadow, b, shadow, stk, stt, stride, cap, wc);
+        return;
+    }
+    const unsigned long long m = __ballot(active);
+    const int n = __popcll(m);
+    int G = 1;
+    while (G < A.split_g && 2 * G * n <= 64) G *= 2;
+    if (n == 0 || n > A.split_max) G = 1;  // wave-uniform
+    const int lane = lane_id();
+    int src = lane;  // the ray this lane walks
+    bool walk = active;
+    if (G > 1) {
+        const int j = lane / G;
+        int q = 0;  // the j-th ray of the wave (wave-uniform loop over m's bits)
+        for (unsigned long long mm = m; mm; mm &= mm - 1ull, ++q)
+            if (q == j) src = __builtin_ctzll(mm);
+        walk = j < n;
+    }
+    Ray rr{mk(__shfl(r.o.x, src), __shfl(r.o.y, src), __shfl(r.o.z, src)),
+           mk(__shfl(r.d.x, src), __shfl(r.d.y, src), __shfl(r.d.z, src))};
+    const float ls = __shfl(lim_shadow, src);
+    bool sh = false;
+    lane_walk<SHADOW, COUNT, WSTAT, SPEC, MT>(A, rr, walk, ls, b, sh, stk, stt, stride, cap, wc, G, lane % G);
+    // the group lane holding this lane's result (recomputed here: nothing extra live through the walk)
+    const int from = G > 1 ? G * __popcll(__ballot(active) & ((1ull << lane) - 1ull)) : lane;
+    if (SHADOW) {
+        int any = sh ? 1 : 0;
+        for (int o = 1; o < G; o <<= 1) any |= __shfl_xor(any, o);
+        any = __shfl(any, from);
+        if (active && any) shadow = true;
+    } else {
+        for (int o = 1; o < G; o <<= 1) {
+            const float d = __shfl_xor(b.d, o);
+            const int sq = __shfl_xor(b.seq, o), sl = __shfl_xor(b.slot, o);
+            const V pp = mk(__shfl_xor(b.p.x, o), __shfl_xor(b.p.y, o), __shfl_xor(b.p.z, o));
+            if (lex_better(d, sq, b)) b = Best{d, sq, pp, sl};
+        }
+        b = Best{__shfl(b.d, from), __shfl(b.seq, from), mk(__shfl(b.p.x, from), __shfl(b.p.y, from), __shfl(b.p.z, from)),
+                 __shfl(b.slot, from)};
+        r = Ray{mk(__shfl(rr.o.x, from), __shfl(rr.o.y, from), __shfl(rr.o.z, from)),
+                mk(__shfl(rr.d.x, from), __shfl(rr.d.y, from), __shfl(rr.d.z, from))};
     }
 }
 
@@ -1232,6 +1391,8 @@ constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
 // buckets of a tile's work; the render kernel counts them per group of
 // kOrderThreads tiles (one k_tile_order workgroup each).
 constexpr int kOrderBuckets = 32, kOrderThreads = 256;
+// lane_walk_any defaults (rt_debug_split)
+constexpr int kSplitMax = 16, kSplitGroup = 8;
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
 
 __device__ __forceinline__ int work_bucket(unsigned c) {
@@ -1258,7 +1419,7 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
 // One bounce of gpu_shader.comp:450-517 for a wave's rays: closest hit, background
 // on a miss, the shadow ray, then Phong and the mirror ray (shade_bounce).
 // bg_y() gives the lane's image row (recomputed, not kept live through the walks).
-template <bool COUNT, bool SPEC, bool COST, bool MT, class BgY>
+template <bool COUNT, bool SPEC, bool COST, bool MT, bool SPLIT, class BgY>
 __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp,
                                             int depth, Ray& ray, bool& alive, V& acc, V& att, BgY bg_y, int* stk,
                                             unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
@@ -1268,7 +1429,8 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     WalkCount w0 = wc;
     unsigned long long c0 = COUNT ? clock64() : 0;
     if (lane_mode)
-        lane_walk<false, COST || COUNT, COUNT, SPEC, MT>(A, ray, alive, 0.f, best, unused, stk, stt, blockDim.x, cap, wc);
+        lane_walk_any<false, COST || COUNT, COUNT, SPEC, MT, SPLIT>(A, ray, alive, 0.f, best, unused, stk, stt,
+                                                                    blockDim.x, cap, wc);
     else
         packet_walk<false, COST || COUNT, COUNT, MT>(A, ray, alive, 0.f, best, unused, wc);
     if (COUNT) walk_rec(rec, 2 * depth, w0, wc, clock64() - c0);
@@ -1290,7 +1452,8 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     w0 = wc;
     c0 = COUNT ? clock64() : 0;
     if (depth >= kp.shadow_lane_from)
-        lane_walk<true, COST || COUNT, COUNT, SPEC, MT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk, stt, blockDim.x, cap, wc);
+        lane_walk_any<true, COST || COUNT, COUNT, SPEC, MT, SPLIT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk,
+                                                                   stt, blockDim.x, cap, wc);
     else
         packet_walk<true, COST || COUNT, COUNT, MT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
     if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
@@ -1331,7 +1494,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     }
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
-        bounce_step<COUNT, SPEC, COST, MT>(A, mat, kp, depth, ray, alive, acc, att,
+        bounce_step<COUNT, SPEC, COST, MT, TAIL>(A, mat, kp, depth, ray, alive, acc, att,
                                        [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec);
         if (TAIL && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
             // Compaction: the rays still alive go to the tail queue (one atomic per wave)
@@ -1494,7 +1657,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
         WalkCount wc{0u, 0u, 0u, 0u};
         for (int depth = kp.tail_from; depth < kp.maxBounces; ++depth) {
             if (__ballot(alive) == 0) break;
-            bounce_step<false, SPEC, false, false>(A, mat, kp, depth, ray, alive, acc, att,
+            bounce_step<false, SPEC, false, false, true>(A, mat, kp, depth, ray, alive, acc, att,
                                             [&]() { return image_row(kp, r); }, stk, stt, kp.lane_stack, wc, nullptr);
         }
         if (have) store_px(kp, r, x, make_float4(acc.x, acc.y, acc.z, 1.0f));
@@ -1887,6 +2050,7 @@ struct rt_ctx {
     int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
     int cone_cull = 1;
     int spec_mode = 1;  // speculative while-while in lane_walk (rt_debug_spec): 1 on, 0 off
+    int split_max = kSplitMax, split_g = kSplitGroup;  // split per-lane walks (rt_debug_split)
     int* tile_order = nullptr;  // diagnostics (rt_debug_tile_order): fixed dispatch order of the 8x8 tiles
     int tile_order_n = 0;
     // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
@@ -2557,6 +2721,8 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->lane_from_depth = c->lane_from_depth;
     b->cone_cull = c->cone_cull;
     b->spec_mode = c->spec_mode;
+    b->split_max = c->split_max;
+    b->split_g = c->split_g;
     b->schedule = c->schedule;
     b->sched_period = c->sched_period;
     b->tail_from = c->tail_from;
@@ -2763,7 +2929,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
 
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
-                          c->boxes_finite};
+                          c->boxes_finite, c->split_max, c->split_g};
         // compaction: bounces >= tail_from of the rays still alive run in k_accel_tail
         k2.tail_queue = nullptr;
         // RT_TAIL_AUTO: from bounce 2 on scenes of many scene-tree items (measured: config 5's
@@ -3453,6 +3619,15 @@ extern "C" int rt_debug_tile_order(rt_ctx* c, const int* order, int n) {
     if (hipMalloc(&c->tile_order, n * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
     HIP_TRY(hipMemcpy(c->tile_order, order, n * sizeof(int), hipMemcpyHostToDevice));
     c->tile_order_n = n;
+    return RT_OK;
+}
+
+// Diagnostics: split per-lane walks (lane_walk_any) of waves with at most max_rays rays
+// over groups of at most group lanes (a power of two, 2..64); max_rays = 0 turns it off.
+extern "C" int rt_debug_split(rt_ctx* c, int max_rays, int group) {
+    if (!c || max_rays < 0 || max_rays > 32 || group < 2 || group > 64 || (group & (group - 1))) return RT_ERR_INVALID;
+    c->split_max = max_rays;
+    c->split_g = group;
     return RT_OK;
 }
 

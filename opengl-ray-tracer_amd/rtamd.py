@@ -617,6 +617,12 @@ class ComputeShader:
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(mode)), "rt_debug_spec")
 
+    def debug_split(self, max_rays, group=8):
+        """Split per-lane walks of waves with <= max_rays rays over groups of <= group lanes (0: off)."""
+        fn = self._lib.rt_debug_split
+        fn.argtypes = [_P, _I, _I]
+        self._chk(fn(self._h, int(max_rays), int(group)), "rt_debug_split")
+
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull
         fn.argtypes = [_P, _I]

@@ -642,6 +642,47 @@ def test_ray_compaction_exact(ctx, tail):
         ctx.set_tail(-1)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,W,H", [(3, 960, 540), (5, 640, 360)])
+def test_split_walks_exact(ctx, cfg, W, H):
+    """lane_walk_any: waves with few rays split each ray's walk over a group of idle
+    lanes (compacted kernels, rt_set_tail). Every split setting renders the unsplit
+    frame bit for bit: closest hits and shadows, the scene tree's overflow fallback
+    to the reference tree (scene stack capped at 2), Moller-Trumbore, and the oracle
+    on a band."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    p = oracle.params(W, H, 3)
+    try:
+        ctx.set_tail(2)
+        ctx.debug_split(0, 8)
+        ref = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+        for mx, g in [(16, 8), (32, 16), (32, 2), (8, 64), (32, 64)]:
+            ctx.debug_split(mx, g)
+            img = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+            assert np.array_equal(img, ref), f"split {mx}:{g}: {int((img != ref).any(axis=-1).sum())} pixels differ"
+        ctx.debug_scene_stack(2)
+        img = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
+        assert np.array_equal(img, ref), "split with scene-stack overflow"
+        ctx.debug_scene_stack(0)
+        ctx.set_tree(rtamd.TREE_REFERENCE)  # binary reference nodes in the shared part
+        assert np.array_equal(gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL), ref), "split, reference tree"
+        ctx.set_tree(rtamd.TREE_SCENE)
+        y0 = H // 2
+        o, _ = oracle.render(fs, W, H, p, y0=y0, out_rows=8)
+        check(img[y0:y0 + 8], o, "split vs oracle")
+        if cfg == 3:  # Moller-Trumbore (its own accelerator, settings inherited)
+            pm = oracle.params(W, H, 3, useMT=True)
+            ctx.debug_split(0, 8)
+            mref = gpu_rows(ctx, fs, W, H, pm, kernel=rtamd.KERNEL_ACCEL)
+            ctx.debug_split(32, 16)
+            assert np.array_equal(gpu_rows(ctx, fs, W, H, pm, kernel=rtamd.KERNEL_ACCEL), mref)
+    finally:
+        ctx.debug_split(16, 8)
+        ctx.debug_scene_stack(0)
+        ctx.set_tree(rtamd.TREE_SCENE)
+        ctx.set_tail(-1)
+
+
 def test_alternating_dispatches_stay_exact(ctx):
     """State carried between dispatches (cost order sets, counter-free dispatches,
     compaction counters by parity and region count) across changing dispatch

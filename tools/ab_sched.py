@@ -1,9 +1,11 @@
-"""A/B of tile dispatch schedules in one process (rt_set_schedule): for each
-config, alternate the modes over several rounds (so clock drift hits both),
-with F frames in flight and one at a time, and check that every mode gives
-the same image as SCHED_COST.
+"""A/B of walk settings in one process: for each config, alternate the modes
+over several rounds (so clock drift hits all), with F frames in flight and one
+at a time, and check that every mode gives the same image as the first.
 
     python tools/ab_sched.py [--configs 3,5,2] [--modes 1,2] [--frames 200] [--rounds 4]
+        modes: tile schedules (rt_set_schedule)
+    python tools/ab_sched.py --split 0:8,16:8,8:8
+        modes: split walks, max_rays:group (rt_debug_split; 0 = off)
 """
 import argparse
 import json
@@ -24,8 +26,18 @@ ap.add_argument("--modes", default="1,2")
 ap.add_argument("--frames", type=int, default=200)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--inflight", type=int, default=2)
+ap.add_argument("--split", default="")
 a = ap.parse_args()
-modes = [int(m) for m in a.modes.split(",")]
+modes = a.split.split(",") if a.split else [int(m) for m in a.modes.split(",")]
+
+
+def apply(c, m):
+    if a.split:
+        mx, g = (int(v) for v in m.split(":"))
+        c.debug_split(mx, g)
+    else:
+        c.set_schedule(m)
+
 out = {}
 for cfg in [int(x) for x in a.configs.split(",")]:
     scene, W, H, mb = WL[cfg]
@@ -59,7 +71,7 @@ for cfg in [int(x) for x in a.configs.split(",")]:
         for m in modes:
             torch.cuda.synchronize()
             for c, _ in ctxs:
-                c.set_schedule(m)
+                apply(c, m)
             run(10 * F, F)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
