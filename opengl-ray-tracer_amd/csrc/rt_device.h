@@ -88,6 +88,8 @@ struct KParams {
     unsigned long long* __restrict__ tile_times;  // optional: start/end wall clock per tile
     int tiles_x, tiles;                      // 8x8 tiles per row, total
     const int* __restrict__ tile_order;      // optional dispatch order of the tiles (rt_set_schedule)
+    int heavy_k, heavy_parts;                // the first heavy_k tiles of tile_order run as heavy_parts
+                                             // waves each, one band of 64/heavy_parts pixels per wave
     unsigned* __restrict__ tile_cost;        // optional: each tile's work (rt_set_schedule)
     unsigned* __restrict__ sched_hist;       // with tile_cost: work-bucket histogram copies of this frame
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane

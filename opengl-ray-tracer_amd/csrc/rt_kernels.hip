@@ -1393,6 +1393,8 @@ constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
 constexpr int kOrderBuckets = 32, kOrderThreads = 256;
 // lane_walk_any defaults (rt_debug_split)
 constexpr int kSplitMax = 16, kSplitGroup = 8;
+// the heaviest tiles of the cost order as several waves (rt_debug_heavy)
+constexpr int kHeavyTiles = -1, kHeavyParts = 4, kHeavyAutoSlots = 2;  // -1: auto
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
 
 __device__ __forceinline__ int work_bucket(unsigned c) {
@@ -1468,7 +1470,10 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
 // orders a later dispatch (rt_set_schedule). COUNT adds the per-walk records.
 template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
-                           int* stk, unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
+                           int part, int* stk, unsigned short* stt, int cap, WalkCount& wc,
+                           unsigned long long* rec) {
+    // part > 0: this wave renders band part - 1 of the tile (64 / heavy_parts lanes)
+    const bool mine = part == 0 || ((threadIdx.x & 63) * kp.heavy_parts >> 6) == part - 1;
     // Pixel coordinates and the background are recomputed where needed rather than
     // kept live through the walks (register pressure: they would be spilled).
     Ray ray;
@@ -1476,7 +1481,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     {
         const PixelCoord pc = tile_pixel(kp, tile);
         ray = primary_ray(kp, pc.x, pc.y);
-        alive = pc.active;
+        alive = pc.active && mine;
     }
     V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
     bool deferred = false;  // the lane's remaining bounces run in k_accel_tail
@@ -1521,7 +1526,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         }
     }
     const PixelCoord pc = tile_pixel(kp, tile);
-    if (pc.active && !deferred) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
+    if (pc.active && mine && !deferred) store_px(kp, pc.r, pc.x, make_float4(acc.x, acc.y, acc.z, 1.0f));
 }
 
 // PERSISTENT: each wave pulls tiles from one device counter until none is
@@ -1549,13 +1554,24 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         if (lane == 0) t = atomicAdd(kp.tile_counter, 1);
         tile = __shfl(t, 0);
     }
-    while (tile < kp.tiles) {
+    // dispatch slots: the heavy_k heaviest tiles (the head of the cost order) as heavy_parts
+    // waves each, then the rest of the order one wave per tile
+    const int hs = kp.heavy_k * kp.heavy_parts;
+    while (tile < kp.tiles + hs - kp.heavy_k) {
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
-        if (kp.tile_order) tile = kp.tile_order[tile];  // dispatch order -> image tile (a permutation)
+        int part = 0;
+        if (kp.tile_order) {  // dispatch order -> image tile (a permutation)
+            if (tile < hs) {
+                part = tile % kp.heavy_parts + 1;
+                tile = kp.tile_order[tile / kp.heavy_parts];
+            } else {
+                tile = kp.tile_order[tile - hs + kp.heavy_k];
+            }
+        }
         WalkCount wc{0u, 0u, 0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
-        accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, stk, stt, kp.lane_stack, wc, rec);
+        accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, part, stk, stt, kp.lane_stack, wc, rec);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1578,8 +1594,10 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 o[5] = mt;
             }
         }
-        if (COST && kp.tile_cost) {
-            const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
+        if (COST && kp.tile_cost && part <= 1) {
+            // a split tile's cost: its first band's, times the bands (one record per tile)
+            const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests) *
+                                            static_cast<unsigned long long>(part ? kp.heavy_parts : 1);
             const unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
             if (lane == 0) {
                 kp.tile_cost[tile] = wk;
@@ -2051,6 +2069,7 @@ struct rt_ctx {
     int cone_cull = 1;
     int spec_mode = 1;  // speculative while-while in lane_walk (rt_debug_spec): 1 on, 0 off
     int split_max = kSplitMax, split_g = kSplitGroup;  // split per-lane walks (rt_debug_split)
+    int heavy_k = kHeavyTiles, heavy_parts = kHeavyParts;  // heaviest tiles as several waves (rt_debug_heavy)
     int* tile_order = nullptr;  // diagnostics (rt_debug_tile_order): fixed dispatch order of the 8x8 tiles
     int tile_order_n = 0;
     // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
@@ -2687,6 +2706,8 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step,
     kp.pitch = pitch;
     kp.shadow_off = 1e-3f;
     kp.rgb = format == RT_FORMAT_RGB32F ? 1 : 0;
+    kp.heavy_k = 0;
+    kp.heavy_parts = 1;
     return RT_OK;
 }
 
@@ -2723,6 +2744,8 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->spec_mode = c->spec_mode;
     b->split_max = c->split_max;
     b->split_g = c->split_g;
+    b->heavy_k = c->heavy_k;
+    b->heavy_parts = c->heavy_parts;
     b->schedule = c->schedule;
     b->sched_period = c->sched_period;
     b->tail_from = c->tail_from;
@@ -2870,6 +2893,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                          : (c->tile_times ? k_accel<false, true, false> : k_accel<false, false, false>));
         k2.tile_order = nullptr;
         k2.tile_cost = nullptr;
+        k2.heavy_k = 0;
+        k2.heavy_parts = 1;
         if (c->tile_order && c->tile_order_n == k2.tiles) {
             k2.tile_order = c->tile_order;
         } else if (c->schedule != RT_SCHED_ROWS) {
@@ -2922,6 +2947,25 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces
                                ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
                                : 0;
+        if (k2.tile_order && k2.tile_order == c->sched_order) {
+            // heavy tiles: explicit (rt_debug_heavy) or auto. A frame of at most
+            // kHeavyAutoSlots waves per wave slot whose walks are all packets (config 2:
+            // 800x600, primary + shadow) is bound by its slowest tiles even with frames
+            // in flight, and a packet walks the union of its rays' nodes: the heaviest
+            // 1/256 of its tiles run as 8 waves of 8 rays (measured -20 %, r02n). Where
+            // per-lane walks dominate the slow tiles (the car's reflections) it loses.
+            int hk = c->heavy_k, hp = c->heavy_parts;
+            if (hk < 0) {
+                const bool small = k2.tiles <= kHeavyAutoSlots * c->cu_count * 16 &&
+                                   std::min(k2.lane_from_depth, k2.shadow_lane_from) >= k2.maxBounces;
+                hk = small ? std::max(16, k2.tiles / 256) : 0;
+                hp = small ? 8 : 1;
+            }
+            if (!c->persistent && !c->tile_times && hp > 1 && hk > 0) {
+                k2.heavy_k = std::min(hk, k2.tiles);
+                k2.heavy_parts = hp;
+            }
+        }
         // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
         // animated scenes keep it: rt_animate refits its boxes and items (prepare_animation)
         const int troot = c->tree_mode == RT_TREE_SCENE ? c->st_root : kNoChild;
@@ -2983,6 +3027,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             k2.tail_queue = nullptr;
         }
         const bool tail_on = k2.tail_queue != nullptr;
+        if (!c->persistent)  // every dispatch slot: the split heavy tiles' extra waves too
+            blocks = (k2.tiles + k2.heavy_k * (k2.heavy_parts - 1) + wpb - 1) / wpb;
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(64 * wpb), lds, c->stream, A, c->mat, k2);
         if (tail_on) {
             const size_t tlds = static_cast<size_t>(k2.lane_stack) * 64 * 6;
@@ -3619,6 +3665,16 @@ extern "C" int rt_debug_tile_order(rt_ctx* c, const int* order, int n) {
     if (hipMalloc(&c->tile_order, n * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
     HIP_TRY(hipMemcpy(c->tile_order, order, n * sizeof(int), hipMemcpyHostToDevice));
     c->tile_order_n = n;
+    return RT_OK;
+}
+
+// Diagnostics: the first k tiles of the cost order (the heaviest) each run as `parts`
+// waves (1, 2, 4 or 8), one band of 64 / parts pixels per wave; parts = 1: off;
+// k = -1: the default policy (kHeavyAutoSlots).
+extern "C" int rt_debug_heavy(rt_ctx* c, int k, int parts) {
+    if (!c || k < -1 || (parts != 1 && parts != 2 && parts != 4 && parts != 8)) return RT_ERR_INVALID;
+    c->heavy_k = k;
+    c->heavy_parts = parts;
     return RT_OK;
 }
 

@@ -623,6 +623,12 @@ class ComputeShader:
         fn.argtypes = [_P, _I, _I]
         self._chk(fn(self._h, int(max_rays), int(group)), "rt_debug_split")
 
+    def debug_heavy(self, k, parts):
+        """Run the k heaviest tiles of the cost order as `parts` waves each (parts 1: off)."""
+        fn = self._lib.rt_debug_heavy
+        fn.argtypes = [_P, _I, _I]
+        self._chk(fn(self._h, int(k), int(parts)), "rt_debug_heavy")
+
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull
         fn.argtypes = [_P, _I]

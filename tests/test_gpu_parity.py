@@ -454,6 +454,45 @@ def test_cost_schedule_identical_images(ctx, sched):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 320, 180, 3), (5, 320, 180, 3)])
+def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
+    """rt_debug_heavy: the heaviest tiles of the cost order run as 2/4/8 waves, one
+    band of pixels each. Frame after frame (cost-recording dispatches included),
+    every pixel is written (NaN-poisoned surface) with the row-major frame's value,
+    also on a stripe set (a rank's rows) and with compaction (config 5 queues rays
+    from the split waves)."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True)
+    ctx.set_kernel(rtamd.KERNEL_ACCEL)
+    try:
+        ctx.set_schedule(rtamd.SCHED_ROWS)
+        ref = ctx.render(W, H)
+        ctx.set_schedule(rtamd.SCHED_COST)
+        full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        for k, parts in [(-1, 4), (16, 8), (64, 4), (10 ** 6, 2), (7, 8)]:
+            ctx.debug_heavy(k, parts)
+            for _ in range(10):
+                full.fill_(float("nan"))
+                ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
+                ctx.sync()
+                img = full.cpu().numpy()
+                assert np.array_equal(img, ref), f"heavy {k}:{parts}: {int((img != ref).any(axis=-1).sum())} px"
+        rows = sum(min(8, H - y) for y in range(8, H, 24))  # rank 1 of 3, 8-row stripes
+        part = torch.empty((rows, W, 4), dtype=torch.float32, device="cuda")
+        want = np.concatenate([ref[y:y + 8] for y in range(8, H, 24)])
+        ctx.debug_heavy(32, 8)
+        for _ in range(10):
+            part.fill_(float("nan"))
+            ctx.dispatch_rows(W, H, 8, 8, 3, rows, part.data_ptr(), W * 16)
+            ctx.sync()
+            assert np.array_equal(part.cpu().numpy(), want)
+    finally:
+        ctx.debug_heavy(-1, 4)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kernel", [rtamd.KERNEL_ACCEL, rtamd.KERNEL_PACKET])
 def test_obj_scene_parity(ctx, kernel):
     """A scene read from OBJ text (rts_parse_obj: a subdivided sphere-ish blob

@@ -6,6 +6,8 @@ at a time, and check that every mode gives the same image as the first.
         modes: tile schedules (rt_set_schedule)
     python tools/ab_sched.py --split 0:8,16:8,8:8
         modes: split walks, max_rays:group (rt_debug_split; 0 = off)
+    python tools/ab_sched.py --heavy 0:1,256:4
+        modes: heaviest tiles as several waves, k:parts (rt_debug_heavy)
 """
 import argparse
 import json
@@ -27,12 +29,18 @@ ap.add_argument("--frames", type=int, default=200)
 ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--inflight", type=int, default=2)
 ap.add_argument("--split", default="")
+ap.add_argument("--heavy", default="", help="modes k:parts (rt_debug_heavy)")
+ap.add_argument("--bounces", type=int, default=0, help="maxBounces override (0: the config's)")
+ap.add_argument("--share", type=int, default=1, help="render rank 0's 8-row stripes of a P-rank frame")
 a = ap.parse_args()
-modes = a.split.split(",") if a.split else [int(m) for m in a.modes.split(",")]
+modes = (a.split or a.heavy).split(",") if (a.split or a.heavy) else [int(m) for m in a.modes.split(",")]
 
 
 def apply(c, m):
-    if a.split:
+    if a.heavy:
+        k, parts = (int(v) for v in m.split(":"))
+        c.debug_heavy(k, parts)
+    elif a.split:
         mx, g = (int(v) for v in m.split(":"))
         c.debug_split(mx, g)
     else:
@@ -41,7 +49,10 @@ def apply(c, m):
 out = {}
 for cfg in [int(x) for x in a.configs.split(",")]:
     scene, W, H, mb = WL[cfg]
+    mb = a.bounces or mb
     fs = rtamd.generate(scene, 0, W, H)
+    P = a.share
+    R = H if P == 1 else sum(min(8, max(0, H - y)) for y in range(0, H, 8 * P))  # rank 0's rows
     F = a.inflight
     # one set of F contexts for every mode (modes switch between timed runs), so
     # that no mode gets streams the others lack
@@ -53,7 +64,7 @@ for cfg in [int(x) for x in a.configs.split(",")]:
         c.upload(fs)
         c.set_params(W, H, mb, True)
         ctxs.append((c, s))
-        bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
+        bufs.append(torch.empty((R, W, 4), dtype=torch.float32, device="cuda"))
     torch.cuda.synchronize()
 
     def run(n, f):
@@ -61,7 +72,10 @@ for cfg in [int(x) for x in a.configs.split(",")]:
             c, _ = ctxs[i % f]
             c.set_camera(fs.camera)
             c.set_light(fs.light)
-            c.dispatch_rows(W, H, 0, 1, 1, H, bufs[i % f].data_ptr(), W * 16)
+            if P == 1:
+                c.dispatch_rows(W, H, 0, 1, 1, H, bufs[i % f].data_ptr(), W * 16)
+            else:
+                c.dispatch_rows(W, H, 0, 8, P, R, bufs[i % f].data_ptr(), W * 16)
             if f == 1:
                 torch.cuda.synchronize()
 
@@ -96,4 +110,4 @@ for cfg in [int(x) for x in a.configs.split(",")]:
     }
     for c, _ in ctxs:
         c.close()
-    print(json.dumps({"config": cfg, "F": F, "modes": out[cfg]}), flush=True)
+    print(json.dumps({"config": cfg, "F": F, "share": P, "modes": out[cfg]}), flush=True)
