@@ -283,8 +283,10 @@ def main():
     # slowest pixels still ~0.22 ms), so strong mode keeps up to 8 frames in flight,
     # each group on its own HIP stream; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
     # queues (default 4) and streams sharing a queue run in order, so the queue count
-    # is raised to F before the runtime starts (measured on one rank's 1/8 share:
-    # 58 us/frame at F = 4 or 8 with 4 queues, 41 us at F = 8 with 8+ queues).
+    # is raised to 2F (at most 32) before the runtime starts: torch's own stream takes
+    # one more. Measured on one rank's 1/8 share (tools/inflight_share.py, r02p):
+    # F = 8 gives 66 us/frame with 8 queues, 41 us with 16; 32 queues with F >= 16
+    # collapse (131-305 us).
     share_rows = -(-H // (world if strong else 1))
     tiles = ((W + 7) // 8) * ((share_rows + 7) // 8)
     if a.inflight > 0:
@@ -296,8 +298,8 @@ def main():
     if strong and not use_group:
         F = 1  # the torch path gathers one shared buffer per step
     hwq = os.environ.get("GPU_MAX_HW_QUEUES", "")
-    if F > (int(hwq) if hwq.isdigit() else 4):
-        os.environ["GPU_MAX_HW_QUEUES"] = str(F)  # (the GPU box exports 4, HIP's default)
+    if 2 * F > (int(hwq) if hwq.isdigit() else 4):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, 2 * F))  # (the GPU box exports 4, HIP's default)
 
     import numpy as np
     import torch
