@@ -88,6 +88,8 @@ struct KParams {
     unsigned long long* __restrict__ tile_times;  // optional: start/end wall clock per tile
     int tiles_x, tiles;                      // 8x8 tiles per row, total
     const int* __restrict__ tile_order;      // optional dispatch order of the tiles (rt_set_schedule)
+    int lane_k, lane_k_mode;                 // the first lane_k dispatch slots: camera rays (bit 0) /
+                                             // their shadows (bit 1) walk per lane
     int heavy_k, heavy_parts;                // the first heavy_k tiles of tile_order run as heavy_parts
                                              // waves each, one band of 64/heavy_parts pixels per wave
     unsigned* __restrict__ tile_cost;        // optional: each tile's work (rt_set_schedule)

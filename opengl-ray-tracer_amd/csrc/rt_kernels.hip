@@ -1424,10 +1424,11 @@ __device__ __forceinline__ void walk_rec(unsigned long long* rec, int slot, cons
 template <bool COUNT, bool SPEC, bool COST, bool MT, bool SPLIT, class BgY>
 __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp,
                                             int depth, Ray& ray, bool& alive, V& acc, V& att, BgY bg_y, int* stk,
-                                            unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec) {
+                                            unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec,
+                                            int lane_from, int shadow_from) {
     Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
     bool unused = false;
-    const bool lane_mode = depth >= kp.lane_from_depth;  // wave-uniform
+    const bool lane_mode = depth >= lane_from;  // wave-uniform
     WalkCount w0 = wc;
     unsigned long long c0 = COUNT ? clock64() : 0;
     if (lane_mode)
@@ -1453,7 +1454,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
     w0 = wc;
     c0 = COUNT ? clock64() : 0;
-    if (depth >= kp.shadow_lane_from)
+    if (depth >= shadow_from)
         lane_walk_any<true, COST || COUNT, COUNT, SPEC, MT, SPLIT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, stk,
                                                                    stt, blockDim.x, cap, wc);
     else
@@ -1471,7 +1472,10 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
 template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int part, int* stk, unsigned short* stt, int cap, WalkCount& wc,
-                           unsigned long long* rec) {
+                           unsigned long long* rec, bool heavy) {
+    // the heaviest slots (lane_k) may walk their camera rays / shadows per lane (lane_k_mode)
+    const int lane_from = heavy && (kp.lane_k_mode & 1) ? 0 : kp.lane_from_depth;
+    const int shadow_from = heavy && (kp.lane_k_mode & 2) ? 0 : kp.shadow_lane_from;
     // part > 0: this wave renders band part - 1 of the tile (64 / heavy_parts lanes)
     const bool mine = part == 0 || ((threadIdx.x & 63) * kp.heavy_parts >> 6) == part - 1;
     // Pixel coordinates and the background are recomputed where needed rather than
@@ -1500,7 +1504,8 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
         bounce_step<COUNT, SPEC, COST, MT, TAIL>(A, mat, kp, depth, ray, alive, acc, att,
-                                       [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec);
+                                       [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec, lane_from,
+                                       shadow_from);
         if (TAIL && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
             // Compaction: the rays still alive go to the tail queue (one atomic per wave)
             // per 64x64-pixel region (8x8 tiles), so a tail wave's rays come from one area
@@ -1561,6 +1566,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         unsigned long long t0 = 0;
         if (TIMED) t0 = wall_clock64();
         int part = 0;
+        const int slot = tile;
         if (kp.tile_order) {  // dispatch order -> image tile (a permutation)
             if (tile < hs) {
                 part = tile % kp.heavy_parts + 1;
@@ -1571,7 +1577,8 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         }
         WalkCount wc{0u, 0u, 0u, 0u};
         unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
-        accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, part, stk, stt, kp.lane_stack, wc, rec);
+        accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, part, stk, stt, kp.lane_stack, wc, rec,
+                                                slot < kp.lane_k);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
             unsigned long long sn = wc.nodes, st = wc.tests, mn = wc.nodes, mt = wc.tests;
@@ -1676,7 +1683,8 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
         for (int depth = kp.tail_from; depth < kp.maxBounces; ++depth) {
             if (__ballot(alive) == 0) break;
             bounce_step<false, SPEC, false, false, true>(A, mat, kp, depth, ray, alive, acc, att,
-                                            [&]() { return image_row(kp, r); }, stk, stt, kp.lane_stack, wc, nullptr);
+                                            [&]() { return image_row(kp, r); }, stk, stt, kp.lane_stack, wc, nullptr,
+                                            kp.lane_from_depth, kp.shadow_lane_from);
         }
         if (have) store_px(kp, r, x, make_float4(acc.x, acc.y, acc.z, 1.0f));
         if (kTailOneShot) break;  // one chunk per wave: no loop-carried state
@@ -2070,6 +2078,7 @@ struct rt_ctx {
     int spec_mode = 1;  // speculative while-while in lane_walk (rt_debug_spec): 1 on, 0 off
     int split_max = kSplitMax, split_g = kSplitGroup;  // split per-lane walks (rt_debug_split)
     int heavy_k = kHeavyTiles, heavy_parts = kHeavyParts;  // heaviest tiles as several waves (rt_debug_heavy)
+    int lane_k = -1, lane_k_mode = 2;  // heaviest slots' walk modes (rt_debug_lane_k; -1: auto)
     int* tile_order = nullptr;  // diagnostics (rt_debug_tile_order): fixed dispatch order of the 8x8 tiles
     int tile_order_n = 0;
     // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
@@ -2708,6 +2717,8 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step,
     kp.rgb = format == RT_FORMAT_RGB32F ? 1 : 0;
     kp.heavy_k = 0;
     kp.heavy_parts = 1;
+    kp.lane_k = 0;
+    kp.lane_k_mode = 0;
     return RT_OK;
 }
 
@@ -2746,6 +2757,8 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->split_g = c->split_g;
     b->heavy_k = c->heavy_k;
     b->heavy_parts = c->heavy_parts;
+    b->lane_k = c->lane_k;
+    b->lane_k_mode = c->lane_k_mode;
     b->schedule = c->schedule;
     b->sched_period = c->sched_period;
     b->tail_from = c->tail_from;
@@ -2944,7 +2957,24 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         k2.shadow_lane_from = c->shadow_walk_override >= 0 ? c->shadow_walk_override
                               : (big && c->lane_from_depth <= 1 ? 0 : c->lane_from_depth);
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
-        const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces
+        if (k2.tile_order && k2.tile_order == c->sched_order) {
+            // the first lane_k dispatch slots (the heaviest tiles): explicit (rt_debug_lane_k)
+            // or auto -- in frames that walk per lane anyway (LDS stacks allocated), the
+            // heaviest 1/128 of the tiles walk their camera rays' shadows per lane: shorter
+            // chains on the slowest tiles (car: serial -5.5 %, 2 in flight equal, r02q)
+            int lk = c->lane_k, lm = c->lane_k_mode;
+            if (lk < 0) {
+                const bool lanes = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces;
+                lk = lanes ? std::max(64, k2.tiles / 128) : 0;
+                lm = 2;
+            }
+            if (lk > 0 && lm > 0) {
+                k2.lane_k = lk;
+                k2.lane_k_mode = lm;
+            }
+        }
+        // LDS stacks for the per-lane walks (also those of the lane_k slots)
+        const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces || k2.lane_k > 0
                                ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
                                : 0;
         if (k2.tile_order && k2.tile_order == c->sched_order) {
@@ -3675,6 +3705,16 @@ extern "C" int rt_debug_heavy(rt_ctx* c, int k, int parts) {
     if (!c || k < -1 || (parts != 1 && parts != 2 && parts != 4 && parts != 8)) return RT_ERR_INVALID;
     c->heavy_k = k;
     c->heavy_parts = parts;
+    return RT_OK;
+}
+
+// Diagnostics: the first k dispatch slots of the cost order (the heaviest tiles) walk
+// their camera rays (mode bit 0) and / or the camera rays' shadow rays (bit 1) per lane;
+// k = -1: the default policy.
+extern "C" int rt_debug_lane_k(rt_ctx* c, int k, int mode) {
+    if (!c || k < -1 || mode < 0 || mode > 3) return RT_ERR_INVALID;
+    c->lane_k = k;
+    c->lane_k_mode = mode;
     return RT_OK;
 }
 

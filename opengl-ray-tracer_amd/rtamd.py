@@ -629,6 +629,12 @@ class ComputeShader:
         fn.argtypes = [_P, _I, _I]
         self._chk(fn(self._h, int(k), int(parts)), "rt_debug_heavy")
 
+    def debug_lane_k(self, k, mode):
+        """The first k dispatch slots walk camera rays (bit 0) / their shadows (bit 1) per lane."""
+        fn = self._lib.rt_debug_lane_k
+        fn.argtypes = [_P, _I, _I]
+        self._chk(fn(self._h, int(k), int(mode)), "rt_debug_lane_k")
+
     def debug_cone_cull(self, on):
         fn = self._lib.rt_debug_cone_cull
         fn.argtypes = [_P, _I]

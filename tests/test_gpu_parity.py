@@ -454,6 +454,34 @@ def test_cost_schedule_identical_images(ctx, sched):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 320, 180, 3)])
+def test_heaviest_slots_walk_per_lane_exact(ctx, cfg, W, H, mb):
+    """rt_debug_lane_k: the heaviest dispatch slots walk their camera rays and / or
+    their shadow rays per lane (LDS stacks even in an all-packet frame). Every pixel
+    equals the row-major frame's, frame after frame."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True)
+    ctx.set_kernel(rtamd.KERNEL_ACCEL)
+    try:
+        ctx.set_schedule(rtamd.SCHED_ROWS)
+        ref = ctx.render(W, H)
+        ctx.set_schedule(rtamd.SCHED_COST)
+        full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        for k, mode in [(64, 1), (64, 2), (10 ** 6, 3), (16, 2), (-1, 2), (0, 0)]:
+            ctx.debug_lane_k(k, mode)
+            for _ in range(10):
+                full.fill_(float("nan"))
+                ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
+                ctx.sync()
+                img = full.cpu().numpy()
+                assert np.array_equal(img, ref), f"lane_k {k}:{mode}: {int((img != ref).any(axis=-1).sum())} px"
+    finally:
+        ctx.debug_lane_k(-1, 2)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 320, 180, 3), (5, 320, 180, 3)])
 def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
     """rt_debug_heavy: the heaviest tiles of the cost order run as 2/4/8 waves, one

@@ -30,14 +30,19 @@ ap.add_argument("--rounds", type=int, default=4)
 ap.add_argument("--inflight", type=int, default=2)
 ap.add_argument("--split", default="")
 ap.add_argument("--heavy", default="", help="modes k:parts (rt_debug_heavy)")
+ap.add_argument("--lanek", default="", help="modes k:mode (rt_debug_lane_k)")
 ap.add_argument("--bounces", type=int, default=0, help="maxBounces override (0: the config's)")
 ap.add_argument("--share", type=int, default=1, help="render rank 0's 8-row stripes of a P-rank frame")
 a = ap.parse_args()
-modes = (a.split or a.heavy).split(",") if (a.split or a.heavy) else [int(m) for m in a.modes.split(",")]
+alt = a.split or a.heavy or a.lanek
+modes = alt.split(",") if alt else [int(m) for m in a.modes.split(",")]
 
 
 def apply(c, m):
-    if a.heavy:
+    if a.lanek:
+        k, mode = (int(v) for v in m.split(":"))
+        c.debug_lane_k(k, mode)
+    elif a.heavy:
         k, parts = (int(v) for v in m.split(":"))
         c.debug_heavy(k, parts)
     elif a.split:
