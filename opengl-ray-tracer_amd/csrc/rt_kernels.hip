@@ -909,6 +909,10 @@ __device__ __forceinline__ unsigned short f_bf16_down(float t) {
 }
 __device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_float(static_cast<unsigned>(b) << 16); }
 
+#ifndef RT_LEAF_PREFETCH
+#define RT_LEAF_PREFETCH 0  // lane_walk's leaf loop software-pipelined (experiment builds)
+#endif
+
 // Per-lane walk ("while-while"): each lane walks its own stack in LDS (code +
 // entry parameter per entry). A lane descends until it holds a leaf, keeping
 // the nearer child in registers and stacking the farther one; the wave then
@@ -1096,8 +1100,18 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
             }
         }
         if (__ballot(count > 0) == 0) return;  // every lane's walk finished
+#if RT_LEAF_PREFETCH
+        // the leaf's records software-pipelined: record i + 1's loads are in flight while
+        // record i is tested (a leaf is a chain of dependent loads otherwise)
+        GeoRec gn;
+        if (count > 0) gn = load_rec(A.prims, start);
+        for (int i = 0; i < count; ++i) {
+            const GeoRec g = gn;
+            if (i + 1 < count) gn = load_rec(A.prims, start + i + 1);
+#else
         for (int i = 0; i < count; ++i) {
             const GeoRec g = load_rec(A.prims, start + i);
+#endif
             if (COUNT) wc.tests++;
             if (WSTAT && first_active()) wc.wtests++;
             if (SHADOW) {

@@ -9,6 +9,6 @@ OUT=$ROOT/build_ab/$NAME
 mkdir -p "$OUT"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
   -fhip-fp32-correctly-rounded-divide-sqrt -w "$@" -o "$OUT/librtamd.so" \
-  "$ROOT/opengl-ray-tracer_amd/csrc/rt_kernels.hip" "$ROOT/opengl-ray-tracer_amd/csrc/lbvh.hip" \
-  "$ROOT/opengl-ray-tracer_amd/csrc/accel.cpp"
+  "$ROOT/opengl-ray-tracer_amd/csrc/rt_kernels.hip" "$ROOT/opengl-ray-tracer_amd/csrc/rt_group.hip" \
+  "$ROOT/opengl-ray-tracer_amd/csrc/lbvh.hip" "$ROOT/opengl-ray-tracer_amd/csrc/accel.cpp" -L/opt/rocm/lib -lrccl
 echo "$OUT/librtamd.so"
