@@ -554,12 +554,18 @@ struct AccelPtrs {
 constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u, kTopLeaf = 0x20000000u, kItem = 0x10000000u;
 constexpr int kNoChild = 0x7fffffff;
 
+// The closest hit so far: distance, rank in the reference walk, ray parameter and
+// record slot. The hit point is o + t d, recomputed from t after the walk: the same
+// float operations as where it was found, so the same bits (two registers fewer
+// through the walks than keeping the point).
 struct Best {
     float d;
     int seq;
-    V p;
+    float t;
     int slot;
 };
+
+__device__ __forceinline__ V hit_point(const Ray& r, float t) { return r.o + t * r.d; }
 
 __device__ __forceinline__ bool lex_better(float d, int seq, const Best& b) {
     return d < b.d || (d == b.d && seq < b.seq);
@@ -571,7 +577,7 @@ __device__ __forceinline__ bool lex_better(float d, int seq, const Best& b) {
 // win. Same result as testing first and comparing after.
 // Moller-Trumbore (gpu_shader.comp:170-195) with the same float operations as
 // intersect(): t > 0 gives INNER at o + t d, whatever the triangle's facing.
-__device__ __forceinline__ bool mt_hit(const float* f, const Ray& r, V& p) {
+__device__ __forceinline__ bool mt_hit(const float* f, const Ray& r, V& p, float& tt) {
     const V p1 = mk(f[4], f[5], f[6]), e1 = mk(f[7], f[8], f[9]), e2 = mk(f[10], f[11], f[12]);
     const V hh = cross(r.d, e2);
     const float a = dot(e1, hh);
@@ -585,7 +591,8 @@ __device__ __forceinline__ bool mt_hit(const float* f, const Ray& r, V& p) {
     if (v < 0.0f || u + v > 1.0f) return false;
     const float t = fi * dot(e2, q);
     if (!(t > 0.0f)) return false;
-    p = r.o + t * r.d;
+    p = hit_point(r, t);
+    tt = t;
     return true;
 }
 
@@ -595,9 +602,10 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
     const int seq = __float_as_int(f[17]);
     if (MT && g.type == 3) {
         V p;
-        if (!mt_hit(f, r, p)) return;
+        float t;
+        if (!mt_hit(f, r, p, t)) return;
         const float d = dist(r.o, p);
-        if (lex_better(d, seq, b)) b = Best{d, seq, p, slot};
+        if (lex_better(d, seq, b)) b = Best{d, seq, t, slot};
         return;
     }
     if (g.type == 0) {
@@ -610,9 +618,9 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
         if (D > 0.0f) {
             float t1 = (-bb - __builtin_sqrtf(D)) / (2.0f * aa);
             if (t1 > 0.0f) {
-                V p = r.o + t1 * r.d;
+                V p = hit_point(r, t1);
                 float d = dist(r.o, p);
-                if (lex_better(d, seq, b)) b = Best{d, seq, p, slot};
+                if (lex_better(d, seq, b)) b = Best{d, seq, t1, slot};
             }
         }
         return;
@@ -627,7 +635,7 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
     if (!(num > 0.0f)) return;
     const float t = num / np;
     if (!(t > 0.0f)) return;
-    V p = r.o + t * r.d;
+    V p = hit_point(r, t);
     float d = dist(r.o, p);
     if (!lex_better(d, seq, b)) return;
     if (g.type == 2) {
@@ -644,7 +652,7 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
         float u = 1.0f - v - w;
         if (u < 0.0f || v < 0.0f || w < 0.0f) return;
     }
-    b = Best{d, seq, p, slot};
+    b = Best{d, seq, t, slot};
 }
 
 // Shadow candidate: an INNER hit nearer than lim (gpu_shader.comp:473-480).
@@ -653,7 +661,8 @@ __device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float 
     const float* f = g.f;
     if (MT && g.type == 3) {
         V p;
-        return mt_hit(f, r, p) && dist(r.o, p) < lim;
+        float t;
+        return mt_hit(f, r, p, t) && dist(r.o, p) < lim;
     }
     if (g.type == 0) {
         V c = mk(f[0], f[1], f[2]);
@@ -909,6 +918,9 @@ __device__ __forceinline__ unsigned short f_bf16_down(float t) {
 }
 __device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_float(static_cast<unsigned>(b) << 16); }
 
+#ifndef RT_SPLIT_ALL
+#define RT_SPLIT_ALL 0  // split walks (lane_walk_any) in every k_accel instance (experiment builds)
+#endif
 #ifndef RT_LEAF_PREFETCH
 #define RT_LEAF_PREFETCH 0  // lane_walk's leaf loop software-pipelined (experiment builds)
 #endif
@@ -1196,11 +1208,10 @@ __device__ __forceinline__ void lane_walk_any(const AccelPtrs& A, Ray& r, bool a
         for (int o = 1; o < G; o <<= 1) {
             const float d = __shfl_xor(b.d, o);
             const int sq = __shfl_xor(b.seq, o), sl = __shfl_xor(b.slot, o);
-            const V pp = mk(__shfl_xor(b.p.x, o), __shfl_xor(b.p.y, o), __shfl_xor(b.p.z, o));
-            if (lex_better(d, sq, b)) b = Best{d, sq, pp, sl};
+            const float tt = __shfl_xor(b.t, o);
+            if (lex_better(d, sq, b)) b = Best{d, sq, tt, sl};
         }
-        b = Best{__shfl(b.d, from), __shfl(b.seq, from), mk(__shfl(b.p.x, from), __shfl(b.p.y, from), __shfl(b.p.z, from)),
-                 __shfl(b.slot, from)};
+        b = Best{__shfl(b.d, from), __shfl(b.seq, from), __shfl(b.t, from), __shfl(b.slot, from)};
         r = Ray{mk(__shfl(rr.o.x, from), __shfl(rr.o.y, from), __shfl(rr.o.z, from)),
                 mk(__shfl(rr.d.x, from), __shfl(rr.d.y, from), __shfl(rr.d.z, from))};
     }
@@ -1440,7 +1451,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
                                             int depth, Ray& ray, bool& alive, V& acc, V& att, BgY bg_y, int* stk,
                                             unsigned short* stt, int cap, WalkCount& wc, unsigned long long* rec,
                                             int lane_from, int shadow_from) {
-    Best best{1e20f, 0x7fffffff, mk(0.f, 0.f, 0.f), -1};
+    Best best{1e20f, 0x7fffffff, 0.f, -1};
     bool unused = false;
     const bool lane_mode = depth >= lane_from;  // wave-uniform
     WalkCount w0 = wc;
@@ -1460,12 +1471,13 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     Ray sr{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
     float ld = 0.f;
     if (alive) {
-        const V hn = shape_normal(load_rec(A.prims, best.slot), best.p);
-        sr = Ray{best.p + hn * kp.shadow_off, normalize(kp.light_pos - best.p)};
-        ld = dist(kp.light_pos, best.p);
+        const V hp = hit_point(ray, best.t);
+        const V hn = shape_normal(load_rec(A.prims, best.slot), hp);
+        sr = Ray{hp + hn * kp.shadow_off, normalize(kp.light_pos - hp)};
+        ld = dist(kp.light_pos, hp);
     }
     bool shadow = false;
-    Best dummy{0.f, 0, mk(0.f, 0.f, 0.f), -1};
+    Best dummy{0.f, 0, 0.f, -1};
     w0 = wc;
     c0 = COUNT ? clock64() : 0;
     if (depth >= shadow_from)
@@ -1476,8 +1488,8 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
     if (alive) {
         const GeoRec g = load_rec(A.prims, best.slot);
-        alive = shade_bounce(kp, ray, best.p, shape_normal(g, best.p), load_mat(mat, g.idx), shadow, acc, att,
-                             1e-3f);
+        const V hp = hit_point(ray, best.t);
+        alive = shade_bounce(kp, ray, hp, shape_normal(g, hp), load_mat(mat, g.idx), shadow, acc, att, 1e-3f);
     }
 }
 
@@ -1517,7 +1529,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
     }
     for (int depth = 0; depth < kp.maxBounces; ++depth) {
         if (__ballot(alive) == 0) break;
-        bounce_step<COUNT, SPEC, COST, MT, TAIL>(A, mat, kp, depth, ray, alive, acc, att,
+        bounce_step<COUNT, SPEC, COST, MT, TAIL || RT_SPLIT_ALL>(A, mat, kp, depth, ray, alive, acc, att,
                                        [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec, lane_from,
                                        shadow_from);
         if (TAIL && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
