@@ -260,6 +260,33 @@ def roofline(info, kname, k_ms, pixels, b_ref, pmc):
     return out
 
 
+def plan_inflight(inflight, W, H, world, strong, use_group, exported):
+    """Frames in flight F and the GPU_MAX_HW_QUEUES value to set (None: keep `exported`).
+
+    Enough of this rank's share of a frame to fill the GPU. A rank's share of a
+    strong-scaled frame is too small (1/8 at 8 GPUs: ~4,000 tiles, its slowest pixels
+    still ~0.22 ms), so strong mode keeps up to 8 frames in flight, each group on its own
+    HIP stream. HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (default 4) and
+    streams sharing a queue run in order, so the queue count is raised to 2F (at most 32)
+    before the runtime starts: torch's own stream takes one more. Measured on one rank's
+    1/8 share (tools/inflight_share.py, r02p): F = 8 gives 66 us/frame with 8 queues,
+    41 us with 16; 32 queues with F >= 16 collapse (131-305 us). Config 2 with F = 4:
+    0.049 ms with 4 queues, 0.033 with 8.
+    """
+    share_rows = -(-H // (world if strong else 1))
+    tiles = ((W + 7) // 8) * ((share_rows + 7) // 8)
+    if inflight > 0:
+        F = inflight
+    elif use_group:
+        F = min(8, max(2, -(-32768 // tiles)))
+    else:
+        F = min(4, max(2, -(-16384 // tiles) + 1))
+    if strong and not use_group:
+        F = 1  # the torch path gathers one shared buffer per step
+    have = int(exported) if str(exported).isdigit() else 4
+    return F, (str(min(32, 2 * F)) if 2 * F > have else None)
+
+
 def main():
     a = parse()
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
@@ -278,28 +305,10 @@ def main():
     if use_group and gloo:
         raise SystemExit("--gather rt needs the nccl backend (one GPU per rank)")
     cfg, W, H, mb, desc, target = WORKLOADS[a.config]
-    # Frames in flight: enough of this rank's share of a frame to fill the GPU. A rank's
-    # share of a strong-scaled frame is too small (1/8 at 8 GPUs: ~4,000 tiles, its
-    # slowest pixels still ~0.22 ms), so strong mode keeps up to 8 frames in flight,
-    # each group on its own HIP stream; HIP maps streams onto GPU_MAX_HW_QUEUES hardware
-    # queues (default 4) and streams sharing a queue run in order, so the queue count
-    # is raised to 2F (at most 32) before the runtime starts: torch's own stream takes
-    # one more. Measured on one rank's 1/8 share (tools/inflight_share.py, r02p):
-    # F = 8 gives 66 us/frame with 8 queues, 41 us with 16; 32 queues with F >= 16
-    # collapse (131-305 us).
-    share_rows = -(-H // (world if strong else 1))
-    tiles = ((W + 7) // 8) * ((share_rows + 7) // 8)
-    if a.inflight > 0:
-        F = a.inflight
-    elif use_group:
-        F = min(8, max(2, -(-32768 // tiles)))
-    else:
-        F = min(4, max(2, -(-16384 // tiles) + 1))
-    if strong and not use_group:
-        F = 1  # the torch path gathers one shared buffer per step
-    hwq = os.environ.get("GPU_MAX_HW_QUEUES", "")
-    if 2 * F > (int(hwq) if hwq.isdigit() else 4):
-        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, 2 * F))  # (the GPU box exports 4, HIP's default)
+    F, hw_queues = plan_inflight(a.inflight, W, H, world, strong, use_group,
+                                 os.environ.get("GPU_MAX_HW_QUEUES", ""))
+    if hw_queues is not None:
+        os.environ["GPU_MAX_HW_QUEUES"] = hw_queues  # before the HIP runtime starts
 
     import numpy as np
     import torch

@@ -77,3 +77,19 @@ def test_roofline_fraction_is_physical():
     r2 = bench.roofline(info, "k_accel", 0.3, 1920 * 1080, 8.5e11, None)
     assert r2["achieved"] == pytest.approx((16 * 1920 * 1080 + 1e6) / 0.3e-3 / 1e9)
     assert r2["traffic"] is None
+
+
+def test_inflight_plan_and_hardware_queues():
+    """Frames in flight per workload, and the hardware-queue count raised to 2F (<= 32)
+    so that the F renderer streams and torch's own stream do not share queues."""
+    # car, 1 GPU: 2 frames in flight, the box's 4 queues suffice
+    assert bench.plan_inflight(0, 1920, 1080, 1, False, False, "4") == (2, None)
+    # 800x600: 4 frames, 8 queues
+    assert bench.plan_inflight(0, 800, 600, 1, False, False, "4") == (4, "8")
+    # a rank's 1/8 stripe share over rt_group: 8 frames, 16 queues
+    assert bench.plan_inflight(0, 1920, 1080, 8, True, True, "4") == (8, "16")
+    # torch-gather strong path: one frame
+    assert bench.plan_inflight(0, 1920, 1080, 2, True, False, "4") == (1, None)
+    # an explicit F; never above 32 queues; an export that already suffices is kept
+    assert bench.plan_inflight(20, 1920, 1080, 1, False, False, "") == (20, "32")
+    assert bench.plan_inflight(8, 1920, 1080, 1, False, False, "16") == (8, None)
