@@ -428,6 +428,14 @@ def main():
 
     serial = timed(1) if F > 1 else None
     serial_kt = ctx.kernel_times() if F > 1 else None
+    # the same one-at-a-time frames with rt_set_latency_mode (what a host that waits for
+    # each frame would set); reported beside serial_ms_per_step, not used for the roofline
+    serial_lat = None
+    if F > 1 and not use_group:
+        ctx.set_latency_mode(1)
+        serial_lat = timed(1)
+        ctx.set_latency_mode(0)
+        ctx.kernel_times()
     elapsed = timed(F)
 
     kt_if = np.concatenate([c_.kernel_times() for c_ in ctxs])
@@ -460,6 +468,7 @@ def main():
             "frames_in_flight": F,
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
             "serial_ms_per_step": (serial if serial is not None else elapsed) / a.steps * 1e3,
+            "serial_ms_per_step_latency_mode": (serial_lat / a.steps * 1e3) if serial_lat is not None else None,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,

@@ -214,6 +214,15 @@ int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 enum rt_schedule { RT_SCHED_ROWS = 0, RT_SCHED_COST = 1, RT_SCHED_COST_XCD = 2 };
 int rt_set_schedule(struct rt_ctx* ctx, int mode);
 
+/* Latency mode, for a host that waits for each frame before the next (the
+ * reference's own loop, src/main.cpp:290-462) rather than keeping frames in
+ * flight. 1: the accelerated kernel's instance with split walks in sparse
+ * waves (idle lanes help a tile's few live rays) and, on frames not already
+ * split, the heaviest 1/512 of the tiles as two waves each. Shortens one frame
+ * (car: -6 to -8 %) and costs throughput when frames overlap. 0 (default): off.
+ * Same image either way. */
+int rt_set_latency_mode(struct rt_ctx* ctx, int on);
+
 /* Ray compaction in the accelerated kernel: the rays still alive after bounce
  * from_bounce - 1 are queued per 64x64-pixel region, and a second kernel runs
  * their remaining bounces 64 rays to a wave instead of in their half-empty tile

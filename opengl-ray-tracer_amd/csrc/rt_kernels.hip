@@ -2105,6 +2105,7 @@ struct rt_ctx {
     int split_max = kSplitMax, split_g = kSplitGroup;  // split per-lane walks (rt_debug_split)
     int heavy_k = kHeavyTiles, heavy_parts = kHeavyParts;  // heaviest tiles as several waves (rt_debug_heavy)
     int lane_k = -1, lane_k_mode = 2;  // heaviest slots' walk modes (rt_debug_lane_k; -1: auto)
+    int latency_mode = 0;              // rt_set_latency_mode
     int* tile_order = nullptr;  // diagnostics (rt_debug_tile_order): fixed dispatch order of the 8x8 tiles
     int tile_order_n = 0;
     // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
@@ -2785,6 +2786,7 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->heavy_parts = c->heavy_parts;
     b->lane_k = c->lane_k;
     b->lane_k_mode = c->lane_k_mode;
+    b->latency_mode = c->latency_mode;
     b->schedule = c->schedule;
     b->sched_period = c->sched_period;
     b->tail_from = c->tail_from;
@@ -3016,6 +3018,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                    std::min(k2.lane_from_depth, k2.shadow_lane_from) >= k2.maxBounces;
                 hk = small ? std::max(16, k2.tiles / 256) : 0;
                 hp = small ? 8 : 1;
+                if (!small && c->latency_mode) {  // rt_set_latency_mode: the heaviest 1/512 as 2 waves
+                    hk = std::max(16, k2.tiles / 512);
+                    hp = 2;
+                }
             }
             if (!c->persistent && !c->tile_times && hp > 1 && hk > 0) {
                 k2.heavy_k = std::min(hk, k2.tiles);
@@ -3077,8 +3083,14 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         } else if (kfn == k_accel<false, false, true>) {
             // production shape: the counter-free kernel on a dispatch that records no tile
             // work; the queueing kernel when the tail runs (other shapes: no compaction)
-            if (tail) kfn = k2.tile_cost ? k_accel<false, false, true, true, true> : k_accel<false, false, true, false, true>;
-            else if (!k2.tile_cost) kfn = k_accel<false, false, true, false>;
+            if (tail || c->latency_mode) {
+                // the compacting instance; in latency mode without a queue (tail_from 0), for
+                // its split walks in sparse waves (lane_walk_any), which the production
+                // instance leaves out for its registers
+                kfn = k2.tile_cost ? k_accel<false, false, true, true, true> : k_accel<false, false, true, false, true>;
+            } else if (!k2.tile_cost) {
+                kfn = k_accel<false, false, true, false>;
+            }
         } else if (tail) {
             k2.tail_queue = nullptr;
         }
@@ -3694,6 +3706,12 @@ extern "C" int rt_debug_sched_period(rt_ctx* c, int period) {
 extern "C" int rt_debug_lane_stack(rt_ctx* c, int n) {
     if (!c || n < 0 || n > kMaxStack) return RT_ERR_INVALID;
     c->lane_stack_override = n;
+    return RT_OK;
+}
+
+extern "C" int rt_set_latency_mode(rt_ctx* c, int on) {
+    if (!c || on < 0 || on > 1) return RT_ERR_INVALID;
+    c->latency_mode = on;
     return RT_OK;
 }
 

@@ -200,6 +200,7 @@ RT_SYMBOLS = {
     "rt_scene_size": (_I, [_P, _P, _P, _P]),
     "rt_read_indices": (_I, [_P, _P, _I]),
     "rt_set_schedule": (_I, [_P, _I]),
+    "rt_set_latency_mode": (_I, [_P, _I]),
     "rt_set_tail": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
@@ -577,6 +578,10 @@ class ComputeShader:
         fn = self._lib.rt_debug_tail_lanes
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(lanes)), "rt_debug_tail_lanes")
+
+    def set_latency_mode(self, on):
+        """rt_set_latency_mode: tune for one frame at a time (split walks, heaviest tiles as 2 waves)."""
+        self._chk(self._lib.rt_set_latency_mode(self._h, int(bool(on))), "rt_set_latency_mode")
 
     def set_schedule(self, mode):
         """SCHED_COST (default): tiles start longest-first by their last work; SCHED_COST_XCD: the same

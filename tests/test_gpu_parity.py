@@ -454,6 +454,34 @@ def test_cost_schedule_identical_images(ctx, sched):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 640, 360, 3), (5, 320, 180, 3)])
+def test_latency_mode_exact(ctx, cfg, W, H, mb):
+    """rt_set_latency_mode: the split-walk instance without a queue and the heaviest tiles
+    as two waves (or, on config 5, compaction as usual): every pixel equals the default
+    mode's frame, frame after frame, and the oracle on a band."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True)
+    ctx.set_kernel(rtamd.KERNEL_ACCEL)
+    try:
+        ref = ctx.render(W, H)
+        ctx.set_latency_mode(1)
+        full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        for _ in range(10):
+            full.fill_(float("nan"))
+            ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
+            ctx.sync()
+            img = full.cpu().numpy()
+            assert np.array_equal(img, ref), f"latency mode: {int((img != ref).any(axis=-1).sum())} px"
+        y0 = H // 2
+        o, _ = oracle.render(fs, W, H, oracle.params(W, H, mb), y0=y0, out_rows=8)
+        check(img[y0:y0 + 8], o, "latency mode vs oracle")
+    finally:
+        ctx.set_latency_mode(0)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 320, 180, 3)])
 def test_heaviest_slots_walk_per_lane_exact(ctx, cfg, W, H, mb):
     """rt_debug_lane_k: the heaviest dispatch slots walk their camera rays and / or

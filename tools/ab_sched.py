@@ -31,15 +31,18 @@ ap.add_argument("--inflight", type=int, default=2)
 ap.add_argument("--split", default="")
 ap.add_argument("--heavy", default="", help="modes k:parts (rt_debug_heavy)")
 ap.add_argument("--lanek", default="", help="modes k:mode (rt_debug_lane_k)")
+ap.add_argument("--latency", default="", help="modes 0/1 (rt_set_latency_mode)")
 ap.add_argument("--bounces", type=int, default=0, help="maxBounces override (0: the config's)")
 ap.add_argument("--share", type=int, default=1, help="render rank 0's 8-row stripes of a P-rank frame")
 a = ap.parse_args()
-alt = a.split or a.heavy or a.lanek
+alt = a.split or a.heavy or a.lanek or a.latency
 modes = alt.split(",") if alt else [int(m) for m in a.modes.split(",")]
 
 
 def apply(c, m):
-    if a.lanek:
+    if a.latency:
+        c.set_latency_mode(int(m))
+    elif a.lanek:
         k, mode = (int(v) for v in m.split(":"))
         c.debug_lane_k(k, mode)
     elif a.heavy:
