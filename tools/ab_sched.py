@@ -32,6 +32,7 @@ ap.add_argument("--split", default="")
 ap.add_argument("--heavy", default="", help="modes k:parts (rt_debug_heavy)")
 ap.add_argument("--lanek", default="", help="modes k:mode (rt_debug_lane_k)")
 ap.add_argument("--latency", default="", help="modes 0/1 (rt_set_latency_mode)")
+ap.add_argument("--with-latency", action="store_true", help="latency mode on under every mode")
 ap.add_argument("--bounces", type=int, default=0, help="maxBounces override (0: the config's)")
 ap.add_argument("--share", type=int, default=1, help="render rank 0's 8-row stripes of a P-rank frame")
 a = ap.parse_args()
@@ -71,6 +72,8 @@ for cfg in [int(x) for x in a.configs.split(",")]:
         c.set_stream(s.cuda_stream)
         c.upload(fs)
         c.set_params(W, H, mb, True)
+        if a.with_latency:
+            c.set_latency_mode(1)
         ctxs.append((c, s))
         bufs.append(torch.empty((R, W, 4), dtype=torch.float32, device="cuda"))
     torch.cuda.synchronize()
