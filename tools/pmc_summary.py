@@ -1,6 +1,10 @@
 """Summarise a tools/profile.sh run into profiles/.
 
-    python tools/pmc_summary.py gpurun_out/prof_TAG KEY [KERNEL_SUBSTR]
+    python tools/pmc_summary.py gpurun_out/prof_TAG KEY [KERNEL_SUBSTR | re:REGEX]
+
+The default bench command also runs a latency-mode pass (another k_accel
+instance): select the production instances with a regex, e.g.
+    re:k_accel<false, false, true, (true|false), false, false>
 
 Copies the rocprofv3 kernel-stats CSV to profiles/TAG_kernel_stats.csv and the
 per-dispatch FETCH_SIZE/WRITE_SIZE of the render kernel into
@@ -11,6 +15,7 @@ reports half the bytes of a wide coalesced read (MI355X_MICROARCH.md, HBM).
 import csv
 import json
 import os
+import re
 import shutil
 import sys
 
@@ -33,9 +38,13 @@ def find(sub, name):
 shutil.copy(find("trace", "kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
 
 
+def matches(name):
+    return re.search(kname[3:], name) is not None if kname.startswith("re:") else kname in name
+
+
 def per_launch(sub, counter):
     vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(find(sub, "counter_collection.csv")))
-            if kname in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if matches(r["Kernel_Name"]) and r["Counter_Name"] == counter]
     return sum(vals) / len(vals), len(vals)
 
 
