@@ -19,10 +19,12 @@ Modes (--mode auto = frames at N = 1, strong at N > 1):
           1080p, up to 4 for frames too small to fill the GPU);
   strong  the north star's multi-GPU frame: every step renders ONE
           1920x1080 frame split over the N GPUs by interleaved 8-row stripes and
-          gathers it to rank 0 through the C ABI's rt_group (ncclGather over
-          xGMI, then k_unstripe into rank 0's image) — total work fixed,
+          gathers it to rank 0 through the C ABI's rt_group (ncclSend/ncclRecv
+          over xGMI, then k_unstripe into rank 0's image) — total work fixed,
           scaling "strong". Frames in flight = several groups, dealt
-          round-robin, each with its own streams, buffers and communicator;
+          round-robin, each with its own streams, buffers and communicator.
+          Rank 0 may take 2 stripes per period (--root-share; auto times 1
+          and 2 before the measured steps): its rows never cross a link;
   weak    each rank renders its own whole frame per step (frame r of a 1-degree
           camera orbit about the config's look-at point), no collective.
 
@@ -90,8 +92,12 @@ def parse(argv=None):
                          "has fewer than 16k 8x8 tiles (too few waves to fill it)")
     ap.add_argument("--mode", default="auto", choices=["auto", "frames", "strong", "weak"])
     ap.add_argument("--gather", default="auto", choices=["auto", "rt", "torch"],
-                    help="strong mode's fan-in: rt = rt_group (RCCL ncclGather, C ABI); torch = "
+                    help="strong mode's fan-in: rt = rt_group (RCCL send/recv, C ABI); torch = "
                          "torch.distributed.gather (gloo rehearsals); auto = rt on nccl, torch on gloo")
+    ap.add_argument("--root-share", default="auto",
+                    help="strong mode over rt_group: rank 0's stripes per period of share + N - 1 "
+                         "(rt_group_set_root_share; rank 0's rows never cross a link); auto = the faster of "
+                         "1 and 2, timed on every rank before the measured steps")
     ap.add_argument("--schedule", default="cost", choices=["cost", "xcd", "rows"],
                     help="tile dispatch order (rt_set_schedule): cost (default), cost dealt to XCDs as bands, rows")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
@@ -369,16 +375,29 @@ def main():
             bufs.append(torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev))
     ctx = ctxs[0]
 
-    # Work of this rank's rows on the reference walk (counting kernel, untimed).
-    st = ctx.collect_stats(W, H, plan.y0(prank), a.stripe, plan.world, rows)
-    mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, rows * W, a.mt),
-                         st["hits"]],
-                        dtype=torch.float64, device="cpu" if gloo else dev)
-    total = mine.clone()
-    if world > 1:
-        dist.all_reduce(total)
-    rays_step = float(total[0] + total[1])  # all ranks' rays of one step
-    b_ref_rank = float(mine[2])
+    # Work of this rank's rows on the reference walk (counting kernel, untimed). Over
+    # rt_group the rows follow the root share, so rt_group_collect_stats counts them.
+    def count_work():
+        if use_group:
+            st = groups[0].collect_stats(W, H, a.stripe)
+            n = st["pixels"] // W
+        else:
+            st = ctx.collect_stats(W, H, plan.y0(prank), a.stripe, plan.world, rows)
+            n = rows
+        mine = torch.tensor([st["closest_rays"], st["shadow_rays"], rtamd.algorithmic_bytes(st, n * W, a.mt),
+                             st["hits"]],
+                            dtype=torch.float64, device="cpu" if gloo else dev)
+        total = mine.clone()
+        if world > 1:
+            dist.all_reduce(total)
+        return float(total[0] + total[1]), float(mine[2]), n  # all ranks' rays of one step
+
+    share = None
+    if use_group:
+        share = 1 if a.root_share == "auto" else int(a.root_share)
+        for g in groups:
+            g.set_root_share(share)
+    rays_step, b_ref_rank, rows = count_work()
 
     cam, light = fs.camera, fs.light
     anim = wheel_frames(fs, 64) if a.animate else None
@@ -393,7 +412,7 @@ def main():
             g = groups[i % inflight]
             g.set_camera(cam)    # SSBO 2 (src/main.cpp:328-330)
             g.set_light(light)   # SSBO 1 (:332-334)
-            g.dispatch(W, H, a.stripe)  # this rank's stripes + ncclGather + unstripe on rank 0
+            g.dispatch(W, H, a.stripe)  # this rank's stripes + send/recv to rank 0 + unstripe there
             return
         c_ = ctxs[i % inflight]
         c_.set_camera(cam)
@@ -426,6 +445,25 @@ def main():
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el[0])
 
+    # Root share (rt_group): with auto, every rank times the candidates the same way and
+    # takes the same (max-over-ranks) verdict; the counted rays do not depend on it.
+    share_probe = None
+    if use_group and a.root_share == "auto":
+        share_probe = {}
+        steps = a.steps
+        a.steps = max(4, 2 * F)
+        for k in ((1, 2) if world > 1 else (1,)):
+            for g in groups:
+                g.set_root_share(k)
+            share_probe[k] = timed(F) / a.steps * 1e3
+        a.steps = steps
+        best = min(share_probe, key=share_probe.get)
+        for g in groups:
+            g.set_root_share(best)
+        share = best
+        share_probe = {str(k): v for k, v in share_probe.items()}
+        rays_step, b_ref_rank, rows = count_work()  # this rank's rows at the chosen share
+
     serial = timed(1) if F > 1 else None
     serial_kt = ctx.kernel_times() if F > 1 else None
     # the same one-at-a-time frames with rt_set_latency_mode (what a host that waits for
@@ -453,7 +491,7 @@ def main():
         fps = frames / elapsed
         gather = None
         if strong:
-            gather = ("rt_group: ncclGather to rank 0 (RCCL over xGMI) + k_unstripe, C ABI (include/rt_group.h)"
+            gather = ("rt_group: ncclSend/ncclRecv to rank 0 (RCCL over xGMI) + k_unstripe, C ABI (include/rt_group.h)"
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
         toggles = (a.brute, a.mt, a.fresnel, a.variant, a.animate)
         pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}") if not any(toggles) and not strong else None
@@ -486,6 +524,8 @@ def main():
                                        f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"
                                        if mode == "weak" else "1 GPU")},
             "gather": gather,
+            "root_share": share,
+            "root_share_probe_ms": share_probe,
             "fps": fps,
             "mrays_primary_per_s": W * H * fps / 1e6,
             "rays_per_step": rays_step,

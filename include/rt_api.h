@@ -167,6 +167,13 @@ enum rt_format { RT_FORMAT_RGBA32F = 0, RT_FORMAT_RGB32F = 1 };
 int rt_dispatch_rows_fmt(struct rt_ctx* ctx, int width, int height, int y0, int stripe, int step, int out_rows,
                          float* dst, size_t pitch, int format);
 
+/* rt_dispatch_rows_fmt with the stripe spacing in rows: compact row r is image
+ * row y0 + (r / stripe) * period + r % stripe (period >= stripe; the forms above
+ * are period = stripe * step). Lets one rank own a wider stripe than the others
+ * in the same period (rt_group_set_root_share). */
+int rt_dispatch_rows_ex(struct rt_ctx* ctx, int width, int height, int y0, int stripe, int period, int out_rows,
+                        float* dst, size_t pitch, int format);
+
 /* glMemoryBarrier + wait: blocks until the context's stream is drained. */
 int rt_sync(struct rt_ctx* ctx);
 
@@ -182,6 +189,9 @@ int rt_device_image(struct rt_ctx* ctx, void** ptr, size_t* pitch);
  * rt_dispatch_rows and returns the totals (synchronous; not for timed loops). */
 int rt_collect_stats(struct rt_ctx* ctx, int width, int height, int y0, int stripe,
                      int step, int out_rows, rt_stats* out);
+/* The same over rt_dispatch_rows_ex's rows. */
+int rt_collect_stats_ex(struct rt_ctx* ctx, int width, int height, int y0, int stripe,
+                        int period, int out_rows, rt_stats* out);
 
 /* Device time of the last render kernel in ms (HIP events on the context stream). */
 int rt_last_kernel_ms(struct rt_ctx* ctx, float* ms);

@@ -4,16 +4,18 @@
  *
  * The reference renders a frame with one glDispatchCompute(W, H, 1) on one GPU
  * (src/main.cpp:352-354). Pixels are independent (gpu_shader.comp:434-623
- * reads no other pixel), so a group splits the frame's rows over its ranks:
- * rank r of P renders the interleaved stripe set
- *     { image row y : (y / stripe) mod P == r }
- * (rt_dispatch_rows_fmt with y0 = r*stripe, step = P) into a compact packed-RGB
- * buffer (12 B per pixel: the alpha is always 1) of rows_max = max over ranks of
- * its row count. One fan-in per frame brings the
- * P buffers to rank 0 — ncclGather over xGMI (RCCL) or device copies — and a
- * kernel on rank 0 scatters the stripes back into image order in rank 0's
- * pitched RGBA32F surface. Interleaving balances sky rows against rows through
- * the car without any per-frame planning; no other collective runs.
+ * reads no other pixel), so a group splits the frame's rows over its ranks in
+ * periods of Q = share + P - 1 stripes of `stripe` rows: rank 0 renders the
+ * first `share` stripes of every period, rank r >= 1 the stripe share - 1 + r.
+ * With share 1 (the default) that is the interleave
+ *     { image row y : (y / stripe) mod P == r }.
+ * Each rank renders (rt_dispatch_rows_ex) into a compact packed-RGB buffer
+ * (12 B per pixel: the alpha is always 1); rank 0 renders straight into its
+ * staging buffer. One fan-in per frame brings the other ranks' rows to rank 0 —
+ * grouped ncclSend/ncclRecv over xGMI (RCCL) or device copies — and a kernel on
+ * rank 0 scatters the stripes back into image order in rank 0's pitched
+ * RGBA32F surface. Interleaving balances sky rows against rows through the car
+ * without any per-frame planning; no other collective runs.
  *
  * Two ways to build a group:
  *  - rt_group_create: ONE process drives every device (ncclCommInitAll, the
@@ -46,7 +48,7 @@ struct rt_group; /* opaque */
 
 enum rt_gather {
     RT_GATHER_AUTO = 0,  /* RCCL when the ranks' devices are distinct, copies otherwise */
-    RT_GATHER_RCCL = 1,  /* ncclGather to rank 0 on the members' streams                */
+    RT_GATHER_RCCL = 1,  /* ncclSend/ncclRecv to rank 0 on the members' streams          */
     RT_GATHER_COPY = 2   /* hipMemcpyPeerAsync into rank 0's staging (one process only) */
 };
 
@@ -82,6 +84,17 @@ int rt_group_set_params(struct rt_group* g, const rt_params* params);
  * gather it into rank 0's surface. Stream-ordered and asynchronous; every rank
  * calls it for every frame, in the same order. */
 int rt_group_dispatch(struct rt_group* g, int width, int height, int stripe);
+
+/* Rank 0's stripes per period (1 <= share <= 64; default 1). Rank 0's rows
+ * never cross a link, so when rank 0's ingress bounds the frame (7 peers' rows
+ * into one GPU), a larger share moves fewer bytes: of a frame's B bytes, rank 0
+ * receives (P - 1) / (share + P - 1) of them. Every rank must set the same
+ * value before the same frame. The image does not depend on it. */
+int rt_group_set_root_share(struct rt_group* g, int share);
+
+/* rt_collect_stats over the rows this process's members render for a
+ * (width, height, stripe) frame at the current share, summed. Synchronous. */
+int rt_group_collect_stats(struct rt_group* g, int width, int height, int stripe, rt_stats* out);
 
 /* Wait until this process's members have finished their last frame. */
 int rt_group_sync(struct rt_group* g);

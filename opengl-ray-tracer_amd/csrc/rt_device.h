@@ -80,7 +80,7 @@ struct KParams {
     V light_pos, light_color;
     float resX, resY;
     int maxBounces, useBVH, useFresnel, useMT;
-    int width, height, y0, stripe, step, out_rows;
+    int width, height, y0, stripe, period, out_rows;  // compact row r -> image row (image_row)
     char* __restrict__ dst;
     size_t pitch;
     unsigned long long* __restrict__ stats;  // rt_stats layout, STATS kernels only
@@ -113,9 +113,13 @@ struct KParams {
                                              // 1e-5 when it renders the brute branch (:565, rt_ctx::brute)
 };
 
-// Row mapping of rt_dispatch_rows (include/rt_api.h).
+// Row mapping of rt_dispatch_rows_ex (include/rt_api.h): stripes of `stripe` rows
+// starting at y0, one every `period` rows (rt_dispatch_rows: period = stripe * step),
+// i.e. y0 + (r / stripe) * period + r % stripe. Written this way because it keeps
+// the register allocation of every production k_accel instance as it was (the
+// direct form moved 23 VGPRs of the compacting instance to scratch).
 __device__ __forceinline__ int image_row(const KParams& kp, int r) {
-    return kp.y0 + (r / kp.stripe) * kp.stripe * kp.step + (r % kp.stripe);
+    return kp.y0 + r + (r / kp.stripe) * (kp.period - kp.stripe);
 }
 
 // getRay (gpu_shader.comp:155-168); imagePlaneHeight/Width come from the host

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -2698,11 +2699,11 @@ size_t sched_set_words(int tiles) {
     return static_cast<size_t>((tiles + kOrderThreads - 1) / kOrderThreads) * kOrderBuckets;
 }
 
-int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
+int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int period, int out_rows, float* dst,
                  size_t pitch, KParams& kp, int format = RT_FORMAT_RGBA32F) {
     if (!c->have_scene || !c->have_cam || !c->have_light) return RT_ERR_NO_SCENE;
     const size_t px = format == RT_FORMAT_RGB32F ? 12 : 16, align = format == RT_FORMAT_RGB32F ? 4 : 16;
-    if (width <= 0 || height <= 0 || stripe <= 0 || step <= 0 || out_rows < 0 || y0 < 0 || !dst ||
+    if (width <= 0 || height <= 0 || stripe <= 0 || period < stripe || out_rows < 0 || y0 < 0 || !dst ||
         (format != RT_FORMAT_RGBA32F && format != RT_FORMAT_RGB32F) || pitch < static_cast<size_t>(width) * px ||
         (pitch % align) != 0 || (reinterpret_cast<uintptr_t>(dst) % align) != 0)
         return RT_ERR_INVALID;
@@ -2736,7 +2737,7 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int step,
     kp.height = height;
     kp.y0 = y0;
     kp.stripe = stripe;
-    kp.step = step;
+    kp.period = period;
     kp.out_rows = out_rows;
     kp.dst = reinterpret_cast<char*>(dst);
     kp.pitch = pitch;
@@ -2863,7 +2864,7 @@ int render(rt_ctx* c, const KParams& kp) {
         else nxt = mt_ctx(t, kt);
         if (!nxt) break;
         KParams kn;
-        const int rc = fill_kparams(nxt, kt.width, kt.height, kt.y0, kt.stripe, kt.step, kt.out_rows,
+        const int rc = fill_kparams(nxt, kt.width, kt.height, kt.y0, kt.stripe, kt.period, kt.out_rows,
                                     reinterpret_cast<float*>(kt.dst), kt.pitch, kn,
                                     kt.rgb ? RT_FORMAT_RGB32F : RT_FORMAT_RGBA32F);
         if (rc != RT_OK) return rc;
@@ -3508,11 +3509,23 @@ int rt_dispatch_rows(rt_ctx* c, int width, int height, int y0, int stripe, int s
     return rt_dispatch_rows_fmt(c, width, height, y0, stripe, step, out_rows, dst, pitch, RT_FORMAT_RGBA32F);
 }
 
+// period = stripe * step, refused when it does not fit an int
+static int stripe_period(int stripe, int step) {
+    if (stripe <= 0 || step <= 0 || step > INT_MAX / stripe) return -1;
+    return stripe * step;
+}
+
 int rt_dispatch_rows_fmt(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, float* dst,
                          size_t pitch, int format) {
+    return rt_dispatch_rows_ex(c, width, height, y0, stripe, stripe_period(stripe, step), out_rows, dst, pitch,
+                               format);
+}
+
+int rt_dispatch_rows_ex(rt_ctx* c, int width, int height, int y0, int stripe, int period, int out_rows, float* dst,
+                        size_t pitch, int format) {
     if (!c) return RT_ERR_INVALID;
     KParams kp;
-    int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, dst, pitch, kp, format);
+    int rc = fill_kparams(c, width, height, y0, stripe, period, out_rows, dst, pitch, kp, format);
     if (rc != RT_OK) return rc;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     return render(c, kp);
@@ -3566,6 +3579,11 @@ int rt_device_image(rt_ctx* c, void** p, size_t* pitch) {
 }
 
 int rt_collect_stats(rt_ctx* c, int width, int height, int y0, int stripe, int step, int out_rows, rt_stats* out) {
+    return rt_collect_stats_ex(c, width, height, y0, stripe, stripe_period(stripe, step), out_rows, out);
+}
+
+int rt_collect_stats_ex(rt_ctx* c, int width, int height, int y0, int stripe, int period, int out_rows,
+                        rt_stats* out) {
     if (!c || !out) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     // The counting kernel needs a destination; use a scratch surface.
@@ -3574,7 +3592,7 @@ int rt_collect_stats(rt_ctx* c, int width, int height, int y0, int stripe, int s
     if (hipMalloc(&scratch, pitch * static_cast<size_t>(out_rows > 0 ? out_rows : 1)) != hipSuccess)
         return RT_ERR_NO_MEMORY;
     KParams kp;
-    int rc = fill_kparams(c, width, height, y0, stripe, step, out_rows, scratch, pitch, kp);
+    int rc = fill_kparams(c, width, height, y0, stripe, period, out_rows, scratch, pitch, kp);
     if (rc == RT_OK) {
         kp.stats = c->stats_dev;
         if (hipMemsetAsync(c->stats_dev, 0, ST_COUNT * sizeof(unsigned long long), c->stream) != hipSuccess)

@@ -187,9 +187,11 @@ RT_SYMBOLS = {
     "rt_dispatch": (_I, [_P, _I, _I, _I, _I]),
     "rt_dispatch_rows": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t]),
     "rt_dispatch_rows_fmt": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I]),
+    "rt_dispatch_rows_ex": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I]),
     "rt_sync": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
     "rt_device_image": (_I, [_P, _P, _P]),
     "rt_collect_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
+    "rt_collect_stats_ex": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
     "rt_last_kernel_ms": (_I, [_P, _P]),
     "rt_kernel_times": (_I, [_P, _P, _I]),
     "rt_accel_info_get": (_I, [_P, _P]),
@@ -217,6 +219,8 @@ GROUP_SYMBOLS = {
     "rt_group_set_camera": (_I, [_P, _P]), "rt_group_set_light": (_I, [_P, _P]),
     "rt_group_set_params": (_I, [_P, _P]),
     "rt_group_dispatch": (_I, [_P, _I, _I, _I]),
+    "rt_group_set_root_share": (_I, [_P, _I]),
+    "rt_group_collect_stats": (_I, [_P, _I, _I, _I, _P]),
     "rt_group_sync": (_I, [_P]),
     "rt_group_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
     "rt_group_device_image": (_I, [_P, _P, _P]),
@@ -505,6 +509,11 @@ class ComputeShader:
         self._chk(self._lib.rt_dispatch_rows_fmt(self._h, width, height, y0, stripe, step, out_rows,
                                                  C.c_void_p(dst_ptr), pitch, 1), "rt_dispatch_rows_fmt")
 
+    def dispatch_rows_ex(self, width, height, y0, stripe, period, out_rows, dst_ptr, pitch, rgb=False):
+        """rt_dispatch_rows_ex: stripes of `stripe` rows from y0, one every `period` rows."""
+        self._chk(self._lib.rt_dispatch_rows_ex(self._h, width, height, y0, stripe, period, out_rows,
+                                                C.c_void_p(dst_ptr), pitch, int(bool(rgb))), "rt_dispatch_rows_ex")
+
     def sync(self):
         self._chk(self._lib.rt_sync(self._h), "rt_sync")
 
@@ -760,6 +769,17 @@ class Group:
 
     def dispatch(self, width, height, stripe=8):
         self._chk(self._lib.rt_group_dispatch(self._h, width, height, stripe), "rt_group_dispatch")
+
+    def set_root_share(self, share):
+        """Rank 0's stripes per period of share + P - 1 (rt_group_set_root_share)."""
+        self._chk(self._lib.rt_group_set_root_share(self._h, int(share)), "rt_group_set_root_share")
+
+    def collect_stats(self, width, height, stripe=8):
+        """Reference-walk totals of this process's members' rows (rt_group_collect_stats)."""
+        st = rt_stats()
+        self._chk(self._lib.rt_group_collect_stats(self._h, width, height, stripe, C.byref(st)),
+                  "rt_group_collect_stats")
+        return st.as_dict()
 
     def sync(self):
         self._chk(self._lib.rt_group_sync(self._h), "rt_group_sync")

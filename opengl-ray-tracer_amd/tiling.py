@@ -43,6 +43,31 @@ class StripePlan:
         return self.y0(rank) + (r // self.stripe) * self.stripe * self.world + (r % self.stripe)
 
 
+@dataclass(frozen=True)
+class SharePlan:
+    """The rows of rt_group with a root share (csrc/rt_group.hip rank_rows,
+    include/rt_group.h rt_group_set_root_share): periods of (share + P - 1)
+    stripes, rank 0 the first `share` of each, rank r >= 1 the stripe
+    share - 1 + r. share = 1 is StripePlan's interleave."""
+    height: int
+    world: int
+    stripe: int
+    share: int = 1
+
+    def mapping(self, rank: int):
+        """(y0, stripe, period, rows) of `rank` (the rt_dispatch_rows_ex arguments)."""
+        period = (self.share + self.world - 1) * self.stripe
+        y0 = 0 if rank == 0 else (self.share - 1 + rank) * self.stripe
+        st = self.share * self.stripe if rank == 0 else self.stripe
+        full, rem = divmod(self.height, period)
+        return y0, st, period, full * st + max(0, min(st, rem - y0))
+
+    def image_rows(self, rank: int) -> torch.Tensor:
+        y0, st, period, n = self.mapping(rank)
+        r = torch.arange(n)
+        return y0 + (r // st) * period + (r % st)
+
+
 def unpermute(gathered: torch.Tensor, plan: StripePlan) -> torch.Tensor:
     """[world, rows_max, W, 4] compacted stripes -> [H, W, 4] image (on gathered's device)."""
     W = gathered.shape[2]

@@ -6,9 +6,10 @@
 //
 // Cases run on whatever devices the box has:
 //   * copy transport, 1..ranks (default 4) ranks all on device 0 (stripes + peer copies + unstripe);
-//   * RCCL transport, one rank per distinct device (ncclCommInitAll + ncclGather),
+//   * the same with rank 0 taking 2 stripes per period (rt_group_set_root_share);
+//   * RCCL transport, one rank per distinct device (ncclCommInitAll + send/recv),
 //     which on a 1-GPU box is the 1-rank communicator;
-//   * on >= 2 devices, RCCL over the first 2 and all devices.
+//   * on >= 2 devices, RCCL over the first 2 and all devices, root share 1 and 2.
 // The scene is the config's own (rts_generate: the reference's builder and
 // serialisers), uploaded as the reference uploads its SSBOs (src/main.cpp:256-275).
 #include <cstdio>
@@ -60,7 +61,7 @@ static int compare(const char* what, const std::vector<float>& ref, const std::v
 }
 
 static int run_group(const char* what, const Scene& s, const rt_params& p, int W, int H, int stripe,
-                     const int* devs, int n, int transport, const std::vector<float>& ref) {
+                     const int* devs, int n, int transport, const std::vector<float>& ref, int share = 1) {
     rt_group* g = nullptr;
     const int rc = rt_group_create(&g, devs, n, transport);
     if (rc != RT_OK) {
@@ -72,6 +73,7 @@ static int run_group(const char* what, const Scene& s, const rt_params& p, int W
     CHECK(rt_group_set_camera(g, &s.cam));
     CHECK(rt_group_set_light(g, &s.light));
     CHECK(rt_group_set_params(g, &p));
+    CHECK(rt_group_set_root_share(g, share));
     // three frames: the buffers are reused across frames, as in a render loop
     for (int f = 0; f < 3; ++f) CHECK(rt_group_dispatch(g, W, H, stripe));
     CHECK(rt_group_sync(g));
@@ -80,7 +82,8 @@ static int run_group(const char* what, const Scene& s, const rt_params& p, int W
     int nr = 0, nl = 0, tr = 0;
     CHECK(rt_group_info(g, &nr, &nl, &tr));
     char label[96];
-    std::snprintf(label, sizeof label, "%s [%d ranks, %s]", what, nr, tr == RT_GATHER_RCCL ? "rccl" : "copy");
+    std::snprintf(label, sizeof label, "%s [%d ranks, %s, share %d]", what, nr, tr == RT_GATHER_RCCL ? "rccl" : "copy",
+                  share);
     // a short destination is refused, not overrun
     const int short_rc = rt_group_read_image(g, img.data(), static_cast<size_t>(W) * 16, W, H - 1);
     CHECK(rt_group_destroy(g));
@@ -126,6 +129,7 @@ int main(int argc, char** argv) {
         char what[64];
         std::snprintf(what, sizeof what, "config %d %dx%d, stripes of 8", config, W, H);
         fails += run_group(what, s, p, W, H, 8, zeros.data(), n, RT_GATHER_COPY, ref);
+        if (n > 1) fails += run_group(what, s, p, W, H, 8, zeros.data(), n, RT_GATHER_COPY, ref, 2);
     }
     fails += run_group("stripes of 5 (ragged last stripe)", s, p, W, H, 5, zeros.data(), 3, RT_GATHER_COPY, ref);
     fails += run_group("stripe taller than the frame", s, p, W, H, H + 3, zeros.data(), 2, RT_GATHER_COPY, ref);
@@ -142,6 +146,8 @@ int main(int argc, char** argv) {
         for (int d = 0; d < ndev; ++d) all[d] = d;
         fails += run_group("rccl over 2 devices", s, p, W, H, 8, all.data(), 2, RT_GATHER_RCCL, ref);
         fails += run_group("rccl over every device", s, p, W, H, 8, all.data(), ndev, RT_GATHER_RCCL, ref);
+        fails += run_group("rccl over 2 devices", s, p, W, H, 8, all.data(), 2, RT_GATHER_RCCL, ref, 2);
+        fails += run_group("rccl over every device", s, p, W, H, 8, all.data(), ndev, RT_GATHER_RCCL, ref, 2);
     }
     std::printf("%s\n", fails ? "FAIL" : "OK");
     return fails ? 1 : 0;

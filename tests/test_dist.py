@@ -62,3 +62,24 @@ def test_stripe_plan_covers_every_row_once():
             plan = tiling.StripePlan(H, world, 8)
             rows = torch.cat([plan.image_rows(r) for r in range(world)])
             assert sorted(rows.tolist()) == list(range(H))
+
+
+def test_root_share_plan_covers_every_row_once():
+    """rt_group's rows with rank 0 taking `share` stripes per period (SharePlan
+    restates csrc/rt_group.hip rank_rows): every image row once; share 1 is the
+    plain interleave; rank 1 holds the most rows of ranks >= 1 (its count sizes
+    the staging slots)."""
+    for H in (1, 7, 8, 13, 270, 1080, 2160):
+        for world in (1, 2, 3, 4, 8):
+            for share in (1, 2, 3):
+                for stripe in (1, 3, 8):
+                    plan = tiling.SharePlan(H, world, stripe, share)
+                    rows = torch.cat([plan.image_rows(r) for r in range(world)])
+                    assert sorted(rows.tolist()) == list(range(H)), (H, world, share, stripe)
+                    n = [plan.mapping(r)[3] for r in range(world)]
+                    assert all(n[1] >= x for x in n[1:]) if world > 1 else True
+                    if share == 1:
+                        sp = tiling.StripePlan(H, world, stripe)
+                        assert all(torch.equal(plan.image_rows(r), sp.image_rows(r)) for r in range(world))
+    # at 1080p over 2 GPUs, share 2 leaves rank 1 a third of the rows to send instead of half
+    assert tiling.SharePlan(1080, 2, 8, 2).mapping(1)[3] == 360

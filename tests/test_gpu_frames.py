@@ -9,8 +9,9 @@
 * Config 4 (3840x2160): oracle bands at the top, through the car and at the
   bottom for the accelerated and the packet kernel; the 8-rank stripe set
   reassembled by rt_group (copy transport on one GPU) equals the single
-  dispatch bit for bit; the 1-rank RCCL group (ncclCommInitRank + ncclGather)
-  equals it too.
+  dispatch bit for bit; the 1-rank RCCL group (ncclCommInitRank) equals it too.
+* Root shares (rt_group_set_root_share): rank 0 taking 2-64 stripes per period
+  reassembles to the single dispatch for 2-8 copy-transport ranks.
 * tests/native/group_check: a C++ host that links librtamd.so through the C
   ABI alone and checks every group case bit for bit (1080p-class and 4K).
 
@@ -175,8 +176,49 @@ def test_config4_group_of_8_reassembles(frame4k, car4k, kernel):
         g.close()
 
 
+@pytest.mark.parametrize("ranks,share,stripe", [(2, 2, 8), (3, 2, 8), (4, 2, 8), (8, 2, 8), (2, 3, 5), (5, 1, 7),
+                                                (8, 3, 3), (3, 64, 1)])
+def test_group_root_share_reassembles(ctx, ranks, share, stripe):
+    """rt_group_set_root_share: rank 0 renders `share` stripes of every period of
+    share + P - 1 (straight into its staging), the others one each; the gathered
+    frame is the single dispatch bit for bit, also when the share changes between
+    frames (buffers resize) and for heights that end inside a period."""
+    W, H = 480, 270
+    fs = rtamd.generate(3, 0, W, H)
+    ref = render(ctx, fs, W, H, 3)
+    g = rtamd.Group([0] * ranks, rtamd.GATHER_COPY)
+    try:
+        g.upload(fs)
+        g.set_params(W, H, 3)
+        for k in (share, 1, share):
+            g.set_root_share(k)
+            assert np.array_equal(g.render(W, H, stripe), ref), f"share {k}"
+            st = g.collect_stats(W, H, stripe)
+            assert st["pixels"] == W * H  # the members' rows cover the frame once
+    finally:
+        g.close()
+
+
+def test_rccl_rank_group_root_share(ctx):
+    """A 1-rank RCCL group at root share 2: rank 0 owns every row (nothing to send)."""
+    W, H = 640, 360
+    fs = rtamd.generate(3, 0, W, H)
+    ref = render(ctx, fs, W, H, 3)
+    g = rtamd.Group(uid=rtamd.group_unique_id(), nranks=1, rank=0, device=0)
+    try:
+        g.upload(fs)
+        g.set_params(W, H, 3)
+        g.set_root_share(2)
+        for _ in range(2):
+            assert np.array_equal(g.render(W, H, 8), ref)
+        with pytest.raises(rtamd.RTError):
+            g.set_root_share(0)
+    finally:
+        g.close()
+
+
 def test_rccl_rank_group_equals_single_dispatch(ctx):
-    """rt_group_create_rank with one rank: ncclCommInitRank + ncclGather + unstripe."""
+    """rt_group_create_rank with one rank: ncclCommInitRank + unstripe."""
     W, H = 640, 360
     fs = rtamd.generate(3, 0, W, H)
     ref = render(ctx, fs, W, H, 3)
