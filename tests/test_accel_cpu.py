@@ -444,4 +444,6 @@ def test_accel_mt_matches_reference_walk(check_lib, src, tree):
     compare(check_lib, fs, O, D, rng.uniform(1, 80, len(O)), tree, mt=1)
     if src == "car":  # camera rays alone: the accelerator still culls (the reference walk tests ~3,100 per ray)
         info = compare(check_lib, fs, o, d, np.full(len(o), 50.0), tree, mt=1)
-        assert info[4] < 1000, info[4]
+        # the normal splits of the MT local build (accel.cpp kMtNormalBias) keep the
+        # grazing cones tight: ~800 tests per ray with spatial splits alone
+        assert info[4] < 650, info[4]

@@ -29,6 +29,7 @@ ap.add_argument("--walk2", type=int, default=-1, help="walk policy (rt_set_walk)
 ap.add_argument("--set2", default="", help="lib2 settings, e.g. schedule=0,launch=2,walk=0")
 ap.add_argument("--nocheck", action="store_true", help="timing only: images may differ (experiments)")
 ap.add_argument("--bounces", type=int, default=0, help="override maxBounces")
+ap.add_argument("--mt", action="store_true", help="useMollerTrumbore = 1 frames")
 ap.add_argument("--child", default=None, help=argparse.SUPPRESS)
 a = ap.parse_args()
 
@@ -39,7 +40,7 @@ if a.child is None:
     for _ in range(a.rounds):
         for name in ("current", "lib2"):
             out = subprocess.run([sys.executable, __file__, "--lib2", a.lib2, "--config", str(a.config),
-                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--bounces", str(a.bounces), "--walk2", str(a.walk2), "--set2", a.set2, "--child", name],
+                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--bounces", str(a.bounces)] + (["--mt"] if a.mt else []) + ["--walk2", str(a.walk2), "--set2", a.set2, "--child", name],
                                  capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
             r = json.loads(out)
             res[name].append(r["ms"])
@@ -63,7 +64,7 @@ for _ in range(F):
     c = rtamd.ComputeShader(0, lib_path=path)
     c.set_stream(s.cuda_stream)
     c.upload(fs)
-    c.set_params(W, H, mb, True)
+    c.set_params(W, H, mb, True, False, a.mt)
     if a.child == "lib2" and a.walk2 >= 0:
         c.set_walk(a.walk2)
     if a.child == "lib2" and a.set2:
