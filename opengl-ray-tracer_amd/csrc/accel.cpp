@@ -80,19 +80,22 @@ NCone normal_cone(const std::vector<Item>& items, int b, int e, F sel) {
 }
 
 // MT: a normal split is taken while it costs less than kMtNormalBias times the
-// spatial one. The cost model prices grazing for uniformly spread directions;
-// camera and reflection rays are not, and on the car (tests/native/accel_check,
-// camera rays) the closest-hit tests per ray went 801 (spatial only) -> 721
-// (bias 1) -> 593 (1.3) -> 502 (2) -> 489 (4).
+// spatial one, and local leaves hold up to kMtLeaf prims. The cost model prices
+// grazing for uniformly spread directions; camera and reflection rays are not.
+// Measured on the car's MT frame (tools/abf.py --mt, profiles/r02zz3_abf_mt_*):
+// spatial splits only 16.7 ms; bias 1 / leaf 4: 14.4; bias 2 / leaf 4: 9.27 (leaf 2:
+// 10.7, leaf 1: 14.4); bias 4 / leaf 4: 9.17; bias 4 / leaf 6: 9.06 (kept); bias 8 /
+// leaf 6: 9.11; bias 4 / leaf 8: 9.43. Closest-hit tests per car camera ray
+// (tests/native/accel_check): 801 spatial only, 502 at bias 2 / leaf 4, 642 kept
+// (bigger leaves test more and visit fewer nodes, which is what costs on the GPU).
 #ifndef RTA_MT_NORMAL_BIAS
-#define RTA_MT_NORMAL_BIAS 2.0
+#define RTA_MT_NORMAL_BIAS 4.0
 #endif
 constexpr double kMtNormalBias = RTA_MT_NORMAL_BIAS;
 #ifndef RTA_MT_LEAF
-#define RTA_MT_LEAF 4
+#define RTA_MT_LEAF 6
 #endif
-constexpr int kMtLeaf = RTA_MT_LEAF;  // MT local leaves hold at most this many prims (2: +16 %, 1: +56 %
-                                      // per frame on the GPU, profiles/r02zz3_abf_mt_leaf.jsonl)
+constexpr int kMtLeaf = RTA_MT_LEAF;  // MT local leaves hold at most this many prims
 
 struct LocalBuilder {
     AccelHost& out;
