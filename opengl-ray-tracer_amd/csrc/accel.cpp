@@ -612,6 +612,53 @@ struct SceneBuilder {
             if (!(chi[ax] - clo[ax] > 0)) continue;
             int cnt[kMaxBins] = {0}, acnt[kMaxBins] = {0};
             Box3 bb[kMaxBins];
+            if (n < kBins) {
+                // Few atoms: only the bins they occupy are set up and swept. Growing by
+                // an empty bin is the identity and every boundary inside a run of empty
+                // bins makes the same partition at the same cost, so the split found
+                // (best_k included: the first of a run scanning down is the next occupied
+                // bin) is the dense sweep's (scene-tree hashes equal on configs 2, 3, 5,
+                // the 222-strip road and three soups). Config 5's whole accelerator build
+                // (93k atoms): 2.1 s -> 0.36 s on the host.
+                int used[kMaxBins], nu = 0;
+                for (int i = b; i < e; ++i) {
+                    const int k = bin_of(atoms[i], ax);
+                    if (acnt[k] == 0) {
+                        used[nu++] = k;
+                        bb[k] = empty_box();
+                    }
+                    cnt[k] += atoms[i].n;
+                    ++acnt[k];
+                    grow(bb[k], atoms[i].box);
+                }
+                std::sort(used, used + nu);
+                Box3 lacc = empty_box();
+                int lcnt = 0, lat = 0;
+                float lcost[kMaxBins];
+                int lats[kMaxBins];
+                for (int j = 0; j < nu; ++j) {
+                    grow(lacc, bb[used[j]]);
+                    lcnt += cnt[used[j]];
+                    lat += acnt[used[j]];
+                    lcost[j] = lcnt ? area(lacc) * lcnt : 0.f;
+                    lats[j] = lat;
+                }
+                Box3 racc = empty_box();
+                int rcnt = 0, rat = 0;
+                for (int j = nu - 1; j >= 1; --j) {
+                    const int k = used[j];
+                    grow(racc, bb[k]);
+                    rcnt += cnt[k];
+                    rat += acnt[k];
+                    const float c = lcost[j - 1] + (rcnt ? area(racc) * rcnt : 0.f);
+                    if (rat && rat < n && log2_ceil(lats[j - 1]) <= room && log2_ceil(rat) <= room && c < best) {
+                        best = c;
+                        best_k = k;
+                        best_axis = ax;
+                    }
+                }
+                continue;
+            }
             for (auto& x : bb) x = empty_box();
             for (int i = b; i < e; ++i) {
                 const int k = bin_of(atoms[i], ax);
