@@ -207,9 +207,10 @@ int rt_set_launch(struct rt_ctx* ctx, int waves_per_block, int persistent);
 
 /* Accelerated kernel: bounces with depth >= lane_from_depth walk one ray per
  * lane (LDS stack) instead of one packet per wave; 0 = all bounces per lane,
- * >= maxBounces = all packet. Default 1: camera rays and their shadow rays
- * walk as packets (coherent), reflections per lane (measured fastest on
- * configs 2, 3 and 5). Same image for every value. */
+ * >= maxBounces = all packet. Default (auto): 1 -- camera rays and their shadow
+ * rays walk as packets (coherent), reflections per lane (measured fastest on
+ * configs 2, 3 and 5) -- and 2 for Moller-Trumbore frames (their first
+ * reflection as packets too). Same image for every value. */
 int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 
 /* Tile dispatch order of the accelerated kernel. RT_SCHED_ROWS: row-major.

@@ -1419,6 +1419,7 @@ constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
 constexpr int kOrderBuckets = 32, kOrderThreads = 256;
 // lane_walk_any defaults (rt_debug_split)
 constexpr int kSplitMax = 16, kSplitGroup = 8;
+constexpr int kMtWalkFrom = 2;  // auto walk policy of Moller-Trumbore frames (walk_from)
 // the heaviest tiles of the cost order as several waves (rt_debug_heavy)
 constexpr int kHeavyTiles = -1, kHeavyParts = 4, kHeavyAutoSlots = 2;  // -1: auto
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
@@ -2100,7 +2101,8 @@ struct rt_ctx {
     unsigned long long* stats_dev = nullptr;
     // launch shape of k_accel (rt_set_launch)
     int waves_per_block = 1, persistent = 0, cu_count = 256;
-    int lane_from_depth = 1;  // bounces >= this use the per-lane walk (0: all, large: none)
+    int lane_from_depth = -1;  // bounces >= this use the per-lane walk (0: all, large: none;
+                               // -1: auto, see walk_from)
     int cone_cull = 1;
     int spec_mode = 1;  // speculative while-while in lane_walk (rt_debug_spec): 1 on, 0 off
     int split_max = kSplitMax, split_g = kSplitGroup;  // split per-lane walks (rt_debug_split)
@@ -2798,6 +2800,17 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->lane_stack_override = c->lane_stack_override;
 }
 
+// The walk policy in force (rt_set_walk, or auto): barycentric frames walk camera
+// rays and their shadows as packets and reflections per lane (1, measured fastest on
+// configs 2, 3 and 5); Moller-Trumbore frames walk the first reflection as packets
+// too (kMtWalkFrom), since their grazing cones force entries that neighbouring rays
+// share (car MT frame 8.99 -> 7.73 ms at 2, per lane for every bounce 12.2 ms;
+// profiles/r02zz5_abf_mt_walk.jsonl).
+int walk_from(const rt_ctx* c) {
+    if (c->lane_from_depth >= 0) return c->lane_from_depth;
+    return c->accel.mt ? kMtWalkFrom : 1;
+}
+
 bool sub_usable(const rt_ctx* b, const KParams& kp) {
     const float cmag = std::max({std::fabs(kp.cam_pos.x), std::fabs(kp.cam_pos.y), std::fabs(kp.cam_pos.z)});
     return b->accel_ok && cmag <= b->accel.origin_lim;
@@ -2965,7 +2978,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             }
             ++c->sched_frame;
         }
-        k2.lane_from_depth = c->lane_from_depth;
+        k2.lane_from_depth = walk_from(c);
         // the root's bounds as kernel arguments while the host copy is current (rt_animate
         // grows boxes on the device)
         k2.root_ok = 0;
@@ -2984,7 +2997,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         // (measured on config 5: -3.7 %; on the car the packet walk is faster)
         const bool big = c->accel.st.item_ref.size() >= kTailAutoItems;
         k2.shadow_lane_from = c->shadow_walk_override >= 0 ? c->shadow_walk_override
-                              : (big && c->lane_from_depth <= 1 ? 0 : c->lane_from_depth);
+                              : (big && k2.lane_from_depth <= 1 ? 0 : k2.lane_from_depth);
         k2.lane_stack = c->lane_stack_override > 0 ? c->lane_stack_override : c->accel.max_stack;
         if (k2.tile_order && k2.tile_order == c->sched_order) {
             // the first lane_k dispatch slots (the heaviest tiles): explicit (rt_debug_lane_k)
