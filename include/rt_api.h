@@ -209,8 +209,8 @@ int rt_set_launch(struct rt_ctx* ctx, int waves_per_block, int persistent);
  * lane (LDS stack) instead of one packet per wave; 0 = all bounces per lane,
  * >= maxBounces = all packet. Default (auto): 1 -- camera rays and their shadow
  * rays walk as packets (coherent), reflections per lane (measured fastest on
- * configs 2, 3 and 5) -- and 2 for Moller-Trumbore frames (their first
- * reflection as packets too). Same image for every value. */
+ * configs 2, 3 and 5) -- and all packets for Moller-Trumbore frames over
+ * reference trees of fewer than 1024 nodes. Same image for every value. */
 int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 
 /* Tile dispatch order of the accelerated kernel. RT_SCHED_ROWS: row-major.

@@ -1419,7 +1419,8 @@ constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
 constexpr int kOrderBuckets = 32, kOrderThreads = 256;
 // lane_walk_any defaults (rt_debug_split)
 constexpr int kSplitMax = 16, kSplitGroup = 8;
-constexpr int kMtWalkFrom = 2;  // auto walk policy of Moller-Trumbore frames (walk_from)
+constexpr int kMtWalkFrom = 1 << 16;      // auto walk policy of Moller-Trumbore frames: all packets
+constexpr int kMtPacketMaxNodes = 1024;  // ... over reference trees of fewer nodes (walk_from)
 // the heaviest tiles of the cost order as several waves (rt_debug_heavy)
 constexpr int kHeavyTiles = -1, kHeavyParts = 4, kHeavyAutoSlots = 2;  // -1: auto
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
@@ -2802,13 +2803,16 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
 
 // The walk policy in force (rt_set_walk, or auto): barycentric frames walk camera
 // rays and their shadows as packets and reflections per lane (1, measured fastest on
-// configs 2, 3 and 5); Moller-Trumbore frames walk the first reflection as packets
-// too (kMtWalkFrom), since their grazing cones force entries that neighbouring rays
-// share (car MT frame 8.99 -> 7.73 ms at 2, per lane for every bounce 12.2 ms;
-// profiles/r02zz5_abf_mt_walk.jsonl).
+// configs 2, 3 and 5). Moller-Trumbore frames over a shallow reference tree with
+// big leaves (the car's 3 nodes, whose local BVHs carry the grazing cones) walk every
+// bounce as packets, since the cones force entries that neighbouring rays share: car
+// MT frame 8.99 ms at 1, 7.73 at 2, 7.00 at 3 (= all packets at depth 3), 12.2 per
+// lane for every bounce. Over a deep tree of small leaves (config 5: 6.86 ms at 1,
+// 11.39 all packets) they keep 1; the monkey is equal either way
+// (profiles/r02zz5_abf_mt_walk*.jsonl).
 int walk_from(const rt_ctx* c) {
     if (c->lane_from_depth >= 0) return c->lane_from_depth;
-    return c->accel.mt ? kMtWalkFrom : 1;
+    return c->accel.mt && c->N < kMtPacketMaxNodes ? kMtWalkFrom : 1;
 }
 
 bool sub_usable(const rt_ctx* b, const KParams& kp) {
