@@ -21,8 +21,13 @@ Modes (--mode auto = frames at N = 1, strong at N > 1):
           1920x1080 frame split over the N GPUs by interleaved 8-row stripes and
           gathers it to rank 0 through the C ABI's rt_group (ncclSend/ncclRecv
           over xGMI, then k_unstripe into rank 0's image) — total work fixed,
-          scaling "strong". Frames in flight = several groups, dealt
-          round-robin, each with its own streams, buffers and communicator.
+          scaling "strong". Frames in flight = the group's frame slots
+          (rt_group_set_frames): one render stream and buffer set per slot,
+          ONE communicator and one fan-in stream per rank. Before timing,
+          one gathered frame is compared bit for bit with rank 0's own
+          single-GPU frame (exit 5 on a mismatch); every wait on the group
+          is bounded (rt_group_sync: exit 4 on a timeout or an RCCL error);
+          the JSON line carries each rank's render / fan-in / unstripe times.
           Rank 0 may take 2 stripes per period (--root-share; auto times 1
           and 2 before the measured steps): its rows never cross a link;
   weak    each rank renders its own whole frame per step (frame r of a 1-degree
@@ -100,6 +105,8 @@ def parse(argv=None):
                          "1 and 2, timed on every rank before the measured steps")
     ap.add_argument("--schedule", default="cost", choices=["cost", "xcd", "rows"],
                     help="tile dispatch order (rt_set_schedule): cost (default), cost dealt to XCDs as bands, rows")
+    ap.add_argument("--walk", type=int, default=-1,
+                    help="walk policy (rt_set_walk): -1 auto, 0 all per lane, >= maxBounces all packets")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = the host's cores (nproc)")
@@ -166,17 +173,38 @@ def cpu_baseline(rtamd, fs, W, H, mb, seconds, threads, toggles=(True, False, Fa
     while True:
         y0 = max(0, H // 2 - rows // 2)
         t0 = time.perf_counter()
-        _, st = oracle.render(fs, W, H, p, y0=y0, out_rows=rows, stats=True, threads=threads)
+        img, st = oracle.render(fs, W, H, p, y0=y0, out_rows=rows, stats=True, threads=threads)
         dt = time.perf_counter() - t0
         if dt >= seconds * 0.5 or rows >= H:
             break
         rows = min(H, max(rows * 2, int(rows * seconds / max(dt, 1e-3) * 0.9)))
     rays = st["closest_rays"] + st["shadow_rays"]
+    cpu_baseline.last_image = (y0, img)  # the timed frames are checked against these rows
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"oracle (GLSL restated, OpenMP, {threads} threads) rows [{y0},{y0 + rows}) of the same "
                       f"{W}x{H} frame: {rows * W} pixels, {rays} rays in {dt:.2f} s",
             "ms_per_frame_equiv": dt * 1e3 * H / rows,
             "cpu": cpu_model(), "cpus_visible": os.cpu_count(), "cpus_affinity": len(os.sched_getaffinity(0))}
+
+
+PARITY_TOL = 1e-4  # per channel (BASELINE.json north_star)
+
+
+def parity_check(frames, ref_y0, ref, what):
+    """The frames the timed loop left in its buffers (one per context in flight: each
+    holds that context's last timed frame) against the oracle's rows [ref_y0, ref_y0 +
+    len(ref)) of the same frame (gpu_shader.comp:433-624 restated, oracle/rt_oracle.c)."""
+    import numpy as np
+    worst, bad = 0.0, 0
+    for f in frames:
+        img = f[ref_y0:ref_y0 + len(ref)].astype(np.float64)
+        d = np.abs(img - ref.astype(np.float64))
+        d[np.isnan(img) & np.isnan(ref)] = 0.0
+        d[np.isnan(d)] = np.inf
+        worst = max(worst, float(d.max()) if d.size else 0.0)
+        bad += int((d > PARITY_TOL).any(axis=-1).sum())
+    return {"max_abs": worst, "bad_pixels": bad, "frames_checked": len(frames), "tol": PARITY_TOL,
+            "rows_checked": [int(ref_y0), int(ref_y0 + len(ref))], "against": what, "ok": bad == 0}
 
 
 def cpu_reference_1core(rtamd, seconds):
@@ -347,21 +375,22 @@ def main():
     prank = rank if strong else 0
     rows = plan.rows(prank)
 
-    # F frames in flight: F renderers per GPU (contexts or groups), each with its own stream
-    groups, ctxs, bufs = [], [], []
+    # F frames in flight: F renderers per GPU (contexts, or the group's frame slots),
+    # each with its own stream
+    grp, ctxs, bufs = None, [], []
     if use_group:
-        for _ in range(F):
-            uid = [rtamd.group_unique_id() if rank == 0 else None]
-            if world > 1:
-                dist.broadcast_object_list(uid, src=0)
-            with quiet_stdout():
-                g = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local)
-            g.upload(fs)
-            g.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
-            g.members[0].set_kernel(kernel_id)
-            g.members[0].set_schedule(SCHEDULES[a.schedule])
-            groups.append(g)
-            ctxs.append(g.members[0])
+        uid = [rtamd.group_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        with quiet_stdout():
+            grp = rtamd.Group(uid=uid[0], nranks=world, rank=rank, device=local, frames=F)
+        grp.upload(fs)
+        grp.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
+        for c_ in grp.contexts:
+            c_.set_kernel(kernel_id)
+            c_.set_schedule(SCHEDULES[a.schedule])
+            c_.set_walk(a.walk)
+        ctxs = list(grp.contexts)
     else:
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
         for s_ in streams:
@@ -371,6 +400,7 @@ def main():
             c_.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             c_.set_kernel(kernel_id)
             c_.set_schedule(SCHEDULES[a.schedule])
+            c_.set_walk(a.walk)
             ctxs.append(c_)
             bufs.append(torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev))
     ctx = ctxs[0]
@@ -379,7 +409,7 @@ def main():
     # rt_group the rows follow the root share, so rt_group_collect_stats counts them.
     def count_work():
         if use_group:
-            st = groups[0].collect_stats(W, H, a.stripe)
+            st = grp.collect_stats(W, H, a.stripe)
             n = st["pixels"] // W
         else:
             st = ctx.collect_stats(W, H, plan.y0(prank), a.stripe, plan.world, rows)
@@ -395,8 +425,7 @@ def main():
     share = None
     if use_group:
         share = 1 if a.root_share == "auto" else int(a.root_share)
-        for g in groups:
-            g.set_root_share(share)
+        grp.set_root_share(share)
     rays_step, b_ref_rank, rows = count_work()
 
     cam, light = fs.camera, fs.light
@@ -409,10 +438,11 @@ def main():
 
     def frame(i, inflight):
         if use_group:
-            g = groups[i % inflight]
-            g.set_camera(cam)    # SSBO 2 (src/main.cpp:328-330)
-            g.set_light(light)   # SSBO 1 (:332-334)
-            g.dispatch(W, H, a.stripe)  # this rank's stripes + send/recv to rank 0 + unstripe there
+            grp.set_camera(cam)    # SSBO 2 (src/main.cpp:328-330)
+            grp.set_light(light)   # SSBO 1 (:332-334)
+            grp.dispatch(W, H, a.stripe)  # this rank's stripes + send/recv to rank 0 + unstripe there
+            if inflight == 1:
+                group_sync()  # one frame at a time: the frame slots would otherwise overlap
             return
         c_ = ctxs[i % inflight]
         c_.set_camera(cam)
@@ -424,11 +454,25 @@ def main():
         if strong:
             tiling.gather_to_root(buf, plan)
 
+    def group_sync():
+        """rt_group_sync is bounded: a fan-in that never completes or an RCCL error
+        ends the run with exit 4 instead of hanging in torch.cuda.synchronize()."""
+        if grp is None:
+            return
+        try:
+            grp.sync()
+        except rtamd.RTError as e:
+            print(f"bench.py rank {rank}: {e}", file=sys.stderr, flush=True)
+            os._exit(4)
+
     def timed(inflight):
         """Wall time of a.steps frames between barriers, max over ranks."""
         for i in range(a.warmup * inflight):
             frame(i, inflight)
+        group_sync()
         torch.cuda.synchronize()
+        if grp is not None:
+            grp.phase_times()  # drop the warm-up frames' phase times
         for c_ in ctxs:
             c_.kernel_times()  # drop warm-up dispatches
         if world > 1:
@@ -437,13 +481,46 @@ def main():
         t0 = time.perf_counter()
         for i in range(a.steps):
             frame(i, inflight)
+        group_sync()
         torch.cuda.synchronize()  # the device: every renderer stream, RCCL and unstripe included
         if world > 1:
             dist.barrier()
+        if grp is not None:
+            phases[inflight] = grp.phase_times()
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cpu" if gloo else dev)
         if world > 1:
             dist.all_reduce(el, op=dist.ReduceOp.MAX)
         return float(el[0])
+
+    # Strong mode over rt_group: before anything is timed, one gathered frame per frame
+    # slot is compared bit for bit with rank 0's own single-GPU frame of the same camera.
+    phases, selfcheck = {}, None
+    if use_group:
+        verdict = torch.zeros(1, dtype=torch.int64, device="cpu" if gloo else dev)
+        want = None
+        if rank == 0:
+            solo = rtamd.ComputeShader(torch.cuda.current_device())
+            solo.upload(fs)
+            solo.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
+            solo.set_kernel(kernel_id)
+            want = solo.render(W, H).view(np.uint32)
+            solo.close()
+        bad = []
+        for j in range(F):
+            frame(j, F)
+            group_sync()
+            if rank == 0:
+                bad.append(int((grp.read_image(W, H).view(np.uint32) != want).any(axis=-1).sum()))
+        if rank == 0:
+            verdict[0] = sum(bad)
+            selfcheck = {"frames": F, "bad_pixels_per_slot": bad, "against": "rank 0's single-GPU frame (bit-exact)",
+                         "ok": sum(bad) == 0}
+        if world > 1:
+            dist.broadcast(verdict, 0)
+        if int(verdict[0]):
+            print(f"bench.py rank {rank}: the gathered frame differs from the single-GPU frame: {bad}",
+                  file=sys.stderr, flush=True)
+            os._exit(5)
 
     # Root share (rt_group): with auto, every rank times the candidates the same way and
     # takes the same (max-over-ranks) verdict; the counted rays do not depend on it.
@@ -453,19 +530,30 @@ def main():
         steps = a.steps
         a.steps = max(4, 2 * F)
         for k in ((1, 2) if world > 1 else (1,)):
-            for g in groups:
-                g.set_root_share(k)
+            grp.set_root_share(k)
             share_probe[k] = timed(F) / a.steps * 1e3
         a.steps = steps
         best = min(share_probe, key=share_probe.get)
-        for g in groups:
-            g.set_root_share(best)
+        grp.set_root_share(best)
         share = best
         share_probe = {str(k): v for k, v in share_probe.items()}
         rays_step, b_ref_rank, rows = count_work()  # this rank's rows at the chosen share
 
     serial = timed(1) if F > 1 else None
     serial_kt = ctx.kernel_times() if F > 1 else None
+    # SURVEY §8(d)'s frame: upload + dispatch + completion, one at a time, FPS = 1 / median.
+    # Each frame waits for its completion (the reference's loop, src/main.cpp:290-462).
+    serial_frames = []
+    if not use_group or world == 1:
+        for i in range(a.warmup):
+            frame(i, 1)
+        torch.cuda.synchronize()
+        for i in range(a.steps):
+            t0 = time.perf_counter()
+            frame(i, 1)
+            torch.cuda.synchronize()
+            serial_frames.append(time.perf_counter() - t0)
+        ctx.kernel_times()
     # the same one-at-a-time frames with rt_set_latency_mode (what a host that waits for
     # each frame would set); reported beside serial_ms_per_step, not used for the roofline
     serial_lat = None
@@ -477,6 +565,14 @@ def main():
     elapsed = timed(F)
 
     kt_if = np.concatenate([c_.kernel_times() for c_ in ctxs])
+    rank_phases = None
+    if grp is not None:
+        mine = dict(phases.get(F, {}), rank=rank)
+        rank_phases = [None] * world
+        if world > 1:
+            dist.all_gather_object(rank_phases, mine)
+        else:
+            rank_phases = [mine]
     # The render kernel's duration is taken where it runs alone (the one-frame-in-flight
     # pass): with frames in flight a dispatch's events also span the time it waits for
     # the other frame's waves to leave the CUs.
@@ -507,6 +603,8 @@ def main():
             "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
             "serial_ms_per_step": (serial if serial is not None else elapsed) / a.steps * 1e3,
             "serial_ms_per_step_latency_mode": (serial_lat / a.steps * 1e3) if serial_lat is not None else None,
+            "serial_frame_ms_median": float(np.median(serial_frames)) * 1e3 if serial_frames else None,
+            "fps_serial_median": 1.0 / float(np.median(serial_frames)) if serial_frames else None,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
@@ -519,13 +617,15 @@ def main():
                        "width": W, "height": H, "maxBounces": mb, "useBVH": int(not a.brute),
                        "useFresnel": int(a.fresnel), "triangle_test": "moller-trumbore" if a.mt else "barycentric",
                        "animate": "wheels turn, device refit per frame" if a.animate else None, "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
-                       "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel,
+                       "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel, "walk": a.walk,
                        "parallelism": (f"row-stripes{a.stripe}x{world}+gather" if strong else
                                        f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"
                                        if mode == "weak" else "1 GPU")},
             "gather": gather,
             "root_share": share,
             "root_share_probe_ms": share_probe,
+            "group_selfcheck": selfcheck,
+            "group_phases_ms": rank_phases,
             "fps": fps,
             "mrays_primary_per_s": W * H * fps / 1e6,
             "rays_per_step": rays_step,
@@ -535,15 +635,32 @@ def main():
             "roofline": roofline(info, kname, k_ms, rows * W, b_ref_rank, pmc),
             "accel": info,
             "cpu_baseline": None,
+            "parity": None,
         }
+        thr = a.cpu_threads or host_cores()
         if world == 1 and not a.no_cpu:
-            thr = a.cpu_threads or host_cores()
             out["cpu_baseline"] = cpu_baseline(rtamd, fs, W, H, mb, a.cpu_seconds, thr,
                                                (not a.brute, a.fresnel, a.mt))
             out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2)
+        if mode == "frames" and anim is None:
+            # the timed frames themselves, against the oracle (outside the timed region)
+            if out["cpu_baseline"] is not None:
+                ry0, ref = cpu_baseline.last_image
+            else:
+                sys.path.insert(0, os.path.join(ROOT, "oracle"))
+                import oracle  # noqa: E402  (checker only)
+                ry0 = max(0, H // 2 - 8)
+                ref, _ = oracle.render(fs, W, H, oracle.params(W, H, mb, not a.brute, a.fresnel, a.mt),
+                                       y0=ry0, out_rows=min(16, H - ry0), threads=thr)
+            torch.cuda.synchronize()
+            out["parity"] = parity_check([b_.cpu().numpy() for b_ in bufs], ry0, ref,
+                                         "oracle/rt_oracle.c (GLSL restated), rows of the same frame")
         print(json.dumps(out), flush=True)
-    for g in groups:
-        g.close()
+        if out["parity"] is not None and not out["parity"]["ok"]:
+            print(f"bench.py: the timed frames differ from the oracle: {out['parity']}", file=sys.stderr)
+            sys.exit(3)
+    if grp is not None:
+        grp.close()
     for c_ in ctxs:
         c_.close()
     if world > 1:

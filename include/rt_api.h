@@ -33,7 +33,8 @@ enum rt_status {
     RT_ERR_NO_SCENE = -4,  /* dispatch before rt_upload_scene / camera / light       */
     RT_ERR_BVH = -5,       /* node/index arrays are out of range or too deep         */
     RT_ERR_NO_DEVICE = -6, /* no HIP device with that ordinal                        */
-    RT_ERR_COMM = -7       /* an RCCL call failed (rt_group.h)                       */
+    RT_ERR_COMM = -7,      /* an RCCL call failed (rt_group.h)                       */
+    RT_ERR_TIMEOUT = -8    /* a group's frames did not finish in time (rt_group.h)   */
 };
 
 /* Uniforms of gpu_shader.comp:126-130, set by src/main.cpp:357-361.
@@ -210,7 +211,8 @@ int rt_set_launch(struct rt_ctx* ctx, int waves_per_block, int persistent);
  * >= maxBounces = all packet. Default (auto): 1 -- camera rays and their shadow
  * rays walk as packets (coherent), reflections per lane (measured fastest on
  * configs 2, 3 and 5) -- and all packets for Moller-Trumbore frames over
- * reference trees of fewer than 1024 nodes. Same image for every value. */
+ * reference trees of fewer than 1024 nodes. -1 restores that automatic policy.
+ * Same image for every value. */
 int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 
 /* Tile dispatch order of the accelerated kernel. RT_SCHED_ROWS: row-major.

@@ -26,11 +26,21 @@
  *    `nranks`, and the ranks meet through the 128-byte id that rank 0 makes
  *    with rt_group_unique_id and sends to the others (ncclCommInitRank).
  *
- * Frames in flight: a group renders one frame at a time (its members' streams
- * order frame k+1's render after frame k's gather). A caller that wants
- * several frames in flight makes several groups and deals frames round-robin.
- * Every call returns an rt_status (rt_api.h); RT_ERR_COMM for RCCL failures
- * (and for RCCL forced on a device list with repeats).
+ * Frames in flight (rt_group_set_frames): each member holds F slots (a
+ * context, a render stream, the frame's buffers) but ONE communicator and ONE
+ * fan-in stream. Frame f renders in slot f mod F; its fan-in is queued on the
+ * fan-in stream behind that render, so frame f + 1 renders while frame f
+ * crosses the links, and every rank posts its sends/receives in frame order on
+ * a single communicator.
+ *
+ * Errors. Every call returns an rt_status (rt_api.h); RT_ERR_COMM for RCCL
+ * failures (and for RCCL forced on a device list with repeats). In an RCCL
+ * group of more than one rank, an error inside rt_group_dispatch, an RCCL
+ * asynchronous error, or an rt_group_sync that runs past the timeout aborts the
+ * communicator (ncclCommAbort): peers may already have posted their half of a
+ * fan-in that will never be matched. Such a group is unusable -- every later
+ * call returns RT_ERR_COMM -- and every rank must destroy its group; the peers
+ * see RT_ERR_COMM or RT_ERR_TIMEOUT from their own rt_group_sync.
  */
 #ifndef RT_GROUP_H
 #define RT_GROUP_H
@@ -69,8 +79,16 @@ int rt_group_destroy(struct rt_group* g);
 int rt_group_info(struct rt_group* g, int* nranks, int* nlocal, int* transport);
 
 /* The context of local member k (0 <= k < nlocal), for per-context settings
- * (rt_set_kernel, rt_set_walk, rt_kernel_times, ...). Owned by the group. */
+ * (rt_set_kernel, rt_set_walk, rt_kernel_times, ...); slot 0's with frames in
+ * flight. Owned by the group. */
 int rt_group_member(struct rt_group* g, int k, struct rt_ctx** ctx);
+/* Member k's context of frame slot `slot` (0 <= slot < frames). */
+int rt_group_member_slot(struct rt_group* g, int k, int slot, struct rt_ctx** ctx);
+
+/* Frames in flight, 1..16 (default 1): call before rt_group_upload_scene. Frame f
+ * renders in slot f mod frames. rt_group_frames returns the count. */
+int rt_group_set_frames(struct rt_group* g, int frames);
+int rt_group_frames(struct rt_group* g);
 
 /* rt_upload_scene / rt_set_camera / rt_set_light / rt_set_params on every
  * local member (the scene is replicated: < 1 MB for the car, 28 MB at 100k). */
@@ -96,10 +114,31 @@ int rt_group_set_root_share(struct rt_group* g, int share);
  * (width, height, stripe) frame at the current share, summed. Synchronous. */
 int rt_group_collect_stats(struct rt_group* g, int width, int height, int stripe, rt_stats* out);
 
-/* Wait until this process's members have finished their last frame. */
+/* Wait until this process's members have finished every dispatched frame.
+ * Bounded: it polls the streams and the communicator's asynchronous error
+ * (ncclCommGetAsyncError) and gives up after the timeout (default 60 s),
+ * aborting the communicator: RT_ERR_TIMEOUT, or RT_ERR_COMM on an RCCL error. */
 int rt_group_sync(struct rt_group* g);
+/* The timeout of rt_group_sync in ms (0 = none). */
+int rt_group_set_timeout(struct rt_group* g, double ms);
+/* Non-blocking: RT_ERR_COMM (and the communicator aborted) once RCCL reports an
+ * asynchronous error, else RT_OK. */
+int rt_group_check(struct rt_group* g);
 
-/* Rank 0's surface (RT_ERR_INVALID in a process without rank 0). read_image
+/* Mean device times (ms) of the frames dispatched since the last call, of this
+ * process's rank 0 member (else its first member), from HIP events: its stripes'
+ * render, its fan-in (from the moment its stream may start it -- its own rows
+ * rendered, or on rank 0 the slot free -- to the last byte sent / received, so it
+ * includes waiting for the slowest peer), rank 0's unstripe, and render start to
+ * the frame's last event. Waits (bounded) for the outstanding frames. */
+typedef struct rt_group_phases {
+    int frames;
+    float render_ms, fanin_ms, unstripe_ms, frame_ms;
+} rt_group_phases;
+int rt_group_phase_times(struct rt_group* g, rt_group_phases* out);
+
+/* Rank 0's surface of the LAST dispatched frame (each frame slot has its own;
+ * RT_ERR_INVALID in a process without rank 0). read_image waits (bounded) and
  * copies the whole frame; width/height must equal the last dispatch's. */
 int rt_group_read_image(struct rt_group* g, float* host_dst, size_t pitch, int width, int height);
 int rt_group_device_image(struct rt_group* g, void** ptr, size_t* pitch);

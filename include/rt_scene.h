@@ -29,7 +29,9 @@ enum rts_config {
     RTS_CONFIG_SPHERES = 1,   /* config 1: 4 spheres + 1 plane, 800x600 (CPU path)        */
     RTS_CONFIG_MONKEY = 2,    /* config 2: 1,240 shapes, 800x600, primary + shadow        */
     RTS_CONFIG_CAR = 3,       /* config 3/4: 4,022 triangles + 100 spheres                */
-    RTS_CONFIG_RANDOM = 5     /* config 5: 100k random triangles, deep BVH                */
+    RTS_CONFIG_RANDOM = 5,    /* config 5: 100k random triangles, deep BVH                */
+    RTS_CONFIG_TRIANGLE = 6   /* the reference's default SCENE 3 (generateScene3): one
+                                 triangle, no BVH built (0 nodes, 0 indices)               */
 };
 
 struct rts_scene* rts_new(void);

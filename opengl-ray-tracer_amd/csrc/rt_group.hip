@@ -14,6 +14,14 @@
 // repeated devices, peer copies into rank 0's staging. k_unstripe then scatters
 // the slots back into image order in rank 0's pitched surface: one coalesced
 // read and one streaming write per pixel (25 + 33 MB at 1080p, ~10 us).
+//
+// Frames in flight (rt_group_set_frames): every member holds F slots -- a
+// context, a render stream and the frame's buffers -- and ONE communicator with
+// ONE fan-in stream. Frame f renders in slot f mod F; its fan-in is queued on
+// the fan-in stream behind the slot's render (an event), so frame f + 1 renders
+// while frame f crosses the links, and every rank posts its send/recv in the
+// same frame order on one stream of one communicator: no two communicators ever
+// wait on each other. rank 0 unstripes each slot into that slot's own surface.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -24,17 +32,40 @@
 
 #include "../../include/rt_api.h"
 #include "../../include/rt_group.h"
+#include "group_wait.h"
 
 namespace {
 
+constexpr int kMaxFrames = 16;   // rt_group_set_frames
+constexpr int kPhaseRing = 64;   // frames whose phase events are kept before they are read
+
+struct Slot {
+    rt_ctx* ctx = nullptr;
+    hipStream_t stream = nullptr;  // this slot's render (and, on rank 0, unstripe) stream
+    float* buf = nullptr;          // ranks >= 1: compact stripes, rows x W packed RGB32F (12 B per pixel)
+    size_t buf_cap = 0;            // bytes
+    float* staging = nullptr;      // rank 0: its rows, then P - 1 slots of rows1 x W packed RGB
+    size_t staging_cap = 0;
+    float* img = nullptr;          // rank 0: this slot's gathered frame (RGBA32F, pitched)
+    size_t img_pitch = 0;
+    int img_w = 0, img_h = 0;
+    hipEvent_t rendered = nullptr;  // this member's stripes are written
+    hipEvent_t fanned = nullptr;    // the fan-in of the slot's frame is done (sent / received / copied)
+    hipEvent_t released = nullptr;  // the slot's buffers may be written again
+    bool used = false;              // `released` / `fanned` have been recorded
+};
+
 struct Member {
     int rank = 0, device = 0;
-    rt_ctx* ctx = nullptr;
-    hipStream_t stream = nullptr;
-    float* buf = nullptr;  // ranks >= 1: compact stripes, rows x W packed RGB32F (12 B per pixel)
-    size_t buf_cap = 0;    // bytes
+    std::vector<Slot> slot;
+    hipStream_t cstream = nullptr;  // fan-in stream: every frame's send/recv (or copies) in frame order
     ncclComm_t comm = nullptr;
-    hipEvent_t rendered = nullptr;  // copy transport: this member's stripes are in buf
+};
+
+// Device-time events of one frame of the timed member (rt_group_phase_times).
+struct PhaseRec {
+    hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // render 0/1, fan-in 0/1, unstripe 0/1
+    bool pending = false, has_fan = false, has_unstripe = false;
 };
 
 // The rows of rank `rank` (stripe `s`, P ranks, rank 0's share k): rank 0 owns
@@ -79,15 +110,20 @@ struct rt_group {
     int nranks = 0;
     int transport = RT_GATHER_COPY;
     std::vector<Member> m;
-    int root = -1;  // local index of rank 0, -1 if another process holds it
-    int share = 1;  // rank 0's stripes per period (rt_group_set_root_share)
-    float* staging = nullptr;  // root: rank 0's rows, then P - 1 slots of rows1 x W packed RGB
-    size_t staging_cap = 0;
-    float* img = nullptr;      // root: the gathered frame
-    size_t img_pitch = 0;
-    int img_w = 0, img_h = 0;
-    hipEvent_t gathered = nullptr;  // copy transport: root has read every member's buf
-    bool gathered_valid = false;
+    int root = -1;     // local index of rank 0, -1 if another process holds it
+    int share = 1;     // rank 0's stripes per period (rt_group_set_root_share)
+    int frames = 1;    // slots per member (rt_group_set_frames)
+    long long next = 0;  // frames dispatched
+    int last_slot = -1;  // slot of the last dispatched frame
+    bool have_scene = false;
+    bool broken = false;        // an RCCL group after an abort: every call fails
+    double timeout_ms = 60000;  // rt_group_set_timeout
+    // phase times of member `tm` (rank 0 when local, else the first member)
+    int tm = 0;
+    std::vector<PhaseRec> ring;
+    int ring_pos = 0;
+    double sum[4] = {0, 0, 0, 0};  // render, fan-in, unstripe, frame (ms)
+    int nsum[4] = {0, 0, 0, 0};
 };
 
 namespace {
@@ -100,28 +136,43 @@ namespace {
     do {                                                  \
         if ((x) != ncclSuccess) return RT_ERR_COMM;       \
     } while (0)
+#define G_TRY(x)                             \
+    do {                                     \
+        const int rc__ = (x);                \
+        if (rc__ != RT_OK) return rc__;      \
+    } while (0)
+
+int add_slot(Member& b) {
+    b.slot.emplace_back();
+    Slot& s = b.slot.back();
+    G_TRY(rt_create(&s.ctx, b.device));
+    G_HIP(hipSetDevice(b.device));
+    G_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    G_HIP(hipEventCreateWithFlags(&s.rendered, hipEventDisableTiming));
+    G_HIP(hipEventCreateWithFlags(&s.fanned, hipEventDisableTiming));
+    G_HIP(hipEventCreateWithFlags(&s.released, hipEventDisableTiming));
+    return rt_set_stream(s.ctx, s.stream);
+}
 
 int add_member(rt_group* g, int rank, int device) {
     Member mb;
     mb.rank = rank;
     mb.device = device;
-    int rc = rt_create(&mb.ctx, device);
-    if (rc != RT_OK) return rc;
     g->m.push_back(mb);  // owned from here (rt_group_destroy frees it)
     Member& b = g->m.back();
     G_HIP(hipSetDevice(device));
-    G_HIP(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
-    G_HIP(hipEventCreateWithFlags(&b.rendered, hipEventDisableTiming));
-    return rt_set_stream(b.ctx, b.stream);
+    G_HIP(hipStreamCreateWithFlags(&b.cstream, hipStreamNonBlocking));
+    return add_slot(b);
 }
 
 int finish_create(rt_group* g) {
     for (size_t k = 0; k < g->m.size(); ++k)
         if (g->m[k].rank == 0) g->root = static_cast<int>(k);
-    if (g->root >= 0) {
-        G_HIP(hipSetDevice(g->m[g->root].device));
-        G_HIP(hipEventCreateWithFlags(&g->gathered, hipEventDisableTiming));
-    }
+    g->tm = g->root >= 0 ? g->root : 0;
+    G_HIP(hipSetDevice(g->m[g->tm].device));
+    g->ring.resize(kPhaseRing);
+    for (PhaseRec& p : g->ring)
+        for (hipEvent_t& e : p.ev) G_HIP(hipEventCreate(&e));
     return RT_OK;
 }
 
@@ -133,6 +184,95 @@ int grow(T*& p, size_t& cap, size_t bytes) {
     cap = 0;
     if (hipMalloc(&p, bytes) != hipSuccess) return RT_ERR_NO_MEMORY;
     cap = bytes;
+    return RT_OK;
+}
+
+// Every communicator aborted: its pending kernels return, and the group is unusable
+// (a peer may have posted a send or receive this process will never match).
+void abort_comms(rt_group* g) {
+    for (Member& b : g->m)
+        if (b.comm) {
+            hipSetDevice(b.device);
+            ncclCommAbort(b.comm);
+            b.comm = nullptr;
+        }
+    if (g->transport == RT_GATHER_RCCL) g->broken = true;
+}
+
+// An error after this process may have left its peers waiting on a fan-in.
+int fail(rt_group* g, int rc) {
+    if (g->transport == RT_GATHER_RCCL && g->nranks > 1) abort_comms(g);
+    return rc;
+}
+
+// Outstanding work on any of the group's streams: 1 yes, 0 none, -1 device error.
+int pending(rt_group* g) {
+    for (Member& b : g->m) {
+        if (hipSetDevice(b.device) != hipSuccess) return -1;
+        auto q = [](hipStream_t s) {
+            if (!s) return 0;
+            const hipError_t e = hipStreamQuery(s);
+            return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+        };
+        int r = q(b.cstream);
+        if (r) return r;
+        for (Slot& s : b.slot)
+            if ((r = q(s.stream))) return r;
+    }
+    return 0;
+}
+
+bool comm_error(rt_group* g) {
+    for (Member& b : g->m) {
+        if (!b.comm) continue;
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(b.comm, &st) != ncclSuccess) return true;
+        if (st != ncclSuccess && st != ncclInProgress) return true;
+    }
+    return false;
+}
+
+// The bounded wait (group_wait.h); on a timeout or an RCCL error the communicators
+// are aborted.
+int wait_all(rt_group* g) {
+    const rtg::WaitResult w = rtg::wait_bounded([g] { return pending(g); }, [g] { return comm_error(g); },
+                                                 g->timeout_ms);
+    if (w == rtg::kWaitDone) return RT_OK;
+    if (w == rtg::kWaitDeviceError) return fail(g, RT_ERR_DEVICE);
+    abort_comms(g);
+    return w == rtg::kWaitTimeout ? RT_ERR_TIMEOUT : RT_ERR_COMM;
+}
+
+void harvest(rt_group* g, PhaseRec& p) {
+    if (!p.pending) return;
+    p.pending = false;
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, p.ev[0], p.ev[1]) == hipSuccess) {
+        g->sum[0] += ms;
+        ++g->nsum[0];
+    }
+    if (p.has_fan && hipEventElapsedTime(&ms, p.ev[2], p.ev[3]) == hipSuccess) {
+        g->sum[1] += ms;
+        ++g->nsum[1];
+    }
+    if (p.has_unstripe && hipEventElapsedTime(&ms, p.ev[4], p.ev[5]) == hipSuccess) {
+        g->sum[2] += ms;
+        ++g->nsum[2];
+    }
+    const hipEvent_t last = p.has_unstripe ? p.ev[5] : (p.has_fan ? p.ev[3] : p.ev[1]);
+    if (hipEventElapsedTime(&ms, p.ev[0], last) == hipSuccess) {
+        g->sum[3] += ms;
+        ++g->nsum[3];
+    }
+}
+
+// Every slot context of every local member.
+template <class F>
+int each_ctx(rt_group* g, F f) {
+    if (!g) return RT_ERR_INVALID;
+    if (g->broken) return RT_ERR_COMM;
+    for (Member& b : g->m)
+        for (Slot& s : b.slot) G_TRY(f(s.ctx));
     return RT_OK;
 }
 
@@ -166,6 +306,7 @@ int rt_group_create(rt_group** out, const int* devices, int n, int transport) {
     g->transport = (transport == RT_GATHER_RCCL || (transport == RT_GATHER_AUTO && distinct && n > 1))
                        ? RT_GATHER_RCCL
                        : RT_GATHER_COPY;
+    g->m.reserve(n);
     int rc = RT_OK;
     for (int k = 0; k < n && rc == RT_OK; ++k) rc = add_member(g, k, devices[k]);
     if (rc == RT_OK && g->transport == RT_GATHER_RCCL) {
@@ -210,23 +351,29 @@ int rt_group_create_rank(rt_group** out, const void* id, int nranks, int rank, i
 
 int rt_group_destroy(rt_group* g) {
     if (!g) return RT_ERR_INVALID;
-    for (Member& b : g->m) {
-        hipSetDevice(b.device);
-        if (b.stream) hipStreamSynchronize(b.stream);
-    }
+    // a group whose fan-in never completes must not hang its owner: bounded, then abort
+    if (!g->broken && wait_all(g) != RT_OK) abort_comms(g);
     for (Member& b : g->m) {
         hipSetDevice(b.device);
         if (b.comm) ncclCommDestroy(b.comm);
-        if (b.ctx) rt_destroy(b.ctx);  // before its stream goes: it is ordered on it
-        if (b.buf) hipFree(b.buf);
-        if (b.rendered) hipEventDestroy(b.rendered);
-        if (b.stream) hipStreamDestroy(b.stream);
+        for (Slot& s : b.slot) {
+            if (!g->broken) hipStreamSynchronize(s.stream);
+            if (s.ctx) rt_destroy(s.ctx);  // before its stream goes: it is ordered on it
+            hipFree(s.buf);
+            hipFree(s.staging);
+            hipFree(s.img);
+            if (s.rendered) hipEventDestroy(s.rendered);
+            if (s.fanned) hipEventDestroy(s.fanned);
+            if (s.released) hipEventDestroy(s.released);
+            if (s.stream) hipStreamDestroy(s.stream);
+        }
+        if (b.cstream) hipStreamDestroy(b.cstream);
     }
-    if (g->root >= 0) {
-        hipSetDevice(g->m[g->root].device);
-        hipFree(g->staging);
-        hipFree(g->img);
-        if (g->gathered) hipEventDestroy(g->gathered);
+    if (!g->m.empty()) {
+        hipSetDevice(g->m[g->tm].device);
+        for (PhaseRec& p : g->ring)
+            for (hipEvent_t e : p.ev)
+                if (e) hipEventDestroy(e);
     }
     delete g;
     return RT_OK;
@@ -240,153 +387,209 @@ int rt_group_info(rt_group* g, int* nranks, int* nlocal, int* transport) {
     return RT_OK;
 }
 
-int rt_group_member(rt_group* g, int k, rt_ctx** ctx) {
-    if (!g || !ctx || k < 0 || k >= static_cast<int>(g->m.size())) return RT_ERR_INVALID;
-    *ctx = g->m[k].ctx;
+int rt_group_set_frames(rt_group* g, int frames) {
+    if (!g || frames < 1 || frames > kMaxFrames || g->have_scene || g->next > 0) return RT_ERR_INVALID;
+    if (g->broken) return RT_ERR_COMM;
+    for (Member& b : g->m)
+        while (static_cast<int>(b.slot.size()) < frames) G_TRY(add_slot(b));
+    g->frames = frames;
+    return RT_OK;
+}
+
+int rt_group_frames(rt_group* g) { return g ? g->frames : RT_ERR_INVALID; }
+
+int rt_group_member(rt_group* g, int k, rt_ctx** ctx) { return rt_group_member_slot(g, k, 0, ctx); }
+
+int rt_group_member_slot(rt_group* g, int k, int slot, rt_ctx** ctx) {
+    if (!g || !ctx || k < 0 || k >= static_cast<int>(g->m.size()) || slot < 0 || slot >= g->frames)
+        return RT_ERR_INVALID;
+    *ctx = g->m[k].slot[slot].ctx;
     return RT_OK;
 }
 
 int rt_group_upload_scene(rt_group* g, const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx,
                           int I) {
-    if (!g) return RT_ERR_INVALID;
-    for (Member& b : g->m) {
-        const int rc = rt_upload_scene(b.ctx, shapes, S, nodes, N, idx, I);
-        if (rc != RT_OK) return rc;
-    }
-    return RT_OK;
+    const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_upload_scene(c, shapes, S, nodes, N, idx, I); });
+    if (rc == RT_OK) g->have_scene = true;
+    return rc;
 }
 
 int rt_group_set_camera(rt_group* g, const FlatCamera* cam) {
-    if (!g) return RT_ERR_INVALID;
-    for (Member& b : g->m) {
-        const int rc = rt_set_camera(b.ctx, cam);
-        if (rc != RT_OK) return rc;
-    }
-    return RT_OK;
+    return each_ctx(g, [&](rt_ctx* c) { return rt_set_camera(c, cam); });
 }
 
 int rt_group_set_light(rt_group* g, const FlatLight* l) {
-    if (!g) return RT_ERR_INVALID;
-    for (Member& b : g->m) {
-        const int rc = rt_set_light(b.ctx, l);
-        if (rc != RT_OK) return rc;
-    }
-    return RT_OK;
+    return each_ctx(g, [&](rt_ctx* c) { return rt_set_light(c, l); });
 }
 
 int rt_group_set_params(rt_group* g, const rt_params* p) {
-    if (!g) return RT_ERR_INVALID;
-    for (Member& b : g->m) {
-        const int rc = rt_set_params(b.ctx, p);
-        if (rc != RT_OK) return rc;
-    }
-    return RT_OK;
+    return each_ctx(g, [&](rt_ctx* c) { return rt_set_params(c, p); });
 }
 
 int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     if (!g || width <= 0 || height <= 0 || stripe <= 0 || height > 65535 ||
         stripe > 65535 / (g->share + g->nranks - 1))
         return RT_ERR_INVALID;
+    if (g->broken) return RT_ERR_COMM;
     const int P = g->nranks, k = g->share;
+    const int j = static_cast<int>(g->next % g->frames);
     const size_t row_b = static_cast<size_t>(width) * 12;  // packed RGB32F
     const int rows0 = rank_rows(height, P, stripe, k, 0).rows;
     const int rows1 = P > 1 ? rank_rows(height, P, stripe, k, 1).rows : 0;  // the most among ranks >= 1
-    const size_t slot = std::max<size_t>(1, static_cast<size_t>(rows1) * row_b);
+    const size_t slot_b = std::max<size_t>(1, static_cast<size_t>(rows1) * row_b);
     const size_t stage = static_cast<size_t>(rows0) * row_b + static_cast<size_t>(P - 1) * rows1 * row_b;
-    auto slot_ptr = [&](int rank) {  // rank's rows in the staging buffer
-        return reinterpret_cast<char*>(g->staging) +
-               (rank == 0 ? 0 : static_cast<size_t>(rows0) * row_b + static_cast<size_t>(rank - 1) * rows1 * row_b);
-    };
-    // (Re)size the buffers; a resize waits for the frames that still use them.
+    // (Re)size slot j's buffers; a resize waits for the frames that still use them.
     bool resize = false;
-    for (Member& b : g->m) resize = resize || (b.rank != 0 && b.buf_cap < slot);
-    if (g->root >= 0)
-        resize = resize || g->staging_cap < stage || g->img_w != width || g->img_h != height;
+    for (Member& b : g->m) {
+        const Slot& s = b.slot[j];
+        resize = resize || (b.rank != 0 && s.buf_cap < slot_b) ||
+                 (b.rank == 0 && (s.staging_cap < stage || s.img_w != width || s.img_h != height));
+    }
     if (resize) {
+        G_TRY(wait_all(g));
         for (Member& b : g->m) {
+            Slot& s = b.slot[j];
             G_HIP(hipSetDevice(b.device));
-            G_HIP(hipStreamSynchronize(b.stream));
-            if (b.rank == 0) continue;
-            const int rc = grow(b.buf, b.buf_cap, slot);
-            if (rc != RT_OK) return rc;
-        }
-        if (g->root >= 0) {
-            Member& r = g->m[g->root];
-            G_HIP(hipSetDevice(r.device));
-            int rc = grow(g->staging, g->staging_cap, std::max<size_t>(stage, 16));
-            if (rc != RT_OK) return rc;
-            if (g->img_w != width || g->img_h != height) {
-                hipFree(g->img);
-                g->img = nullptr;
-                g->img_w = g->img_h = 0;
+            if (b.rank != 0) {
+                G_TRY(grow(s.buf, s.buf_cap, slot_b));
+                continue;
+            }
+            G_TRY(grow(s.staging, s.staging_cap, std::max<size_t>(stage, 16)));
+            if (s.img_w != width || s.img_h != height) {
+                hipFree(s.img);
+                s.img = nullptr;
+                s.img_w = s.img_h = 0;
                 size_t pitch = 0;
-                if (hipMallocPitch(reinterpret_cast<void**>(&g->img), &pitch, static_cast<size_t>(width) * 16,
+                if (hipMallocPitch(reinterpret_cast<void**>(&s.img), &pitch, static_cast<size_t>(width) * 16,
                                    height) != hipSuccess)
                     return RT_ERR_NO_MEMORY;
-                g->img_pitch = pitch;
-                g->img_w = width;
-                g->img_h = height;
+                s.img_pitch = pitch;
+                s.img_w = width;
+                s.img_h = height;
             }
         }
     }
-    // 1. every local rank renders its stripes on its own stream (rank 0 straight into
-    //    its staging rows; the others into buf, sent after the render)
-    for (Member& b : g->m) {
-        G_HIP(hipSetDevice(b.device));
-        if (g->transport == RT_GATHER_COPY && g->gathered_valid && b.rank != 0)
-            G_HIP(hipStreamWaitEvent(b.stream, g->gathered, 0));  // root has read the previous frame's buf
-        const Rows w = rank_rows(height, P, stripe, k, b.rank);
-        if (w.rows == 0) continue;
-        float* dst = b.rank == 0 ? g->staging : b.buf;
-        const int rc = rt_dispatch_rows_ex(b.ctx, width, height, w.y0, w.stripe, w.period, w.rows, dst, row_b,
-                                           RT_FORMAT_RGB32F);
-        if (rc != RT_OK) return rc;
+    PhaseRec& ph = g->ring[g->ring_pos];
+    if (ph.pending) {  // kPhaseRing frames ago: read its times (it has long finished)
+        hipSetDevice(g->m[g->tm].device);
+        if (hipEventSynchronize(ph.ev[ph.has_unstripe ? 5 : (ph.has_fan ? 3 : 1)]) != hipSuccess)
+            return fail(g, RT_ERR_DEVICE);
+        harvest(g, ph);
     }
-    // 2. fan-in to rank 0's staging: rank r's rows to slot r
+    ph.has_fan = ph.has_unstripe = false;
+    // 1. every local rank renders its stripes on slot j's stream (rank 0 straight into
+    //    its staging rows; the others into buf, once the fan-in of the frame that
+    //    last used the slot has sent it)
+    for (size_t mi = 0; mi < g->m.size(); ++mi) {
+        Member& b = g->m[mi];
+        Slot& s = b.slot[j];
+        const bool timed = static_cast<int>(mi) == g->tm;
+        if (hipSetDevice(b.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (s.used && b.rank != 0) {
+            // RCCL: released on this member's fan-in stream; copies: rank 0's copy of it
+            const hipEvent_t free_ev = g->transport == RT_GATHER_COPY ? g->m[g->root].slot[j].fanned : s.released;
+            if (hipStreamWaitEvent(s.stream, free_ev, 0) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        }
+        if (timed && hipEventRecord(ph.ev[0], s.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        const Rows w = rank_rows(height, P, stripe, k, b.rank);
+        if (w.rows > 0) {
+            float* dst = b.rank == 0 ? s.staging : s.buf;
+            const int rc = rt_dispatch_rows_ex(s.ctx, width, height, w.y0, w.stripe, w.period, w.rows, dst, row_b,
+                                               RT_FORMAT_RGB32F);
+            if (rc != RT_OK) return fail(g, rc);
+        }
+        if (timed && hipEventRecord(ph.ev[1], s.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (hipEventRecord(s.rendered, s.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+    }
+    auto slot_ptr = [&](int rank) {  // rank's rows in slot j's staging buffer
+        return reinterpret_cast<char*>(g->m[g->root].slot[j].staging) +
+               (rank == 0 ? 0 : static_cast<size_t>(rows0) * row_b + static_cast<size_t>(rank - 1) * rows1 * row_b);
+    };
+    // 2. fan-in to rank 0's staging on the members' fan-in streams, in frame order
     if (g->transport == RT_GATHER_RCCL && P > 1) {
-        G_NCCL(ncclGroupStart());
+        for (size_t mi = 0; mi < g->m.size(); ++mi) {
+            Member& b = g->m[mi];
+            Slot& s = b.slot[j];
+            if (hipSetDevice(b.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            // a sender waits for its rows; rank 0 for the previous unstripe of this slot's staging
+            const hipEvent_t before = b.rank == 0 ? (s.used ? s.released : nullptr) : s.rendered;
+            if (before && hipStreamWaitEvent(b.cstream, before, 0) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            if (static_cast<int>(mi) == g->tm && hipEventRecord(ph.ev[2], b.cstream) != hipSuccess)
+                return fail(g, RT_ERR_DEVICE);
+        }
+        if (ncclGroupStart() != ncclSuccess) return fail(g, RT_ERR_COMM);
         for (Member& b : g->m) {
+            Slot& s = b.slot[j];
             ncclResult_t res = ncclSuccess;
             if (b.rank == 0) {
                 for (int r = 1; r < P && res == ncclSuccess; ++r) {
                     const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, r).rows) * width * 3;
-                    if (n) res = ncclRecv(slot_ptr(r), n, ncclFloat32, r, b.comm, b.stream);
+                    if (n) res = ncclRecv(slot_ptr(r), n, ncclFloat32, r, b.comm, b.cstream);
                 }
             } else {
                 const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, b.rank).rows) * width * 3;
-                if (n) res = ncclSend(b.buf, n, ncclFloat32, 0, b.comm, b.stream);
+                if (n) res = ncclSend(s.buf, n, ncclFloat32, 0, b.comm, b.cstream);
             }
             if (res != ncclSuccess) {
                 ncclGroupEnd();
-                return RT_ERR_COMM;
+                return fail(g, RT_ERR_COMM);
             }
         }
-        G_NCCL(ncclGroupEnd());
-    } else if (g->transport == RT_GATHER_COPY) {
-        Member& r = g->m[g->root];
-        for (Member& b : g->m) {
-            if (b.rank == 0) continue;
-            G_HIP(hipSetDevice(b.device));
-            G_HIP(hipEventRecord(b.rendered, b.stream));
+        if (ncclGroupEnd() != ncclSuccess) return fail(g, RT_ERR_COMM);
+        for (size_t mi = 0; mi < g->m.size(); ++mi) {
+            Member& b = g->m[mi];
+            Slot& s = b.slot[j];
+            if (hipSetDevice(b.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            if (static_cast<int>(mi) == g->tm) {
+                if (hipEventRecord(ph.ev[3], b.cstream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+                ph.has_fan = true;
+            }
+            if (hipEventRecord(s.fanned, b.cstream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            if (b.rank != 0) {
+                if (hipEventRecord(s.released, b.cstream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+                s.used = true;
+            }
         }
+    } else if (g->transport == RT_GATHER_COPY && P > 1) {
+        Member& r = g->m[g->root];
+        Slot& rs = r.slot[j];
         G_HIP(hipSetDevice(r.device));
+        if (rs.used) G_HIP(hipStreamWaitEvent(r.cstream, rs.released, 0));
+        if (g->tm == g->root) G_HIP(hipEventRecord(ph.ev[2], r.cstream));
         for (Member& b : g->m) {
             if (b.rank == 0) continue;
             const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, b.rank).rows) * row_b;
-            G_HIP(hipStreamWaitEvent(r.stream, b.rendered, 0));
-            if (n) G_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank), r.device, b.buf, b.device, n, r.stream));
+            G_HIP(hipStreamWaitEvent(r.cstream, b.slot[j].rendered, 0));
+            if (n) G_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank), r.device, b.slot[j].buf, b.device, n, r.cstream));
+            b.slot[j].used = true;  // its next render waits for rs.fanned
         }
-        G_HIP(hipEventRecord(g->gathered, r.stream));
-        g->gathered_valid = true;
+        if (g->tm == g->root) {
+            G_HIP(hipEventRecord(ph.ev[3], r.cstream));
+            ph.has_fan = true;
+        }
+        G_HIP(hipEventRecord(rs.fanned, r.cstream));
     }
-    // 3. rank 0: stripes back into image order
+    // 3. rank 0: stripes back into image order, into slot j's surface
     if (g->root >= 0) {
         Member& r = g->m[g->root];
-        G_HIP(hipSetDevice(r.device));
-        hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, height), dim3(256), 0, r.stream, g->staging, rows0,
-                           rows1, width, stripe, k, k + P - 1, reinterpret_cast<f4v*>(g->img), g->img_pitch / 16);
-        G_HIP(hipGetLastError());
+        Slot& rs = r.slot[j];
+        if (hipSetDevice(r.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (P > 1 && hipStreamWaitEvent(rs.stream, rs.fanned, 0) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (g->tm == g->root && hipEventRecord(ph.ev[4], rs.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, height), dim3(256), 0, rs.stream, rs.staging, rows0,
+                           rows1, width, stripe, k, k + P - 1, reinterpret_cast<f4v*>(rs.img), rs.img_pitch / 16);
+        if (hipGetLastError() != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (g->tm == g->root) {
+            if (hipEventRecord(ph.ev[5], rs.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            ph.has_unstripe = true;
+        }
+        if (hipEventRecord(rs.released, rs.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        rs.used = true;
     }
+    ph.pending = true;
+    g->ring_pos = (g->ring_pos + 1) % kPhaseRing;
+    g->last_slot = j;
+    ++g->next;
     return RT_OK;
 }
 
@@ -399,13 +602,13 @@ int rt_group_set_root_share(rt_group* g, int share) {
 int rt_group_collect_stats(rt_group* g, int width, int height, int stripe, rt_stats* out) {
     if (!g || !out || width <= 0 || height <= 0 || stripe <= 0 || stripe > 65535 / (g->share + g->nranks - 1))
         return RT_ERR_INVALID;
+    if (g->broken) return RT_ERR_COMM;
     std::memset(out, 0, sizeof *out);
     for (Member& b : g->m) {
         const Rows w = rank_rows(height, g->nranks, stripe, g->share, b.rank);
         if (w.rows == 0) continue;
         rt_stats st;
-        const int rc = rt_collect_stats_ex(b.ctx, width, height, w.y0, w.stripe, w.period, w.rows, &st);
-        if (rc != RT_OK) return rc;
+        G_TRY(rt_collect_stats_ex(b.slot[0].ctx, width, height, w.y0, w.stripe, w.period, w.rows, &st));
         uint64_t* o = reinterpret_cast<uint64_t*>(out);
         const uint64_t* a = reinterpret_cast<const uint64_t*>(&st);
         for (size_t i = 0; i < sizeof st / sizeof(uint64_t); ++i) o[i] += a[i];
@@ -413,31 +616,65 @@ int rt_group_collect_stats(rt_group* g, int width, int height, int stripe, rt_st
     return RT_OK;
 }
 
+int rt_group_set_timeout(rt_group* g, double ms) {
+    if (!g || !(ms >= 0)) return RT_ERR_INVALID;
+    g->timeout_ms = ms;
+    return RT_OK;
+}
+
+int rt_group_check(rt_group* g) {
+    if (!g) return RT_ERR_INVALID;
+    if (g->broken) return RT_ERR_COMM;
+    if (comm_error(g)) {
+        abort_comms(g);
+        return RT_ERR_COMM;
+    }
+    return RT_OK;
+}
+
 int rt_group_sync(rt_group* g) {
     if (!g) return RT_ERR_INVALID;
-    for (Member& b : g->m) {
-        G_HIP(hipSetDevice(b.device));
-        G_HIP(hipStreamSynchronize(b.stream));
+    if (g->broken) return RT_ERR_COMM;
+    return wait_all(g);
+}
+
+int rt_group_phase_times(rt_group* g, rt_group_phases* out) {
+    if (!g || !out) return RT_ERR_INVALID;
+    G_TRY(rt_group_sync(g));
+    hipSetDevice(g->m[g->tm].device);
+    for (PhaseRec& p : g->ring) harvest(g, p);
+    out->frames = g->nsum[3];
+    out->render_ms = g->nsum[0] ? static_cast<float>(g->sum[0] / g->nsum[0]) : 0.f;
+    out->fanin_ms = g->nsum[1] ? static_cast<float>(g->sum[1] / g->nsum[1]) : 0.f;
+    out->unstripe_ms = g->nsum[2] ? static_cast<float>(g->sum[2] / g->nsum[2]) : 0.f;
+    out->frame_ms = g->nsum[3] ? static_cast<float>(g->sum[3] / g->nsum[3]) : 0.f;
+    for (int i = 0; i < 4; ++i) {
+        g->sum[i] = 0;
+        g->nsum[i] = 0;
     }
     return RT_OK;
 }
 
 int rt_group_read_image(rt_group* g, float* dst, size_t pitch, int width, int height) {
-    if (!g || g->root < 0 || !dst || !g->img || width != g->img_w || height != g->img_h ||
-        pitch < static_cast<size_t>(width) * 16)
-        return RT_ERR_INVALID;
+    if (!g || g->root < 0 || !dst || g->last_slot < 0) return RT_ERR_INVALID;
     Member& r = g->m[g->root];
+    Slot& s = r.slot[g->last_slot];
+    if (!s.img || width != s.img_w || height != s.img_h || pitch < static_cast<size_t>(width) * 16)
+        return RT_ERR_INVALID;
+    G_TRY(rt_group_sync(g));
     G_HIP(hipSetDevice(r.device));
-    G_HIP(hipMemcpy2DAsync(dst, pitch, g->img, g->img_pitch, static_cast<size_t>(width) * 16, height,
-                           hipMemcpyDeviceToHost, r.stream));
-    G_HIP(hipStreamSynchronize(r.stream));
+    G_HIP(hipMemcpy2DAsync(dst, pitch, s.img, s.img_pitch, static_cast<size_t>(width) * 16, height,
+                           hipMemcpyDeviceToHost, s.stream));
+    G_HIP(hipStreamSynchronize(s.stream));
     return RT_OK;
 }
 
 int rt_group_device_image(rt_group* g, void** p, size_t* pitch) {
-    if (!g || g->root < 0 || !p || !pitch || !g->img) return RT_ERR_INVALID;
-    *p = g->img;
-    *pitch = g->img_pitch;
+    if (!g || g->root < 0 || !p || !pitch || g->last_slot < 0) return RT_ERR_INVALID;
+    const Slot& s = g->m[g->root].slot[g->last_slot];
+    if (!s.img) return RT_ERR_INVALID;
+    *p = s.img;
+    *pitch = s.img_pitch;
     return RT_OK;
 }
 

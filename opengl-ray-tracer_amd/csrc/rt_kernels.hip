@@ -3046,8 +3046,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 k2.heavy_parts = hp;
             }
         }
-        // The scene tree's boxes are not refit by rt_animate: animated scenes walk the reference tree.
-        // animated scenes keep it: rt_animate refits its boxes and items (prepare_animation)
+        // Animated scenes keep the scene tree: rt_animate refits its boxes and items (prepare_animation).
         const int troot = c->tree_mode == RT_TREE_SCENE ? c->st_root : kNoChild;
         // production shape on a dispatch that records no tile work: the counter-free kernel
 
@@ -3166,7 +3165,8 @@ const char* rt_status_string(int s) {
         case RT_ERR_NO_SCENE: return "scene, camera or light not uploaded";
         case RT_ERR_BVH: return "node/index arrays out of range or deeper than the 64-entry stack";
         case RT_ERR_NO_DEVICE: return "no such HIP device";
-        case RT_ERR_COMM: return "RCCL call failed";
+        case RT_ERR_COMM: return "RCCL call failed (the group's communicator is aborted)";
+        case RT_ERR_TIMEOUT: return "timed out waiting for a group's frames (the communicator is aborted)";
         default: return "unknown status";
     }
 }
@@ -3688,8 +3688,8 @@ extern "C" int rt_set_tree(rt_ctx* c, int mode) {
 extern "C" int rt_debug_anim_rebuilds(rt_ctx* c) { return c ? c->anim_rebuilds : -1; }
 
 extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
-    if (!c || lane_from_depth < 0) return RT_ERR_INVALID;
-    c->lane_from_depth = lane_from_depth;
+    if (!c || lane_from_depth < -1) return RT_ERR_INVALID;
+    c->lane_from_depth = lane_from_depth;  // -1: back to the automatic policy (walk_from)
     return RT_OK;
 }
 

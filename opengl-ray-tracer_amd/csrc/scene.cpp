@@ -571,6 +571,20 @@ void gen_random(rts_scene* s, float aspect) {
     s->build(25);
 }
 
+// The reference's default scene (`int SCENE = 3`, src/main.cpp:46): generateScene3
+// (:1196-1229) -- Camera() at (0,-10,40) with the window's aspect, the scene-2 light,
+// ONE Triangle((0,0,0), (5,0,0), (2.5,-5,0)) with the Material() defaults, LookAt
+// the origin. It never calls buildBVH: no nodes and no bvhIndices are serialised,
+// so the GLSL's BVH branch would start from bvhNodes[-1] (gpu_shader.comp:386).
+void gen_triangle(rts_scene* s, float aspect) {
+    const float cam[3] = {0.f, -10.f, 40.f}, lp[3] = {14.8f, -17.f, 17.f}, white[3] = {1.f, 1.f, 1.f};
+    rts_set_camera(s, cam, 60.f, aspect);  // Camera() default fov (src/camera.hpp:50)
+    rts_set_light(s, lp, white, 26.f);
+    const float a[3] = {0.f, 0.f, 0.f}, b[3] = {5.f, 0.f, 0.f}, c[3] = {2.5f, -5.f, 0.f};
+    rts_add_triangle(s, a, b, c, 0, nullptr);
+    rts_camera_look_at(s, a);
+}
+
 }  // namespace
 
 extern "C" {
@@ -890,6 +904,7 @@ int rts_generate(rts_scene* s, int config, int variant, float aspect) {
         case RTS_CONFIG_MONKEY: gen_monkey(s, aspect); break;
         case RTS_CONFIG_CAR: gen_car(s, variant, aspect); break;
         case RTS_CONFIG_RANDOM: gen_random(s, aspect); break;
+        case RTS_CONFIG_TRIANGLE: gen_triangle(s, aspect); break;
         default: return -1;
     }
     return 0;

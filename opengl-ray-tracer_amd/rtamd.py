@@ -116,7 +116,8 @@ def algorithmic_bytes(st: dict, pixels_written: int, use_mt: bool = False) -> in
 
 STATUS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "device allocation failed",
           -4: "scene, camera or light not uploaded", -5: "node/index arrays out of range or deeper than the 64-entry stack",
-          -6: "no such HIP device", -7: "RCCL call failed"}
+          -6: "no such HIP device", -7: "RCCL call failed (the group's communicator is aborted)",
+          -8: "timed out waiting for a group's frames (the communicator is aborted)"}
 
 
 class RTError(RuntimeError):
@@ -215,6 +216,12 @@ GROUP_SYMBOLS = {
     "rt_group_destroy": (_I, [_P]),
     "rt_group_info": (_I, [_P, _P, _P, _P]),
     "rt_group_member": (_I, [_P, _I, _P]),
+    "rt_group_member_slot": (_I, [_P, _I, _I, _P]),
+    "rt_group_set_frames": (_I, [_P, _I]),
+    "rt_group_frames": (_I, [_P]),
+    "rt_group_set_timeout": (_I, [_P, C.c_double]),
+    "rt_group_check": (_I, [_P]),
+    "rt_group_phase_times": (_I, [_P, _P]),
     "rt_group_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
     "rt_group_set_camera": (_I, [_P, _P]), "rt_group_set_light": (_I, [_P, _P]),
     "rt_group_set_params": (_I, [_P, _P]),
@@ -703,15 +710,25 @@ class _Member(ComputeShader):
         self._h = None
 
 
+class GroupPhases(C.Structure):
+    _fields_ = [("frames", C.c_int), ("render_ms", C.c_float), ("fanin_ms", C.c_float),
+                ("unstripe_ms", C.c_float), ("frame_ms", C.c_float)]
+
+
 class Group:
     """One frame over several GPUs (include/rt_group.h): interleaved row stripes
-    per rank, gathered to rank 0 by ncclGather (RCCL) or device copies.
+    per rank (rank 0 may take `share` stripes per period, set_root_share), gathered
+    to rank 0 by one grouped ncclSend/ncclRecv per frame over xGMI (RCCL) or by
+    device copies, then unstriped on rank 0.
 
     Group(devices=[0, 1, ...])            one process drives every device
     Group(uid=..., nranks=P, rank=r, device=d)   one process per GPU
+    frames=F: F frames in flight (slots), one communicator and one fan-in stream.
+    `members` holds each local member's slot-0 context, `contexts` every slot's.
     """
 
-    def __init__(self, devices=None, transport=GATHER_AUTO, uid=None, nranks=None, rank=None, device=None):
+    def __init__(self, devices=None, transport=GATHER_AUTO, uid=None, nranks=None, rank=None, device=None,
+                 frames=1):
         self._lib = rt_lib()
         h = C.c_void_p()
         if uid is not None:
@@ -725,11 +742,18 @@ class Group:
         n, nl, tr = C.c_int(), C.c_int(), C.c_int()
         self._chk(self._lib.rt_group_info(h, C.byref(n), C.byref(nl), C.byref(tr)), "rt_group_info")
         self.nranks, self.nlocal, self.transport = n.value, nl.value, tr.value
-        self.members = []
+        if frames != 1:
+            self._chk(self._lib.rt_group_set_frames(h, int(frames)), "rt_group_set_frames")
+        self.frames = self._lib.rt_group_frames(h)
+        self.members, self.contexts = [], []
         for k in range(self.nlocal):
-            c = C.c_void_p()
-            self._chk(self._lib.rt_group_member(h, k, C.byref(c)), "rt_group_member")
-            self.members.append(_Member(self._lib, c, device if uid is not None else int(devices[k])))
+            dev = device if uid is not None else int(devices[k])
+            for j in range(self.frames):
+                c = C.c_void_p()
+                self._chk(self._lib.rt_group_member_slot(h, k, j, C.byref(c)), "rt_group_member_slot")
+                self.contexts.append(_Member(self._lib, c, dev))
+                if j == 0:
+                    self.members.append(self.contexts[-1])
 
     @staticmethod
     def _chk(rc, what):
@@ -738,7 +762,7 @@ class Group:
 
     def close(self):
         if getattr(self, "_h", None):
-            for m in self.members:
+            for m in self.contexts:
                 m.close()
             self._lib.rt_group_destroy(self._h)
             self._h = None
@@ -782,7 +806,22 @@ class Group:
         return st.as_dict()
 
     def sync(self):
+        """Bounded wait (rt_group_set_timeout); RTError -8 / -7 with the communicator aborted."""
         self._chk(self._lib.rt_group_sync(self._h), "rt_group_sync")
+
+    def set_timeout(self, ms):
+        self._chk(self._lib.rt_group_set_timeout(self._h, float(ms)), "rt_group_set_timeout")
+
+    def check(self):
+        """Non-blocking RCCL asynchronous-error poll (rt_group_check)."""
+        self._chk(self._lib.rt_group_check(self._h), "rt_group_check")
+
+    def phase_times(self):
+        """Mean device ms of render / fan-in / unstripe / whole frame since the last call."""
+        p = GroupPhases()
+        self._chk(self._lib.rt_group_phase_times(self._h, C.byref(p)), "rt_group_phase_times")
+        return {"frames": p.frames, "render_ms": p.render_ms, "fanin_ms": p.fanin_ms,
+                "unstripe_ms": p.unstripe_ms, "frame_ms": p.frame_ms}
 
     def read_image(self, width, height):
         out = np.empty((height, width, 4), np.float32)

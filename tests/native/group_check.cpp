@@ -61,29 +61,31 @@ static int compare(const char* what, const std::vector<float>& ref, const std::v
 }
 
 static int run_group(const char* what, const Scene& s, const rt_params& p, int W, int H, int stripe,
-                     const int* devs, int n, int transport, const std::vector<float>& ref, int share = 1) {
+                     const int* devs, int n, int transport, const std::vector<float>& ref, int share = 1,
+                     int frames = 1) {
     rt_group* g = nullptr;
     const int rc = rt_group_create(&g, devs, n, transport);
     if (rc != RT_OK) {
         std::printf("%-44s create failed: %s\n", what, rt_status_string(rc));
         return 1;
     }
+    CHECK(rt_group_set_frames(g, frames));
     CHECK(rt_group_upload_scene(g, s.shapes.data(), static_cast<int>(s.shapes.size()), s.nodes.data(),
                                 static_cast<int>(s.nodes.size()), s.idx.data(), static_cast<int>(s.idx.size())));
     CHECK(rt_group_set_camera(g, &s.cam));
     CHECK(rt_group_set_light(g, &s.light));
     CHECK(rt_group_set_params(g, &p));
     CHECK(rt_group_set_root_share(g, share));
-    // three frames: the buffers are reused across frames, as in a render loop
-    for (int f = 0; f < 3; ++f) CHECK(rt_group_dispatch(g, W, H, stripe));
+    // 2F + 1 frames: every slot's buffers are reused across frames, as in a render loop
+    for (int f = 0; f < 2 * frames + 1; ++f) CHECK(rt_group_dispatch(g, W, H, stripe));
     CHECK(rt_group_sync(g));
     std::vector<float> img(static_cast<size_t>(W) * H * 4);
     CHECK(rt_group_read_image(g, img.data(), static_cast<size_t>(W) * 16, W, H));
     int nr = 0, nl = 0, tr = 0;
     CHECK(rt_group_info(g, &nr, &nl, &tr));
     char label[96];
-    std::snprintf(label, sizeof label, "%s [%d ranks, %s, share %d]", what, nr, tr == RT_GATHER_RCCL ? "rccl" : "copy",
-                  share);
+    std::snprintf(label, sizeof label, "%s [%d ranks, %s, share %d, %d in flight]", what, nr,
+                  tr == RT_GATHER_RCCL ? "rccl" : "copy", share, frames);
     // a short destination is refused, not overrun
     const int short_rc = rt_group_read_image(g, img.data(), static_cast<size_t>(W) * 16, W, H - 1);
     CHECK(rt_group_destroy(g));
@@ -134,6 +136,8 @@ int main(int argc, char** argv) {
     fails += run_group("stripes of 5 (ragged last stripe)", s, p, W, H, 5, zeros.data(), 3, RT_GATHER_COPY, ref);
     fails += run_group("stripe taller than the frame", s, p, W, H, H + 3, zeros.data(), 2, RT_GATHER_COPY, ref);
     fails += run_group("rccl, one rank per device", s, p, W, H, 8, zeros.data(), 1, RT_GATHER_RCCL, ref);
+    fails += run_group("frames in flight", s, p, W, H, 8, zeros.data(), 3, RT_GATHER_COPY, ref, 2, 4);
+    fails += run_group("rccl, frames in flight", s, p, W, H, 8, zeros.data(), 1, RT_GATHER_RCCL, ref, 1, 3);
     {
         rt_group* g = nullptr;
         const int rc = rt_group_create(&g, zeros.data(), 2, RT_GATHER_RCCL);
@@ -148,6 +152,7 @@ int main(int argc, char** argv) {
         fails += run_group("rccl over every device", s, p, W, H, 8, all.data(), ndev, RT_GATHER_RCCL, ref);
         fails += run_group("rccl over 2 devices", s, p, W, H, 8, all.data(), 2, RT_GATHER_RCCL, ref, 2);
         fails += run_group("rccl over every device", s, p, W, H, 8, all.data(), ndev, RT_GATHER_RCCL, ref, 2);
+        fails += run_group("rccl over every device", s, p, W, H, 8, all.data(), ndev, RT_GATHER_RCCL, ref, 1, 4);
     }
     std::printf("%s\n", fails ? "FAIL" : "OK");
     return fails ? 1 : 0;

@@ -3,6 +3,7 @@
 import ctypes as C
 import os
 import re
+import subprocess
 
 import pytest
 
@@ -35,7 +36,7 @@ def test_exports(header):
 
 def test_status_strings():
     lib = rtamd.rt_lib()
-    for code in range(0, -8, -1):
+    for code in range(0, -9, -1):
         assert lib.rt_status_string(code).decode() == rtamd.STATUS[code]
 
 
@@ -54,3 +55,14 @@ def test_kernel_is_gfx950():
     with open(os.path.join(rtamd.LIBDIR, "librtamd.so"), "rb") as f:
         blob = f.read()
     assert b"gfx950" in blob
+
+
+def test_group_wait_is_bounded():
+    """rt_group_sync's poll loop (csrc/group_wait.h) on the CPU with fake queries:
+    completion, a fan-in that never completes (the deadline fires instead of a
+    hang), an RCCL asynchronous error and a device error (tests/native/wait_check.cpp)."""
+    exe = os.path.join(ROOT, "tests", "native", "build", "wait_check")
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "native"), "build/wait_check"], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "wait_check ok" in r.stdout

@@ -30,8 +30,8 @@ def test_gpus_2_from_a_plain_invocation(mode):
 
 
 def test_strong_mode_over_rt_group_one_rank():
-    """The N > 1 default's code path (rt_group per frame in flight, ncclCommInitRank,
-    ncclGather, unstripe) with one rank: the 1-GPU rehearsal of what the driver's
+    """The N > 1 default's code path (rt_group, ncclCommInitRank, the grouped
+    ncclSend/ncclRecv fan-in, unstripe) with one rank: the 1-GPU rehearsal of what the driver's
     8-GPU run measures."""
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--mode", "strong", "--steps", "5",

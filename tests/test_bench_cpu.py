@@ -93,3 +93,24 @@ def test_inflight_plan_and_hardware_queues():
     # an explicit F; never above 32 queues; an export that already suffices is kept
     assert bench.plan_inflight(20, 1920, 1080, 1, False, False, "") == (20, "32")
     assert bench.plan_inflight(8, 1920, 1080, 1, False, False, "16") == (8, None)
+
+
+def test_parity_check_of_timed_frames():
+    """bench.parity_check: every in-flight context's last frame against the oracle rows."""
+    ref = np.random.default_rng(1).random((4, 8, 4)).astype(np.float32)
+    good = np.zeros((10, 8, 4), np.float32)
+    good[3:7] = ref
+    r = bench.parity_check([good, good.copy()], 3, ref, "t")
+    assert r["ok"] and r["bad_pixels"] == 0 and r["max_abs"] == 0 and r["frames_checked"] == 2
+    assert r["rows_checked"] == [3, 7]
+    bad = good.copy()
+    bad[4, 2, 1] += 2e-4
+    bad[5, 5, 0] = np.nan
+    r = bench.parity_check([good, bad], 3, ref, "t")
+    assert not r["ok"] and r["bad_pixels"] == 2 and r["max_abs"] == np.inf
+    # a NaN the oracle also produces is not a mismatch
+    ref2 = ref.copy()
+    ref2[0, 0, 0] = np.nan
+    g2 = good.copy()
+    g2[3, 0, 0] = np.nan
+    assert bench.parity_check([g2], 3, ref2, "t")["ok"]

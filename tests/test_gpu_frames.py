@@ -369,3 +369,155 @@ def test_rgb_format_equals_rgba(ctx):
     assert (rgba[..., 3] == 1).all()
     with pytest.raises(rtamd.RTError):
         ctx.dispatch_rows_rgb(W, H, y0, 8, 1, rows, out.data_ptr(), W * 12 - 4)
+
+
+# --------------------------------------------------------------------------
+# The reference's default scene (SCENE = 3, generateScene3, src/main.cpp:1196-1229)
+
+@pytest.mark.parametrize("mt", [0, 1], ids=["barycentric", "moller_trumbore"])
+@pytest.mark.parametrize("bvh", [1, 0], ids=["bvh_branch", "brute_branch"])
+@pytest.mark.parametrize("kernel", [rtamd.KERNEL_AUTO, rtamd.KERNEL_PACKET], ids=["auto", "packet"])
+def test_default_scene3_vs_oracle(ctx, bvh, mt, kernel):
+    """One triangle and no tree (N = 0, I = 0): the brute branch renders the
+    triangle, the BVH branch (which the GLSL starts at bvhNodes[-1]) sees nothing.
+    Whole 800x600 frames, 3 bounces, Fresnel off and on."""
+    W, H = 800, 600
+    fs = rtamd.generate(6, 0, W, H)
+    assert len(fs.nodes) == 0 and len(fs.indices) == 0 and len(fs.shapes) == 1
+    ctx.upload(fs)
+    ctx.set_kernel(kernel)
+    try:
+        for fres in (0, 1):
+            ctx.set_params(W, H, 3, bool(bvh), bool(fres), bool(mt))
+            out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+            ctx.sync()
+            img = out.cpu().numpy()
+            ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, bvh, fres, mt))
+            check(img, ref, f"scene 3 bvh={bvh} mt={mt} fresnel={fres}")
+            bg, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, 1))
+            lit = int((img != bg).any(axis=-1).sum())
+            assert (lit == 0) if bvh else (lit > 1000), lit
+    finally:
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+
+
+# --------------------------------------------------------------------------
+# The bench's steady state, frame by frame (bench.py frames mode)
+
+@pytest.fixture(scope="module")
+def car_full_ref():
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    ref, _ = oracle.render(fs, W, H, oracle.params(W, H, 3))
+    return fs, ref
+
+
+def test_bench_steady_state_frames_vs_oracle(car_full_ref):
+    """What bench.py times: two contexts on their own streams, frames dealt
+    round-robin with nothing waited on between them, the cost-ordered schedule
+    (re-derived every 8th dispatch; the dispatches between run the counter-free
+    instance with the auto lane_k slots), 1920x1080, depth 3. Each of the 24
+    frames goes to its own buffer and every one is checked against one full-frame
+    oracle render (gpu_shader.comp:433-624)."""
+    fs, ref = car_full_ref
+    W, H, F, n = 1920, 1080, 2, 24
+    streams = [torch.cuda.Stream() for _ in range(F)]
+    ctxs = []
+    try:
+        for st in streams:
+            c = rtamd.ComputeShader(0)
+            c.set_stream(st.cuda_stream)
+            c.upload(fs)
+            c.set_params(W, H, 3, True, False, False)
+            c.set_schedule(rtamd.SCHED_COST)
+            ctxs.append(c)
+        outs = [torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda") for _ in range(n)]
+        torch.cuda.synchronize()
+        for i in range(n):
+            c = ctxs[i % F]
+            c.set_camera(fs.camera)
+            c.set_light(fs.light)
+            c.dispatch_rows(W, H, 0, 1, 1, H, outs[i].data_ptr(), W * 16)
+        torch.cuda.synchronize()
+        assert all(c.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL for c in ctxs)
+        for i, o in enumerate(outs):
+            check(o.cpu().numpy(), ref, f"steady-state frame {i} (context {i % F})")
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+# --------------------------------------------------------------------------
+# rt_group frames in flight (rt_group_set_frames): one communicator, F slots
+
+def _orbit_cameras(W, H, n):
+    cams = []
+    for d in range(n):
+        sc = rtamd.Scene().generate(3, 0, W / H)
+        sc.orbit((0.0, 0.0, 0.0), 3.0 * d)
+        cams.append(sc.serializeScene().camera)
+    return cams
+
+
+def _in_flight_check(ctx, g, fs, W, H, stripe):
+    """Frames with a different camera each, dispatched back to back with nothing
+    waited on: for every prefix length n the last frame (read_image) equals the
+    single dispatch of its camera, so no slot's buffers leak into another's."""
+    cams = _orbit_cameras(W, H, 5)
+    refs = []
+    for c in cams:
+        ctx.upload(rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, c, fs.light))
+        ctx.set_params(W, H, 3, True, False, False)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+        out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+        torch.cuda.synchronize()
+        ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+        ctx.sync()
+        refs.append(out.cpu().numpy())
+    assert not np.array_equal(refs[0], refs[1])
+    g.upload(fs)
+    g.set_params(W, H, 3)
+    for n in range(1, 2 * g.frames + 2):
+        for i in range(n):
+            g.set_camera(cams[i % len(cams)])
+            g.dispatch(W, H, stripe)
+        img = g.read_image(W, H)
+        assert np.array_equal(img, refs[(n - 1) % len(cams)]), f"{n} frames in flight"
+
+
+@pytest.mark.parametrize("ranks,frames,share", [(8, 3, 1), (4, 8, 2), (2, 2, 1)])
+def test_group_frames_in_flight_copy(ctx, ranks, frames, share):
+    W, H = 480, 270
+    fs = rtamd.generate(3, 0, W, H)
+    g = rtamd.Group([0] * ranks, rtamd.GATHER_COPY, frames=frames)
+    try:
+        assert g.frames == frames and len(g.contexts) == ranks * frames and len(g.members) == ranks
+        g.set_root_share(share)
+        _in_flight_check(ctx, g, fs, W, H, 8)
+        ph = g.phase_times()
+        assert ph["frames"] > 0 and ph["render_ms"] > 0 and ph["fanin_ms"] > 0 and ph["unstripe_ms"] > 0
+        assert ph["frame_ms"] >= ph["render_ms"]
+        with pytest.raises(rtamd.RTError):
+            g._chk(g._lib.rt_group_set_frames(g._h, 2), "rt_group_set_frames")  # only before the upload
+    finally:
+        g.close()
+
+
+def test_rccl_rank_group_frames_in_flight(ctx):
+    """One RCCL rank (ncclCommInitRank) with 4 frame slots on one communicator;
+    the bounded sync and the asynchronous-error poll report success."""
+    W, H = 640, 360
+    fs = rtamd.generate(3, 0, W, H)
+    g = rtamd.Group(uid=rtamd.group_unique_id(), nranks=1, rank=0, device=0, frames=4)
+    try:
+        assert g.transport == rtamd.GATHER_RCCL and g.frames == 4
+        g.set_timeout(30000)
+        _in_flight_check(ctx, g, fs, W, H, 8)
+        g.check()
+        g.sync()
+        ph = g.phase_times()
+        assert ph["frames"] > 0 and ph["render_ms"] > 0 and ph["unstripe_ms"] > 0
+    finally:
+        g.close()

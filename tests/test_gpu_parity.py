@@ -369,7 +369,7 @@ def test_scene_tree_equals_reference_tree(ctx, scene, walk):
         ctx.set_tree(rtamd.TREE_SCENE)
         b = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
     finally:
-        ctx.set_walk(1)
+        ctx.set_walk(-1)
         ctx.set_tree(rtamd.TREE_SCENE)
     info = ctx.accel_info()
     assert info["scene_tree"] == 1 and info["tree_nested"] == 1 and info["last_kernel"] == rtamd.KERNEL_ACCEL
@@ -388,7 +388,7 @@ def test_scene_tree_stack_overflow_is_exact(ctx, scene, cap):
         W, H = 960, 540
         fs = rtamd.generate(int(scene[1]), 0, W, H)
     p = oracle.params(W, H, 3)
-    ctx.set_walk(1)
+    ctx.set_walk(-1)
     ctx.set_tree(rtamd.TREE_REFERENCE)
     a = gpu_rows(ctx, fs, W, H, p, kernel=rtamd.KERNEL_ACCEL)
     ctx.set_tree(rtamd.TREE_SCENE)
@@ -402,7 +402,7 @@ def test_scene_tree_stack_overflow_is_exact(ctx, scene, cap):
             assert bad == 0, f"walk {walk} cap {cap}: {bad} pixels differ"
     finally:
         ctx.debug_scene_stack(0)
-        ctx.set_walk(1)
+        ctx.set_walk(-1)
 
 
 @pytest.mark.parametrize("walk", [0, 1, 99])
@@ -416,7 +416,7 @@ def test_walk_policies_identical(ctx, walk):
     try:
         img = gpu_rows(ctx, fs, W, H, p, y0=480, rows=16, kernel=rtamd.KERNEL_ACCEL)
     finally:
-        ctx.set_walk(1)
+        ctx.set_walk(-1)
     check(img, ref, f"walk {walk}")
 
 

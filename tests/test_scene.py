@@ -109,3 +109,31 @@ def test_errors_are_status_codes():
         sc.add_mesh(np.zeros((3, 3), np.float32), np.array([0, 1, 5], np.uint32))
     with pytest.raises(rtamd.RTError):
         sc.generate(4)
+
+
+def test_default_scene3_single_triangle_no_tree():
+    """The reference's default scene (`int SCENE = 3`, src/main.cpp:46; generateScene3
+    :1196-1229): one triangle with the Material() defaults, Camera() at (0,-10,40)
+    looking at the origin, the scene-2 light, and no buildBVH call -- zero nodes and
+    zero bvhIndices. The brute branch sees the triangle, the BVH branch nothing."""
+    sc = rtamd.Scene().generate(6, 0, 800 / 600)
+    assert sc.counts() == (1, 0, 0)
+    fs = sc.serializeScene()
+    s = fs.shapes[0]
+    assert int(s["type"]) == 3
+    np.testing.assert_array_equal(s["triP1"], [0, 0, 0])
+    np.testing.assert_array_equal(s["triP2"], [5, 0, 0])
+    np.testing.assert_array_equal(s["triP3"], [2.5, -5, 0])
+    np.testing.assert_array_equal(s["planeNormal"], [0, 0, -1])  # normalize(cross(b-a, c-a))
+    np.testing.assert_array_equal(fs.camera["Position"][0], [0, -10, 40])
+    assert float(fs.camera["fov"][0]) == 60.0 and abs(float(fs.camera["aspectRatio"][0]) - 4 / 3) < 1e-7
+    W, H = 200, 150
+    bg, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, 1))
+    for mt in (0, 1):
+        img, _ = oracle.render(fs, W, H, oracle.params(W, H, 3, 0, 0, mt))
+        hit = (img != bg).any(axis=-1)
+        assert 50 < int(hit.sum()) < W * H // 4, mt
+        # the base vertex (0,0,0) is the look-at point (NDC 0 = row H/2); row 0 is NDC +1
+        # along Up ~ (0,0.97,0.24), so the apex at y = -5 lies in the rows below
+        ys = np.nonzero(hit.any(axis=1))[0]
+        assert ys.min() == H // 2 and ys.max() < H * 3 // 4
