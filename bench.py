@@ -272,13 +272,21 @@ def pmc_entry(key):
 
 
 def roofline(info, kname, k_ms, pixels, b_ref, pmc):
-    """The render kernel against the HBM roofline (see the module docstring)."""
+    """The render kernel against its rooflines (see the module docstring).
+
+    HBM: achieved = DRAM bytes per launch (PMC) / this run's kernel time; frac vs 8 TB/s.
+    Issue: from the SQ passes of the same solo command (tools/sq_summary.py), the
+    VALU and SALU instruction counts against the CU's issue rates give a floor per
+    launch; issue.frac = that floor / this run's kernel time. `bound` names what
+    binds: "hbm" if the HBM fraction is the larger, else "latency" -- neither pipe
+    is saturated, and waves wait on dependent fetches (issue.wait_frac)."""
     compulsory = 16.0 * pixels + float(info.get("record_bytes", 0))
     k_s = k_ms * 1e-3
-    measured = pmc["bytes"] if pmc else None
+    measured = pmc.get("bytes") if pmc else None
     achieved = (measured if measured else compulsory) / k_s / 1e9
+    frac = achieved / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": achieved / HBM_PEAK_GBS,
+           "frac": frac,
            "basis": ("measured DRAM bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
                      f"{pmc['source']}) / this run's mean kernel time") if measured else
                     "compulsory bytes per launch (16 B/pixel image store + the kernel's device records once) "
@@ -286,11 +294,24 @@ def roofline(info, kname, k_ms, pixels, b_ref, pmc):
            "traffic": measured,
            "algorithmic_bytes_per_launch": compulsory,
            "algorithmic_GBps": compulsory / k_s / 1e9,
+           "traffic_over_algorithmic": (measured / compulsory) if measured else None,
            "reference_equivalent_bytes_per_launch": b_ref,
            "reference_equivalent_GBps": b_ref / k_s / 1e9,
            "kernel": kname, "kernel_ms": k_ms}
-    if pmc and "issue" in pmc:
-        out["issue"] = pmc["issue"]
+    iss = pmc.get("issue") if pmc else None
+    if iss:
+        out["issue"] = dict(iss)
+        if iss.get("valu_floor_ms") is not None:
+            floor = max(iss["valu_floor_ms"], iss["salu_floor_ms"])
+            out["issue"]["floor_ms"] = floor
+            out["issue"]["frac"] = floor / k_ms
+            out["issue"]["binding_pipe"] = "valu" if iss["valu_floor_ms"] >= iss["salu_floor_ms"] else "salu"
+            if out["issue"]["frac"] > frac:
+                out["bound"] = "latency"
+                out["bound_detail"] = (
+                    f"dependent-fetch latency: the busiest issue pipe ({out['issue']['binding_pipe']}) needs "
+                    f"{floor:.3f} of the kernel's {k_ms:.3f} ms at full rate (frac {out['issue']['frac']:.2f}), "
+                    f"HBM {frac:.3f}; waves wait {iss['wait_frac']:.0%} of their cycles")
     return out
 
 
@@ -589,8 +610,9 @@ def main():
         if strong:
             gather = ("rt_group: ncclSend/ncclRecv to rank 0 (RCCL over xGMI) + k_unstripe, C ABI (include/rt_group.h)"
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
-        toggles = (a.brute, a.mt, a.fresnel, a.variant, a.animate)
-        pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}") if not any(toggles) and not strong else None
+        suffix = "".join(f"_{n}" for n, on in (("brute", a.brute), ("mt", a.mt), ("fresnel", a.fresnel),
+                                                  ("variant", a.variant), ("animate", a.animate)) if on)
+        pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}{suffix}") if not strong else None
         out = {
             "metric": METRIC,
             "value": rays_step * a.steps / elapsed / 1e6,

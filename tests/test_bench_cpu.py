@@ -114,3 +114,16 @@ def test_parity_check_of_timed_frames():
     g2 = good.copy()
     g2[3, 0, 0] = np.nan
     assert bench.parity_check([g2], 3, ref2, "t")["ok"]
+
+
+def test_roofline_names_the_binding_resource():
+    """With the SQ passes' issue floors the line says what binds: latency when the
+    busiest issue pipe's floor is a larger fraction of the kernel time than HBM."""
+    info = {"record_bytes": 1_000_000}
+    iss = {"valu_floor_ms": 0.09, "salu_floor_ms": 0.11, "wait_frac": 0.3, "valu_busy": 0.5}
+    r = bench.roofline(info, "k_accel", 0.3, 1920 * 1080, 8.5e11, {"bytes": 45e6, "source": "x", "issue": iss})
+    assert r["bound"] == "latency" and r["issue"]["binding_pipe"] == "salu"
+    assert r["issue"]["frac"] == pytest.approx(0.11 / 0.3) and r["frac"] < r["issue"]["frac"]
+    # an HBM-heavy kernel keeps "hbm"
+    r2 = bench.roofline(info, "k", 0.3, 1920 * 1080, 0.0, {"bytes": 2e9, "source": "x", "issue": iss})
+    assert r2["bound"] == "hbm"

@@ -13,3 +13,4 @@ for w in -1 1 3; do
   timeout -k 10 200 python bench.py --config 5 --brute --mt --no-cpu --steps 20 --warmup 3 --walk $w > gpurun_out/bench_r03a_c5_brute_mt_walk$w.json 2>> gpurun_out/bench_r03a.err || exit $?
 done
 grep -ho '"ms_per_step": [0-9.]*\|"walk": [-0-9]*' gpurun_out/bench_r03a_c5_brute_mt_walk*.json
+bash tools/gpu_prof.sh r03a_c3 || exit $?
