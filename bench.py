@@ -207,12 +207,13 @@ def parity_check(frames, ref_y0, ref, what):
             "rows_checked": [int(ref_y0), int(ref_y0 + len(ref))], "against": what, "ok": bad == 0}
 
 
-def cpu_reference_1core(rtamd, seconds):
+def cpu_reference_1core(rtamd, seconds, cfg=3, variant=0, W=1920, H=1080):
     """BASELINE.md "CPU-ref": the reference's own CPU path, cpuRayTracer
     (src/main.cpp:848-894: brute force over every shape, primary rays only, CPU
     phong) restated in oracle/rt_oracle.c, on ONE core as the reference runs it.
-    Config 1 (800x600, 4 spheres + 1 plane) whole frames, and the car scene's
-    1920x1080 primary rays on a band of rows (the whole frame would take minutes)."""
+    Config 1 (800x600, 4 spheres + 1 plane) whole frames, and the run's own scene
+    (generator config `cfg`) at W x H, primary rays only, on a band of rows through
+    the middle (a whole frame would take minutes)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (cpu_baseline leg only)
     fs1 = rtamd.generate(1, 0, 800, 600)
@@ -222,21 +223,21 @@ def cpu_reference_1core(rtamd, seconds):
         oracle.cpu_raytracer(fs1, 800, 600, threads=1)
         n1 += 1
     ms1 = (time.perf_counter() - t0) / n1 * 1e3
-    fs3 = rtamd.generate(3, 0, 1920, 1080)
-    rows, y0 = 2, 539
+    fs3 = rtamd.generate(cfg, variant, W, H)
+    rows, y0 = 2, H // 2 - 1
     while True:
         t0 = time.perf_counter()
-        oracle.cpu_raytracer(fs3, 1920, 1080, y0=y0, y1=y0 + rows, threads=1)
+        oracle.cpu_raytracer(fs3, W, H, y0=y0, y1=y0 + rows, threads=1)
         dt = time.perf_counter() - t0
         if dt >= seconds * 0.5 or rows >= 64:
             break
         rows = min(64, max(rows * 2, int(rows * seconds / max(dt, 1e-3) * 0.9)))
     return {"kind": "port", "path": "cpuRayTracer (src/main.cpp:848-894)", "cores": 1, "cpu": cpu_model(),
             "config1_ms_per_frame": ms1, "config1_mrays_primary_per_s": 800 * 600 / ms1 / 1e3,
-            "config3_primary_only_mrays_per_s": rows * 1920 / dt / 1e6,
-            "config3_primary_only_ms_per_frame_equiv": dt * 1e3 * 1080 / rows,
+            "this_config_primary_only_mrays_per_s": rows * W / dt / 1e6,
+            "this_config_primary_only_ms_per_frame_equiv": dt * 1e3 * H / rows,
             "sample": f"cpuRayTracer restated (oracle/rt_oracle.c orc_cpu_raytracer), 1 thread: config 1 {n1} "
-                      f"whole 800x600 frames; config 3 rows [{y0},{y0 + rows}) of 1920x1080 in {dt:.2f} s"}
+                      f"whole 800x600 frames; this run's scene rows [{y0},{y0 + rows}) of {W}x{H} in {dt:.2f} s"}
 
 
 def wheel_frames(fs, n):
@@ -550,7 +551,8 @@ def main():
         share_probe = {}
         steps = a.steps
         a.steps = max(4, 2 * F)
-        for k in ((1, 2) if world > 1 else (1,)):
+        # rank 0's rows never cross a link: with more peers a larger share moves fewer bytes
+        for k in ((1,) if world == 1 else (1, 2) if world < 4 else (1, 2, 3, 4)):
             grp.set_root_share(k)
             share_probe[k] = timed(F) / a.steps * 1e3
         a.steps = steps
@@ -663,7 +665,8 @@ def main():
         if world == 1 and not a.no_cpu:
             out["cpu_baseline"] = cpu_baseline(rtamd, fs, W, H, mb, a.cpu_seconds, thr,
                                                (not a.brute, a.fresnel, a.mt))
-            out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2)
+            out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2, cfg, a.variant,
+                                                                            W, H)
         if mode == "frames" and anim is None:
             # the timed frames themselves, against the oracle (outside the timed region)
             if out["cpu_baseline"] is not None:

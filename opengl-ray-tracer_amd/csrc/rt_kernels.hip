@@ -856,7 +856,10 @@ __device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f
         // kNoPrune children (accel.h): no distance limit, entered at parameter 0
         const bool np = th[k] < -6.0f;
         tn[k] = fmaxf(fmaxf(fminf(x0[k], x1[k]), fminf(y0[k], y1[k])), fmaxf(fminf(z0[k], z1[k]), 0.0f));
-        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), fminf(fmaxf(z0[k], z1[k]), np ? INFINITY : tl));
+        // min(tz, np ? inf : tl) as a select of two mins: a min fed by a select gets an
+        // extra canonicalising max on gfx950 (IEEE mode), one per child on the walk's path
+        const float tz = fmaxf(z0[k], z1[k]);
+        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), np ? fminf(tz, INFINITY) : fminf(tz, tl));
         te[k] = np ? 0.0f : tn[k];
     }
     if (MT) {
@@ -926,6 +929,10 @@ __device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_flo
 #define RT_LEAF_PREFETCH 0  // lane_walk's leaf loop software-pipelined (experiment builds)
 #endif
 
+#ifndef RT_FLAT_LOOP
+#define RT_FLAT_LOOP 1  // lane_walk's SPEC descent as a one-exit loop (r03: config 5 -3 %)
+#endif
+
 // Per-lane walk ("while-while"): each lane walks its own stack in LDS (code +
 // entry parameter per entry). A lane descends until it holds a leaf, keeping
 // the nearer child in registers and stacking the farther one; the wave then
@@ -943,7 +950,11 @@ __device__ __forceinline__ float bf16_f(unsigned short b) { return __uint_as_flo
 // round of leaf tests (and a shadow hit ends the group's walks); the result is
 // the (distance, rank) minimum over the group, which does not depend on which
 // lane tested which leaf.
-template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool SPEC = true, bool MT = false>
+// FLAT_SHADOW: a shadow hit sets the lane's flags and ends its leaf loop through the loop
+// test, instead of returning from inside the loop (r03: car -1.7 % in flight and serially;
+// config 5 +0.5 %, so the big-scene instances, which split walks, keep the return).
+template <bool SHADOW, bool COUNT = false, bool WSTAT = false, bool SPEC = true, bool MT = false,
+          bool FLAT_SHADOW = false>
 __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float lim_shadow, Best& b, bool& shadow,
                           int* stk, unsigned short* stt, int stride, int cap, WalkCount& wc, int sg = 1,
                           int si = 0) {
@@ -952,17 +963,20 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
     const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
     const rta::RayC c = ray_c(r, A.origin_lim);
     float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
+    // sp: the stack top as an element offset (entries x stride), so a push or pop
+    // adds or subtracts stride instead of multiplying (v_mul_lo_u32 is quarter rate)
     int sp = 0, cur = A.troot;
+    const int capo = cap * stride;
     bool have = true;
     // The scene tree has no static stack bound: a lane whose push would not fit
     // drops it and marks `ovf`; when its walk ends it walks the reference tree
     // from the root (with the best hit so far), whose bound the builder checked.
     bool ovf = false;
-    int pcap = min(cap, A.scene_stack);  // push bound of the tree being walked
+    int pcap = min(cap, A.scene_stack) * stride;  // push bound of the tree being walked (offset)
     unsigned fm = 0;
     if (!use_scene(A, fast, c)) {
         have = enter_root(A, r, inv, c, tl, cur);
-        pcap = cap;
+        pcap = capo;
     } else if (A.nfew > 0) {
         fm = few_mask(A, r, inv);
     }
@@ -993,9 +1007,9 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 } else if (h >= ss) {  // positions si and si + ss (ss >= 2, h <= 4) are this lane's
                     if (si + ss < h) {
                         if (sp < pcap) {
-                            stk[sp * stride] = pick_code(w, si + ss);
-                            stt[sp * stride] = f_bf16_down(pick_t(w, si + ss));
-                            ++sp;
+                            stk[sp] = pick_code(w, si + ss);
+                            stt[sp] = f_bf16_down(pick_t(w, si + ss));
+                            sp += stride;
                         } else {
                             ovf = true;
                         }
@@ -1031,6 +1045,35 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
         // for one; a lane that meets a second leaf parks on it (kept for the next
         // round), and the round ends when every walking lane holds a leaf
         // (measured: config 3 -4 %, config 5 -14 %).
+#if RT_FLAT_LOOP
+        // SPEC in one-exit form: a lane that finishes, parks or ends its walk sets `stop`
+        // instead of leaving the loop, and the round ends on the wave-uniform test alone
+        // (the same steps in the same order per lane; fewer lane-mask merges per step).
+        bool stop = ended;
+        if (SPEC && !ended) {
+            for (;;) {
+                if (__ballot(!stop && count == 0) == 0) break;
+                if (!stop && !have) {
+                    if (sp == 0) {
+                        if (ovf) {  // a scene-tree push was dropped: the reference tree, from its root
+                            ovf = false;
+                            pcap = capo;
+                            have = enter_root(A, r, inv, c, tl, cur);
+                        }
+                        if (!have) {
+                            ended = count == 0;  // walk finished (a held leaf is still tested)
+                            stop = true;
+                        }
+                    } else {
+                        sp -= stride;
+                        have = !(bf16_f(stt[sp]) > tl);  // dropped if a nearer hit was found since the push
+                        cur = stk[sp];
+                    }
+                }
+                const unsigned uc = static_cast<unsigned>(cur);
+                stop = stop || (have && count > 0 && (uc & (kTopLeaf | kLeaf)));  // park on a leaf
+                if (stop || !have) continue;
+#else
         if (!ended) {
             for (;;) {
                 if (SPEC ? __ballot(!ended && count == 0) == 0 : count > 0) break;
@@ -1038,7 +1081,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     if (sp == 0) {
                         if (ovf) {  // a scene-tree push was dropped: the reference tree, from its root
                             ovf = false;
-                            pcap = cap;
+                            pcap = capo;
                             if (enter_root(A, r, inv, c, tl, cur)) {
                                 have = true;
                                 continue;
@@ -1047,13 +1090,14 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                         if (count == 0) ended = true;  // walk finished (a held leaf is still tested)
                         break;
                     }
-                    --sp;
-                    if (bf16_f(stt[sp * stride]) > tl) continue;  // a nearer hit was found since the push
-                    cur = stk[sp * stride];
+                    sp -= stride;
+                    if (bf16_f(stt[sp]) > tl) continue;  // a nearer hit was found since the push
+                    cur = stk[sp];
                     have = true;
                 }
                 const unsigned uc = static_cast<unsigned>(cur);
                 if (count > 0 && (uc & (kTopLeaf | kLeaf))) break;  // park on a leaf
+#endif
                 if (COUNT) wc.nodes++;
                 if (WSTAT && first_active()) wc.wnodes++;
                 have = false;
@@ -1082,9 +1126,9 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     for (int s2 = 3; s2 >= 1; --s2) {
                         if (w.t[s2] < INFINITY) {
                             if (sp < pcap) {
-                                stk[sp * stride] = w.code[s2];
-                                stt[sp * stride] = f_bf16_down(w.t[s2]);
-                                ++sp;
+                                stk[sp] = w.code[s2];
+                                stt[sp] = f_bf16_down(w.t[s2]);
+                                sp += stride;
                             } else {
                                 ovf = true;  // scene tree only: local trees fit their bound
                             }
@@ -1098,10 +1142,10 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     const Kids k = ref_kids(A, uc, r, inv, c, tl, true, fast);
                     if (k.ha && k.hb) {
                         const bool a_first = !(k.tb < k.ta);  // nearer entry first
-                        if (sp < cap) {
-                            stk[sp * stride] = a_first ? k.cb : k.ca;
-                            stt[sp * stride] = f_bf16_down(a_first ? k.tb : k.ta);
-                            ++sp;
+                        if (sp < capo) {
+                            stk[sp] = a_first ? k.cb : k.ca;
+                            stt[sp] = f_bf16_down(a_first ? k.tb : k.ta);
+                            sp += stride;
                         }
                         cur = a_first ? k.ca : k.cb;
                         have = true;
@@ -1127,7 +1171,15 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
 #endif
             if (COUNT) wc.tests++;
             if (WSTAT && first_active()) wc.wtests++;
-            if (SHADOW) {
+            if (SHADOW && FLAT_SHADOW) {
+                // an occluder ends this lane's walk at the next round's test (no exit
+                // from inside the loop)
+                if (try_shadow<MT>(g, r, lim_shadow)) {
+                    shadow = true;
+                    ended = true;
+                    count = i + 1;
+                }
+            } else if (SHADOW) {
                 if (try_shadow<MT>(g, r, lim_shadow)) {
                     shadow = true;
                     if (sg == 1) return;
@@ -1175,7 +1227,7 @@ __device__ __forceinline__ void lane_walk_any(const AccelPtrs& A, Ray& r, bool a
                                               bool& shadow, int* stk, unsigned short* stt, int stride, int cap,
                                               WalkCount& wc) {
     if (!SPLIT) {  // the plain walk, without the split's registers
-        lane_walk<SHADOW, COUNT, WSTAT, SPEC, MT>(A, r, active, lim_shadow, b, shadow, stk, stt, stride, cap, wc);
+        lane_walk<SHADOW, COUNT, WSTAT, SPEC, MT, true>(A, r, active, lim_shadow, b, shadow, stk, stt, stride, cap, wc);
         return;
     }
     const unsigned long long m = __ballot(active);
