@@ -335,6 +335,31 @@ def test_mt_accelerated_equals_literal(ctx, cfg, W, H, mb, bvh, fresnel):
         assert np.array_equal(fast, lit)
 
 
+@pytest.mark.parametrize("k,parts", [(16, 8), (64, 4), (8, 2)])
+def test_mt_heavy_tiles_split_equals_literal(ctx, k, parts):
+    """MT frames over the car's shallow tree walk every bounce as packets, so the
+    heavy-tile split (the heaviest k tiles of the cost order as `parts` waves, here
+    forced with rt_debug_heavy) applies to them: frames after the first (cost order
+    in place, tiles split) equal the literal k_packet MT frame bit for bit."""
+    W, H = 800, 600
+    fs = rtamd.generate(3, 0, W, H)
+    lit = render_mt(ctx, fs, W, H, 3, True, rtamd.KERNEL_PACKET)
+    ctx.debug_heavy(k, parts)
+    try:
+        ctx.upload(fs)
+        ctx.set_params(W, H, 3, True, False, True)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+        for i in range(3):
+            out = torch.full((H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+            ctx.sync()
+            assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL
+            assert np.array_equal(out.cpu().numpy(), lit), f"frame {i}"
+    finally:
+        ctx.debug_heavy(-1, 4)
+
+
 def test_mt_vs_oracle_band(ctx):
     W, H = 1920, 1080
     fs = rtamd.generate(3, 0, W, H)

@@ -27,6 +27,7 @@ ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--frames", type=int, default=200)
 ap.add_argument("--walk2", type=int, default=-1, help="walk policy (rt_set_walk) for the lib2 runs")
 ap.add_argument("--set2", default="", help="lib2 settings, e.g. schedule=0,launch=2,walk=0")
+ap.add_argument("--set", default="", help="settings for both builds, e.g. latency=1")
 ap.add_argument("--nocheck", action="store_true", help="timing only: images may differ (experiments)")
 ap.add_argument("--bounces", type=int, default=0, help="override maxBounces")
 ap.add_argument("--mt", action="store_true", help="useMollerTrumbore = 1 frames")
@@ -40,7 +41,7 @@ if a.child is None:
     for _ in range(a.rounds):
         for name in ("current", "lib2"):
             out = subprocess.run([sys.executable, __file__, "--lib2", a.lib2, "--config", str(a.config),
-                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--bounces", str(a.bounces)] + (["--mt"] if a.mt else []) + ["--walk2", str(a.walk2), "--set2", a.set2, "--child", name],
+                                  "--inflight", str(a.inflight), "--frames", str(a.frames), "--bounces", str(a.bounces)] + (["--mt"] if a.mt else []) + ["--walk2", str(a.walk2), "--set2", a.set2, "--set", a.set, "--child", name],
                                  capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
             r = json.loads(out)
             res[name].append(r["ms"])
@@ -67,13 +68,15 @@ for _ in range(F):
     c.set_params(W, H, mb, True, False, a.mt)
     if a.child == "lib2" and a.walk2 >= 0:
         c.set_walk(a.walk2)
-    if a.child == "lib2" and a.set2:
-        for kv in a.set2.split(","):
+    sets = ([a.set] if a.set else []) + ([a.set2] if a.child == "lib2" and a.set2 else [])
+    for kv in ",".join(sets).split(",") if sets else []:
+        if True:
             k, v = kv.split("=")
             {"schedule": lambda x: c.set_schedule(x), "launch": lambda x: c.set_launch(x, False),
              "persistent": lambda x: c.set_launch(1, bool(x)), "period": lambda x: c.debug_sched_period(x), "tail": lambda x: c.set_tail(x), "tlanes": lambda x: c.debug_tail_lanes(x), "shwalk": lambda x: c.debug_shadow_walk(x),
              "spec": lambda x: c.debug_spec(x), "stack": lambda x: c.debug_lane_stack(x),
-             "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x)}[k](int(v))
+             "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x),
+             "latency": lambda x: c.set_latency_mode(x)}[k](int(v))
     ctxs.append((c, s))
     bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
 
