@@ -565,9 +565,12 @@ def main():
     serial = timed(1) if F > 1 else None
     serial_kt = ctx.kernel_times() if F > 1 else None
     # SURVEY §8(d)'s frame: upload + dispatch + completion, one at a time, FPS = 1 / median.
-    # Each frame waits for its completion (the reference's loop, src/main.cpp:290-462).
+    # Each frame waits for its completion (the reference's loop, src/main.cpp:290-462), with
+    # rt_set_latency_mode on: the setting for a host that waits for every frame.
     serial_frames = []
     if not use_group or world == 1:
+        if not use_group:
+            ctx.set_latency_mode(1)
         for i in range(a.warmup):
             frame(i, 1)
         torch.cuda.synchronize()
@@ -576,6 +579,8 @@ def main():
             frame(i, 1)
             torch.cuda.synchronize()
             serial_frames.append(time.perf_counter() - t0)
+        if not use_group:
+            ctx.set_latency_mode(0)
         ctx.kernel_times()
     # the same one-at-a-time frames with rt_set_latency_mode (what a host that waits for
     # each frame would set); reported beside serial_ms_per_step, not used for the roofline
@@ -628,6 +633,9 @@ def main():
             "serial_ms_per_step": (serial if serial is not None else elapsed) / a.steps * 1e3,
             "serial_ms_per_step_latency_mode": (serial_lat / a.steps * 1e3) if serial_lat is not None else None,
             "serial_frame_ms_median": float(np.median(serial_frames)) * 1e3 if serial_frames else None,
+            "serial_frame_median_mode": ("each frame waited for (host sync), rt_set_latency_mode on"
+                                         if serial_frames and not use_group else
+                                         "each frame waited for (host sync)" if serial_frames else None),
             "fps_serial_median": 1.0 / float(np.median(serial_frames)) if serial_frames else None,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",

@@ -1101,7 +1101,35 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 if (COUNT) wc.nodes++;
                 if (WSTAT && first_active()) wc.wnodes++;
                 have = false;
-                if ((uc & (kTopLeaf | kItem)) == (kTopLeaf | kItem)) {
+                // kLocal codes (wide nodes and local leaves, including few-leaf items) first,
+                // as one region: a round in which no lane holds a reference-tree code skips
+                // the rest with one exec test instead of three
+                if (uc & kLocal) {
+                    if (uc & kLeaf) {
+                        start = static_cast<int>((uc >> 6) & 0x3fffffu);
+                        count = static_cast<int>(uc & 0x3fu);
+                        if (uc & kItem) count = ((fm >> (count >> 3)) & 1u) ? (count & 7) : 0;  // few-leaf item
+                    } else {
+                        Kids4 w = wide_kids<MT>(A, uc, c, tl, true);
+                        sort4(w);
+#pragma unroll
+                        for (int s2 = 3; s2 >= 1; --s2) {
+                            if (w.t[s2] < INFINITY) {
+                                if (sp < pcap) {
+                                    stk[sp] = w.code[s2];
+                                    stt[sp] = f_bf16_down(w.t[s2]);
+                                    sp += stride;
+                                } else {
+                                    ovf = true;  // scene tree only: local trees fit their bound
+                                }
+                            }
+                        }
+                        if (w.t[0] < INFINITY) {
+                            cur = w.code[0];
+                            have = true;
+                        }
+                    }
+                } else if ((uc & (kTopLeaf | kItem)) == (kTopLeaf | kItem)) {
                     int s0, n0;
                     if (enter_item(A, uc, r, inv, s0, n0)) {
                         start = s0;
@@ -1113,29 +1141,6 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     count = lf.y;
                     if (lf.z != kNoChild) {
                         cur = lf.z;  // local root: entered with the leaf
-                        have = true;
-                    }
-                } else if (uc & kLeaf) {
-                    start = static_cast<int>((uc >> 6) & 0x3fffffu);
-                    count = static_cast<int>(uc & 0x3fu);
-                    if (uc & kItem) count = ((fm >> (count >> 3)) & 1u) ? (count & 7) : 0;  // few-leaf item
-                } else if (uc & kLocal) {
-                    Kids4 w = wide_kids<MT>(A, uc, c, tl, true);
-                    sort4(w);
-#pragma unroll
-                    for (int s2 = 3; s2 >= 1; --s2) {
-                        if (w.t[s2] < INFINITY) {
-                            if (sp < pcap) {
-                                stk[sp] = w.code[s2];
-                                stt[sp] = f_bf16_down(w.t[s2]);
-                                sp += stride;
-                            } else {
-                                ovf = true;  // scene tree only: local trees fit their bound
-                            }
-                        }
-                    }
-                    if (w.t[0] < INFINITY) {
-                        cur = w.code[0];
                         have = true;
                     }
                 } else {
