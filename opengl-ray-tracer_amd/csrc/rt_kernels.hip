@@ -1050,7 +1050,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
         // instead of leaving the loop, and the round ends on the wave-uniform test alone
         // (the same steps in the same order per lane; fewer lane-mask merges per step).
         bool stop = ended;
-        if (SPEC && !ended) {
+        if (SPEC) {  // ended lanes are stopped: no exec test around the loop (config 5: -2 %)
             for (;;) {
                 if (__ballot(!stop && count == 0) == 0) break;
                 if (!stop && !have) {
