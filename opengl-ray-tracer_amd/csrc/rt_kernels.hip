@@ -1038,6 +1038,9 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
             }
         }
     }
+    // From here `cur == kNoChild` means the lane holds no node (no separate flag: one
+    // lane mask fewer to merge at every join of the descent)
+    if (!have) cur = kNoChild;
     bool ended = false;
     for (;;) {
         // While-while: a lane descends until it holds a leaf. SPEC (speculative):
@@ -1053,39 +1056,37 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
         if (SPEC) {  // ended lanes are stopped: no exec test around the loop (config 5: -2 %)
             for (;;) {
                 if (__ballot(!stop && count == 0) == 0) break;
-                if (!stop && !have) {
+                if (!stop && cur == kNoChild) {
                     if (sp == 0) {
                         if (ovf) {  // a scene-tree push was dropped: the reference tree, from its root
                             ovf = false;
                             pcap = capo;
-                            have = enter_root(A, r, inv, c, tl, cur);
+                            if (!enter_root(A, r, inv, c, tl, cur)) cur = kNoChild;
                         }
-                        if (!have) {
+                        if (cur == kNoChild) {
                             ended = count == 0;  // walk finished (a held leaf is still tested)
                             stop = true;
                         }
                     } else {
                         sp -= stride;
-                        have = !(bf16_f(stt[sp]) > tl);  // dropped if a nearer hit was found since the push
-                        cur = stk[sp];
+                        const int pc = stk[sp];
+                        cur = bf16_f(stt[sp]) > tl ? kNoChild : pc;  // dropped if a nearer hit was found since the push
                     }
                 }
                 const unsigned uc = static_cast<unsigned>(cur);
-                stop = stop || (have && count > 0 && (uc & (kTopLeaf | kLeaf)));  // park on a leaf
-                if (stop || !have) continue;
+                stop = stop || (cur != kNoChild && count > 0 && (uc & (kTopLeaf | kLeaf)));  // park on a leaf
+                if (stop || cur == kNoChild) continue;
 #else
         if (!ended) {
             for (;;) {
                 if (SPEC ? __ballot(!ended && count == 0) == 0 : count > 0) break;
-                if (!have) {
+                if (cur == kNoChild) {
                     if (sp == 0) {
                         if (ovf) {  // a scene-tree push was dropped: the reference tree, from its root
                             ovf = false;
                             pcap = capo;
-                            if (enter_root(A, r, inv, c, tl, cur)) {
-                                have = true;
-                                continue;
-                            }
+                            if (enter_root(A, r, inv, c, tl, cur)) continue;
+                            cur = kNoChild;
                         }
                         if (count == 0) ended = true;  // walk finished (a held leaf is still tested)
                         break;
@@ -1093,14 +1094,13 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     sp -= stride;
                     if (bf16_f(stt[sp]) > tl) continue;  // a nearer hit was found since the push
                     cur = stk[sp];
-                    have = true;
                 }
                 const unsigned uc = static_cast<unsigned>(cur);
                 if (count > 0 && (uc & (kTopLeaf | kLeaf))) break;  // park on a leaf
 #endif
                 if (COUNT) wc.nodes++;
                 if (WSTAT && first_active()) wc.wnodes++;
-                have = false;
+                cur = kNoChild;  // the branches below set the next node, if any
                 // kLocal codes (wide nodes and local leaves, including few-leaf items) first,
                 // as one region: a round in which no lane holds a reference-tree code skips
                 // the rest with one exec test instead of three
@@ -1124,10 +1124,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                                 }
                             }
                         }
-                        if (w.t[0] < INFINITY) {
-                            cur = w.code[0];
-                            have = true;
-                        }
+                        if (w.t[0] < INFINITY) cur = w.code[0];
                     }
                 } else if ((uc & (kTopLeaf | kItem)) == (kTopLeaf | kItem)) {
                     int s0, n0;
@@ -1139,10 +1136,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                     const int4 lf = A.tleaf[uc & 0x0fffffffu];
                     start = lf.x;
                     count = lf.y;
-                    if (lf.z != kNoChild) {
-                        cur = lf.z;  // local root: entered with the leaf
-                        have = true;
-                    }
+                    cur = lf.z;  // the local root (kNoChild: none) is entered with the leaf
                 } else {
                     const Kids k = ref_kids(A, uc, r, inv, c, tl, true, fast);
                     if (k.ha && k.hb) {
@@ -1153,10 +1147,8 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                             sp += stride;
                         }
                         cur = a_first ? k.ca : k.cb;
-                        have = true;
                     } else if (k.ha || k.hb) {
                         cur = k.ha ? k.ca : k.cb;
-                        have = true;
                     }
                 }
             }

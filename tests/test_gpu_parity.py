@@ -437,11 +437,17 @@ def test_cost_schedule_identical_images(ctx, sched):
     full = torch.empty((180, 320, 4), dtype=torch.float32, device="cuda")
     # dispatch 1 records tile work, 2-8 reuse its order with the counter-free kernel,
     # 9 records again (the order is re-derived every 8th dispatch)
-    for _ in range(10):
+    for i in range(10):
         full.fill_(float("nan"))
+        torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
         ctx.dispatch_rows(320, 180, 0, 1, 1, 180, full.data_ptr(), 320 * 16)
         ctx.sync()
-        assert np.array_equal(full.cpu().numpy(), ref)
+        img = full.cpu().numpy()
+        if not np.array_equal(img, ref):
+            nan = int(np.isnan(img).any(-1).sum())
+            bad = np.argwhere((img != ref).any(-1))
+            pytest.fail(f"frame {i}: {len(bad)} pixels differ ({nan} unwritten), first {bad[:4].tolist()}, "
+                        f"got {img[tuple(bad[0])].tolist()} want {ref[tuple(bad[0])].tolist()}")
     band = ctx.render(320, 180)[40:120]
     out = torch.zeros((80, 320, 4), dtype=torch.float32, device="cuda")
     for _ in range(2):  # alternate tile counts: the order sets must stay consistent
@@ -469,6 +475,7 @@ def test_latency_mode_exact(ctx, cfg, W, H, mb):
         full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
         for _ in range(10):
             full.fill_(float("nan"))
+            torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
             ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
             ctx.sync()
             img = full.cpu().numpy()
@@ -500,6 +507,7 @@ def test_heaviest_slots_walk_per_lane_exact(ctx, cfg, W, H, mb):
             ctx.debug_lane_k(k, mode)
             for _ in range(10):
                 full.fill_(float("nan"))
+                torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
                 ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
                 ctx.sync()
                 img = full.cpu().numpy()
@@ -530,6 +538,7 @@ def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
             ctx.debug_heavy(k, parts)
             for _ in range(10):
                 full.fill_(float("nan"))
+                torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
                 ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
                 ctx.sync()
                 img = full.cpu().numpy()
@@ -540,6 +549,7 @@ def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
         ctx.debug_heavy(32, 8)
         for _ in range(10):
             part.fill_(float("nan"))
+            torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
             ctx.dispatch_rows(W, H, 8, 8, 3, rows, part.data_ptr(), W * 16)
             ctx.sync()
             assert np.array_equal(part.cpu().numpy(), want)

@@ -10,7 +10,7 @@ for n in $NAMES; do
     for f in 2 1; do
       fr=200; [ $c = 5 ] && fr=30
       echo -n "$n config $c inflight $f: "
-      timeout -k 10 300 python tools/abf.py --lib2 build_ab/$n/librtamd.so --config $c --inflight $f --frames $fr --rounds 3 2>&1 | grep -v amdgpu.ids | tail -1 || exit 1
+      timeout -k 10 150 python tools/abf.py --lib2 build_ab/$n/librtamd.so --config $c --inflight $f --frames $fr --rounds 3 2>&1 | grep -v amdgpu.ids | tail -1 || exit 1
     done
   done
 done
