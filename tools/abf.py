@@ -55,7 +55,7 @@ if a.child is None:
     sys.exit(0)
 
 cfg, W, H, mb = WL[a.config]
-mb = a.bounces or mb
+mb = 0 if a.bounces < 0 else (a.bounces or mb)
 fs = rtamd.generate(cfg, 0, W, H)
 F = a.inflight
 path = None if a.child == "current" else a.lib2
