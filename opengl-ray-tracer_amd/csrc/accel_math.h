@@ -39,7 +39,58 @@ struct RayC {
     float ox, oy, oz;  // o * inv
     float dx, dy, dz;  // d / |d|
     float rdl;         // 1 / |d|
+    int dq;            // rint(127 d/|d|) as 3 signed bytes, byte 3 = -128 (cone_culls_q)
 };
+
+// Quantized back-face cones (the barycentric accelerator's wide nodes,
+// rt_kernels.hip wide_kids): one 32-bit word per child, bytes 0-2 the axis as
+// a_q = rint(127 a) (signed), byte 3 a threshold t8. With the ray's
+// d_q = rint(127 d/|d|), the integer dot(a_q, d_q) equals 127^2 a.d up to
+//   127 (|a| |d_q - 127 d/|d|| + |a_q - 127 a|) + |a_q - 127 a| |d_q - 127 d/|d||
+//   <= 127 (1.0000001 * 0.5001 * sqrt(3) + 0.5 * sqrt(3)) + 0.751 < 221
+// (0.5001 covers the float d/|d| and the product 127 d). The word culls when
+// dot(a_q, d_q) < 128 t8, i.e. when one dot4 with d_q's byte 3 = -128 is
+// negative; t8 = floor((127^2 thr - 222) / 128) makes that imply a.d < thr,
+// the float cone's own condition (cone_culls without its rounding allowance).
+// |dot(a_q, d_q)| <= 127.87^2 < 16384, so t8 = -128 never culls.
+constexpr int kConeNp = static_cast<int>(0x80000000u);     // kNoPrune child: a_q = 0, t8 = -128
+constexpr int kConeNever = static_cast<int>(0x81000000u);  // never culls: a_q = 0, t8 = -127
+
+RTA_HD int sdot4(int a, int b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_sdot4(a, b, 0, false);
+#else
+    int s = 0;
+    for (int i = 0; i < 4; ++i)
+        s += static_cast<int>(static_cast<signed char>((a >> (8 * i)) & 0xff)) *
+             static_cast<int>(static_cast<signed char>((b >> (8 * i)) & 0xff));
+    return s;
+#endif
+}
+
+RTA_HD bool cone_culls_q(int w, int dq) { return sdot4(w, dq) < 0; }
+
+// The ray's d_q (RayC::dq). A NaN component gives 0 there: such a ray has no
+// INNER hit (every shape test compares against N.d), so what it culls is moot.
+RTA_HD int ray_dq(float dx, float dy, float dz) {
+    auto b = [](float v) {
+        const float r = std::rint(127.0f * v);
+        return (r >= -127.0f && r <= 127.0f) ? static_cast<int>(r) & 0xff : 0;
+    };
+    return b(dx) | (b(dy) << 8) | (b(dz) << 16) | static_cast<int>(0x80000000u);
+}
+
+// Host: the cone word of a float cone (axis, thr) as AccelHost holds it.
+inline int cone_word(float ax, float ay, float az, float thr) {
+    if (thr <= -6.0f) return kConeNp;  // kNoPrune (accel.h)
+    const double t = std::floor((16129.0 * static_cast<double>(thr) - 222.0) / 128.0);
+    if (!(t > -128.0) || !std::isfinite(ax) || !std::isfinite(ay) || !std::isfinite(az)) return kConeNever;
+    const double a[3] = {ax, ay, az};
+    if (!(std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]) <= 1.0000001)) return kConeNever;  // the bound needs |a| ~ 1
+    int w = 0;
+    for (int i = 0; i < 3; ++i) w |= (static_cast<int>(std::nearbyint(127.0 * a[i])) & 0xff) << (8 * i);
+    return w | ((static_cast<int>(t > 127.0 ? 127.0 : t) & 0xff) << 24);
+}
 
 RTA_HD float clamp_inv(float d) {
     return std::fabs(d) < 1.0f / kInvCap ? std::copysign(kInvCap, d) : 1.0f / d;
@@ -61,6 +112,7 @@ RTA_HD RayC ray_consts(float ox, float oy, float oz, float dx, float dy, float d
     c.dx = dx * c.rdl;
     c.dy = dy * c.rdl;
     c.dz = dz * c.rdl;
+    c.dq = ray_dq(c.dx, c.dy, c.dz);
     return c;
 }
 

@@ -729,10 +729,6 @@ __device__ __forceinline__ bool box_enter(const rta::RayC& c, float4 lo, float4 
     return rta::box_enter(c, lo.x, lo.y, lo.z, hi.x, hi.y, hi.z, tl, te);
 }
 
-__device__ __forceinline__ bool cone_ok(const rta::RayC& c, float4 k) {
-    return !rta::cone_culls(c, k.x, k.y, k.z, k.w);
-}
-
 // Scene-tree item (accel.h, SceneTree): the exact box test of its reference
 // leaf (gpu_shader.comp:364-377; NaN-free for the rays that take the scene
 // tree), then its prim range.
@@ -876,20 +872,64 @@ __device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f
     h1 = (tn[1] <= tf[1]) & !(dn[1] < thr[1]);
 }
 
+// The barycentric accelerator's wide node, 8 float4 = 128 B (one cache line):
+// the four children's boxes as above, one quantized back-face cone word per
+// child (accel_math.h, cone_word; kConeNp marks a kNoPrune child) and the child
+// codes. Same boxes, entry parameters and limits as wide_pair; the cone test is
+// one dot4 per child.
+__device__ __forceinline__ void wide_pair_q(const rta::RayC& c, float tl, f2 lx, f2 ly, f2 lz, f2 hx, f2 hy, f2 hz,
+                                            int w0, int w1, float& t0, float& t1, bool& h0, bool& h1) {
+    const f2 ix = {c.ix, c.ix}, iy = {c.iy, c.iy}, iz = {c.iz, c.iz};
+    const f2 ox = {-c.ox, -c.ox}, oy = {-c.oy, -c.oy}, oz = {-c.oz, -c.oz};
+    const f2 x0 = fma2(lx, ix, ox), x1 = fma2(hx, ix, ox);
+    const f2 y0 = fma2(ly, iy, oy), y1 = fma2(hy, iy, oy);
+    const f2 z0 = fma2(lz, iz, oz), z1 = fma2(hz, iz, oz);
+    const int w[2] = {w0, w1};
+    float tn[2], tf[2], te[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const bool np = w[k] == rta::kConeNp;
+        tn[k] = fmaxf(fmaxf(fminf(x0[k], x1[k]), fminf(y0[k], y1[k])), fmaxf(fminf(z0[k], z1[k]), 0.0f));
+        const float tz = fmaxf(z0[k], z1[k]);
+        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), np ? fminf(tz, INFINITY) : fminf(tz, tl));
+        te[k] = np ? 0.0f : tn[k];
+    }
+    t0 = te[0];
+    t1 = te[1];
+    h0 = (tn[0] <= tf[0]) & !rta::cone_culls_q(w0, c.dq);
+    h1 = (tn[1] <= tf[1]) & !rta::cone_culls_q(w1, c.dq);
+}
+
+// Wide-node record stride in float4: 8 (quantized cones), 11 for the
+// Moller-Trumbore accelerator's float grazing cones.
+constexpr int kWideRec = 8, kWideRecMt = 11;
+
 template <bool MT = false>
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
-    const float4* q = A.lnodes + 11 * static_cast<size_t>(uc & 0x3fffffffu);
+    const float4* q = A.lnodes + (MT ? kWideRecMt : kWideRec) * static_cast<size_t>(uc & 0x3fffffffu);
     const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
-    const float4 ax = q[6], ay = q[7], az = q[8], th = q[9], cd = q[10];
-    const int cc[4] = {__float_as_int(cd.x), __float_as_int(cd.y), __float_as_int(cd.z), __float_as_int(cd.w)};
     float t[4];
     bool h[4];
-    wide_pair<MT>(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y}, (f2){hy.x, hy.y},
-              (f2){hz.x, hz.y}, (f2){ax.x, ax.y}, (f2){ay.x, ay.y}, (f2){az.x, az.y}, (f2){th.x, th.y}, t[0], t[1],
-              h[0], h[1]);
-    wide_pair<MT>(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w}, (f2){hy.z, hy.w},
-              (f2){hz.z, hz.w}, (f2){ax.z, ax.w}, (f2){ay.z, ay.w}, (f2){az.z, az.w}, (f2){th.z, th.w}, t[2], t[3],
-              h[2], h[3]);
+    int cc[4];
+    if (MT) {
+        const float4 ax = q[6], ay = q[7], az = q[8], th = q[9], cd = q[10];
+        cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
+        cc[3] = __float_as_int(cd.w);
+        wide_pair<MT>(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y},
+                      (f2){hy.x, hy.y}, (f2){hz.x, hz.y}, (f2){ax.x, ax.y}, (f2){ay.x, ay.y}, (f2){az.x, az.y},
+                      (f2){th.x, th.y}, t[0], t[1], h[0], h[1]);
+        wide_pair<MT>(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w},
+                      (f2){hy.z, hy.w}, (f2){hz.z, hz.w}, (f2){ax.z, ax.w}, (f2){ay.z, ay.w}, (f2){az.z, az.w},
+                      (f2){th.z, th.w}, t[2], t[3], h[2], h[3]);
+    } else {
+        const float4 cw = q[6], cd = q[7];
+        cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
+        cc[3] = __float_as_int(cd.w);
+        wide_pair_q(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y}, (f2){hy.x, hy.y},
+                    (f2){hz.x, hz.y}, __float_as_int(cw.x), __float_as_int(cw.y), t[0], t[1], h[0], h[1]);
+        wide_pair_q(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w}, (f2){hy.z, hy.w},
+                    (f2){hz.z, hz.w}, __float_as_int(cw.z), __float_as_int(cw.w), t[2], t[3], h[2], h[3]);
+    }
     Kids4 k;
 #pragma unroll
     for (int s2 = 0; s2 < 4; ++s2) {
@@ -1926,6 +1966,7 @@ struct AnimOut {
     const int* prim_seq;
     float4* sbox;                     // per animated shape: reference box, conservative box (4 float4)
     float origin_lim;
+    int mt;                           // the accelerator's wide nodes: kWideRecMt float cones, else kWideRec
 };
 
 // One thread per animated shape: rewrites its records and derives its two
@@ -1959,7 +2000,10 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
     if (fl & AF_CONE)
         for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
             const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
-            reinterpret_cast<float*>(o.lnodes + 11 * static_cast<size_t>(w) + 9)[sl] = -4.f;  // never cull
+            if (o.mt)
+                reinterpret_cast<float*>(o.lnodes + kWideRecMt * static_cast<size_t>(w) + 9)[sl] = -4.f;
+            else  // never cull
+                reinterpret_cast<int*>(o.lnodes + kWideRec * static_cast<size_t>(w) + 6)[sl] = rta::kConeNever;
         }
     if (!(fl & AF_BOUNDED)) return;
     rta::Box3 b;
@@ -2023,7 +2067,8 @@ __global__ __launch_bounds__(256) void k_grow_nodes(AnimMaps m, AnimOut o) {
 // (a local subtree's prims are contiguous, accel.cpp LocalBuilder).
 // dirty[j] = (4*w + s, first prim, end prim, 0).
 __global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ dirty, int n,
-                                                     const float4* __restrict__ pbox, float4* __restrict__ lnodes) {
+                                                     const float4* __restrict__ pbox, float4* __restrict__ lnodes,
+                                                     int rec) {
     const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= n) return;
     const int4 d = dirty[j];
@@ -2037,18 +2082,18 @@ __global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ di
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
         const int w = d.x >> 2, sl = d.x & 3;
         const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
-        reinterpret_cast<float*>(lnodes + 11 * static_cast<size_t>(w) + lane)[sl] = v;
+        reinterpret_cast<float*>(lnodes + rec * static_cast<size_t>(w) + lane)[sl] = v;
     }
 }
 
 // Scene-tree wide slots of the unbounded subtree (kNoPrune): their boxes are the
 // reference leaves' padded boxes, which animation grows; while a set is animated
 // they are infinite (entered by every ray; the items' exact boxes still gate).
-__global__ void k_inf_slots(const int* __restrict__ slots, int n, float4* __restrict__ lnodes) {
+__global__ void k_inf_slots(const int* __restrict__ slots, int n, float4* __restrict__ lnodes, int rec) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int w = slots[i] >> 2, sl = slots[i] & 3;
-    for (int r = 0; r < 6; ++r) reinterpret_cast<float*>(lnodes + 11 * static_cast<size_t>(w) + r)[sl] = r < 3 ? -INFINITY : INFINITY;
+    for (int r = 0; r < 6; ++r) reinterpret_cast<float*>(lnodes + rec * static_cast<size_t>(w) + r)[sl] = r < 3 ? -INFINITY : INFINITY;
 }
 
 // The scene-tree items' exact boxes (titems) from the grown reference leaves.
@@ -2355,8 +2400,10 @@ int build_upload_accel(rt_ctx* c) {
         an[4 * k + 2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[k]));
         an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
     }
-    // lnodes: the wide local nodes (accel.h, build_wide), 11 float4 each (wide_kids).
+    // lnodes: the wide local nodes (accel.h, build_wide), kWideRec float4 each with
+    // quantized cones (kWideRecMt with the MT accelerator's float grazing cones; wide_kids).
     const size_t P = A.prim_shape.size();
+    const int rec = A.mt ? kWideRecMt : kWideRec;
     bool codes_ok = true;
     auto leaf_code = [&](size_t j) -> int {
         const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
@@ -2370,7 +2417,7 @@ int build_upload_accel(rt_ctx* c) {
     const size_t nw = A.wchild.size() / rta::kWide;
     const size_t nws = use_st ? T.wchild.size() / rta::kWide : 0;
     if (nw + nws >= (1u << 28) || T.item_ref.size() >= (1u << 28)) return RT_OK;
-    std::vector<float4> ln(11 * (nw + nws ? nw + nws : 1));
+    std::vector<float4> ln(rec * (nw + nws ? nw + nws : 1));
     auto emit_wide = [&](size_t w, size_t at, const std::vector<int>& wchild, const std::vector<int>& wsub,
                          const std::vector<rta::Box3>& boxes, const std::vector<float>& cones,
                          const std::function<int(int)>& leaf_of, size_t sub_base) {
@@ -2391,10 +2438,14 @@ int build_upload_accel(rt_ctx* c) {
                 code = sub < 0 ? leaf_of(j) : static_cast<int>(kLocal | static_cast<unsigned>(sub_base + sub));
             }
             for (int a = 0; a < 6; ++a) v[a][s2] = box[a];
-            for (int a = 0; a < 4; ++a) v[6 + a][s2] = cone[a];
-            v[10][s2] = bits_f(code);
+            if (A.mt) {
+                for (int a = 0; a < 4; ++a) v[6 + a][s2] = cone[a];
+            } else {
+                v[6][s2] = bits_f(j < 0 ? rta::kConeNever : rta::cone_word(cone[0], cone[1], cone[2], cone[3]));
+            }
+            v[rec - 1][s2] = bits_f(code);
         }
-        for (int r = 0; r < 11; ++r) ln[11 * at + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
+        for (int r = 0; r < rec; ++r) ln[rec * at + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
     };
     for (size_t w = 0; w < nw; ++w)
         emit_wide(w, w, A.wchild, A.wsub, A.lbox, A.lcone, [&](int j) { return leaf_code(static_cast<size_t>(j)); },
@@ -2690,7 +2741,7 @@ int prepare_animation(rt_ctx* c) {
             HIP_TRY(hipMemcpyAsync(c->anim_inf_slots, inf_slots.data(), inf_slots.size() * sizeof(int),
                                    hipMemcpyHostToDevice, c->stream));
             hipLaunchKernelGGL(k_inf_slots, dim3((c->n_inf_slots + 255) / 256), dim3(256), 0, c->stream,
-                               c->anim_inf_slots, c->n_inf_slots, c->lnodes);
+                               c->anim_inf_slots, c->n_inf_slots, c->lnodes, c->accel.mt ? kWideRecMt : kWideRec);
             HIP_TRY(hipGetLastError());
         }
     }
@@ -3462,7 +3513,7 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat,
                       acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
                       acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
-                      c->accel.origin_lim};
+                      c->accel.origin_lim, c->accel.mt ? 1 : 0};
     hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
                        reinterpret_cast<const FlatShape*>(c->anim_frame),
                        reinterpret_cast<const int*>(c->anim_frame + n * sizeof(FlatShape)), c->anim, out);
@@ -3470,7 +3521,7 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
         hipLaunchKernelGGL(k_grow_nodes, dim3((c->anim.nodes + 3) / 4), dim3(256), 0, c->stream, c->anim, out);
     if (acc && c->n_dirty > 0)
         hipLaunchKernelGGL(k_refit_local, dim3((c->n_dirty + 3) / 4), dim3(256), 0, c->stream, c->refit_dirty,
-                           c->n_dirty, c->pbox, c->lnodes);
+                           c->n_dirty, c->pbox, c->lnodes, c->accel.mt ? kWideRecMt : kWideRec);
     if (c->N > 0)
         hipLaunchKernelGGL(k_refresh_nodes, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, c->N,
                            c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr);

@@ -447,3 +447,13 @@ def test_accel_mt_matches_reference_walk(check_lib, src, tree):
         # the normal splits of the MT local build (accel.cpp kMtNormalBias) keep the
         # grazing cones tight: 801 tests per ray with spatial splits alone, 642 kept
         assert info[4] < 700, info[4]
+
+
+def test_quantized_cones_conservative():
+    """The wide nodes' quantized back-face cones (accel_math.h cone_word /
+    cone_culls_q) cull only directions the float cone culls: 4M random and
+    near-boundary directions over 20k cones (tests/native/cone_check.cpp)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "native"), "build/cone_check"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "tests", "native", "build", "cone_check")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0 and "cone_check ok" in r.stdout, r.stdout + r.stderr
