@@ -182,7 +182,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                             if (!grazing(rc, k) && !padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
                         } else {
                             if (!padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
-                            if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                            if (rta::cone_culls_q(rta::cone_word(k[0], k[1], k[2], k[3]), rc.dq)) continue;  // the device's quantized cone
                         }
                         const int sub = A.st.wsub[rta::kWide * w + s2];
                         if (sub >= 0) {
@@ -218,7 +218,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                             if (!grazing(rc, k) && !padded(rc, A.lbox[j], l)) continue;
                         } else {
                             if (!padded(rc, A.lbox[j], l)) continue;
-                            if (rta::cone_culls(rc, k[0], k[1], k[2], k[3])) continue;
+                            if (rta::cone_culls_q(rta::cone_word(k[0], k[1], k[2], k[3]), rc.dq)) continue;  // the device's quantized cone
                         }
                         if (A.la[j] < 0) scan(-A.la[j] - 1, A.lb[j]);
                         else st.push_back(-(A.wsub[rta::kWide * w + s2] + 1));
