@@ -38,6 +38,21 @@ struct GeoRec {
 };
 static_assert(sizeof(GeoRec) == 80, "GeoRec is 5 float4");
 
+// The accelerated walks' prim record (k_pack_prims), 64 B: f[0..14] as GeoRec's,
+// except that triangles keep d01 in f[13] and the barycentric denominator in
+// f[14]; d00 and d11 are recomputed from the stored edges with pack_geo's float
+// operations, so they have the same bits. st = seq << 2 | type, seq the shape's
+// rank in the reference walk: (distance, st) orders candidates as (distance, seq).
+// Shape types outside 0-3 are packed as planes with a NaN normal (no hit, as in
+// the reference). The shape index is kept apart (AccelPtrs::prim_shape), read
+// once per bounce for the winner's material.
+struct PrimRec {
+    float f[15];
+    int st;
+};
+static_assert(sizeof(PrimRec) == 64, "PrimRec is 4 float4");
+__device__ __forceinline__ int prim_type(const PrimRec& g) { return g.st & 3; }
+
 struct V {
     float x, y, z;
 };
@@ -211,6 +226,10 @@ __device__ __forceinline__ V shape_normal(const GeoRec& g, V p) {
     if (g.type == 0) return normalize(p - mk(g.f[0], g.f[1], g.f[2]));
     return mk(g.f[0], g.f[1], g.f[2]);
 }
+__device__ __forceinline__ V shape_normal(const PrimRec& g, V p) {
+    if (prim_type(g) == 0) return normalize(p - mk(g.f[0], g.f[1], g.f[2]));
+    return mk(g.f[0], g.f[1], g.f[2]);
+}
 
 struct Mat {
     V color;
@@ -273,6 +292,15 @@ __device__ __forceinline__ GeoRec load_rec(const float4* __restrict__ base, int 
     const float4* src = base + 5 * static_cast<size_t>(j);
 #pragma unroll
     for (int k = 0; k < 5; ++k) dst[k] = src[k];
+    return g;
+}
+
+__device__ __forceinline__ PrimRec load_prim(const float4* __restrict__ base, int j) {
+    PrimRec g;
+    float4* dst = reinterpret_cast<float4*>(&g);
+    const float4* src = base + 4 * static_cast<size_t>(j);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = src[k];
     return g;
 }
 

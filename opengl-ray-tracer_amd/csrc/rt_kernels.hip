@@ -103,6 +103,28 @@ __device__ __forceinline__ void store_geo(float4* out, const GeoRec& g) {
     for (int k = 0; k < 5; ++k) out[k] = in[k];
 }
 
+// PrimRec (rt_device.h) of a shape's GeoRec and its rank in the reference walk.
+__device__ __forceinline__ PrimRec pack_prim(const GeoRec& g, int seq) {
+    PrimRec p;
+    for (int k = 0; k < 15; ++k) p.f[k] = g.f[k];
+    int type = g.type;
+    if (type == 3) {
+        p.f[13] = g.f[14];  // d01
+        p.f[14] = g.f[16];  // d00 * d11 - d01 * d01
+    } else if (type < 0 || type > 3) {  // no INNER hit (get_intersection: NONE)
+        type = 1;
+        p.f[0] = p.f[1] = p.f[2] = __int_as_float(0x7fc00000);
+    }
+    p.st = (seq << 2) | type;
+    return p;
+}
+
+__device__ __forceinline__ void store_prim(float4* prims, int j, const PrimRec& p) {
+    const float4* in = reinterpret_cast<const float4*>(&p);
+    float4* out = prims + 4 * static_cast<size_t>(j);
+    for (int k = 0; k < 4; ++k) out[k] = in[k];
+}
+
 __device__ __forceinline__ void store_mat(float4* mat, int j, const FlatMaterial& m) {
     mat[2 * j] = make_float4(m.color.x, m.color.y, m.color.z, m.fresnelStrength);
     mat[2 * j + 1] =
@@ -535,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_packet(const float4* __restrict__ ge
 
 struct AccelPtrs {
     const float4* __restrict__ anodes;  // 4 float4 per reference node (the root's entry test)
-    const float4* __restrict__ prims;   // 5 float4 per prim, f[17] = rank
+    const float4* __restrict__ prims;   // 4 float4 per prim (PrimRec)
     const float4* __restrict__ lnodes;  // 6 float4 per local inner node: both child boxes + codes, cones
     const float4* __restrict__ wnodes;  // 8 float4 per reference inner node: both children's exact + content boxes
     const int4* __restrict__ tleaf;     // per reference leaf: plain start, plain count, local root code
@@ -549,6 +571,7 @@ struct AccelPtrs {
     int boxes_finite;                   // no reference node box holds a NaN (ray_aabb_fast)
     int split_max;                      // lane_walk_any: split walks of waves with <= this many rays (0: off)
     int split_g;                        // ... over groups of at most this many lanes (a power of two)
+    const int* __restrict__ prim_shape; // shape index per prim slot (the winner's material)
 };
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
@@ -597,11 +620,24 @@ __device__ __forceinline__ bool mt_hit(const float* f, const Ray& r, V& p, float
     return true;
 }
 
+// The barycentric terms of a PrimRec triangle (gpu_shader.comp:218-229): d00 and
+// d11 recomputed as pack_geo computes them, d01 and the denominator stored.
+__device__ __forceinline__ bool tri_inside(const float* f, V p) {
+    const V e1 = mk(f[7], f[8], f[9]), e2 = mk(f[10], f[11], f[12]);
+    const V tp = p - mk(f[4], f[5], f[6]);
+    const float d20 = dot(tp, e1), d21 = dot(tp, e2);
+    const float d00 = dot(e1, e1), d11 = dot(e2, e2);
+    const float v = (d11 * d20 - f[13] * d21) / f[14];
+    const float w = (d00 * d21 - f[13] * d20) / f[14];
+    const float u = 1.0f - v - w;
+    return !(u < 0.0f || v < 0.0f || w < 0.0f);
+}
+
 template <bool MT = false>
-__device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray& r, Best& b) {
+__device__ __forceinline__ void try_closest(const PrimRec& g, int slot, const Ray& r, Best& b) {
     const float* f = g.f;
-    const int seq = __float_as_int(f[17]);
-    if (MT && g.type == 3) {
+    const int seq = g.st, type = prim_type(g);
+    if (MT && type == 3) {
         V p;
         float t;
         if (!mt_hit(f, r, p, t)) return;
@@ -609,7 +645,7 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
         if (lex_better(d, seq, b)) b = Best{d, seq, t, slot};
         return;
     }
-    if (g.type == 0) {
+    if (type == 0) {
         V c = mk(f[0], f[1], f[2]);
         V oc = r.o - c;
         float aa = dot(r.d, r.d);
@@ -626,7 +662,6 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
         }
         return;
     }
-    if (g.type < 1 || g.type > 3) return;
     V n = mk(f[0], f[1], f[2]);
     const float np = dot(n, r.d);
     // INNER needs np > 0 and t = num / np > 0 (gpu_shader.comp:206-212,276-283):
@@ -639,33 +674,28 @@ __device__ __forceinline__ void try_closest(const GeoRec& g, int slot, const Ray
     V p = hit_point(r, t);
     float d = dist(r.o, p);
     if (!lex_better(d, seq, b)) return;
-    if (g.type == 2) {
+    if (type == 2) {
         V lp = p - mk(f[4], f[5], f[6]);
         float up = dot(lp, mk(f[9], f[10], f[11]));
         float vp = dot(lp, mk(f[12], f[13], f[14]));
         if (up < 0.0f || up > f[7] || vp < 0.0f || vp > f[8]) return;
-    } else if (g.type == 3) {
-        V tp = p - mk(f[4], f[5], f[6]);
-        float d20 = dot(tp, mk(f[7], f[8], f[9]));
-        float d21 = dot(tp, mk(f[10], f[11], f[12]));
-        float v = (f[15] * d20 - f[14] * d21) / f[16];
-        float w = (f[13] * d21 - f[14] * d20) / f[16];
-        float u = 1.0f - v - w;
-        if (u < 0.0f || v < 0.0f || w < 0.0f) return;
+    } else if (type == 3) {
+        if (!tri_inside(f, p)) return;
     }
     b = Best{d, seq, t, slot};
 }
 
 // Shadow candidate: an INNER hit nearer than lim (gpu_shader.comp:473-480).
 template <bool MT = false>
-__device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float lim) {
+__device__ __forceinline__ bool try_shadow(const PrimRec& g, const Ray& r, float lim) {
     const float* f = g.f;
-    if (MT && g.type == 3) {
+    const int type = prim_type(g);
+    if (MT && type == 3) {
         V p;
         float t;
         return mt_hit(f, r, p, t) && dist(r.o, p) < lim;
     }
-    if (g.type == 0) {
+    if (type == 0) {
         V c = mk(f[0], f[1], f[2]);
         V oc = r.o - c;
         float aa = dot(r.d, r.d);
@@ -676,7 +706,6 @@ __device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float 
         float t1 = (-bb - __builtin_sqrtf(D)) / (2.0f * aa);
         return t1 > 0.0f && dist(r.o, r.o + t1 * r.d) < lim;
     }
-    if (g.type < 1 || g.type > 3) return false;
     V n = mk(f[0], f[1], f[2]);
     const float np = dot(n, r.d);
     if (!(np > 0.0f)) return false;  // signs first, as in try_closest
@@ -686,21 +715,13 @@ __device__ __forceinline__ bool try_shadow(const GeoRec& g, const Ray& r, float 
     if (!(t > 0.0f)) return false;
     V p = r.o + t * r.d;
     if (!(dist(r.o, p) < lim)) return false;
-    if (g.type == 2) {
+    if (type == 2) {
         V lp = p - mk(f[4], f[5], f[6]);
         float up = dot(lp, mk(f[9], f[10], f[11]));
         float vp = dot(lp, mk(f[12], f[13], f[14]));
         return !(up < 0.0f || up > f[7] || vp < 0.0f || vp > f[8]);
     }
-    if (g.type == 3) {
-        V tp = p - mk(f[4], f[5], f[6]);
-        float d20 = dot(tp, mk(f[7], f[8], f[9]));
-        float d21 = dot(tp, mk(f[10], f[11], f[12]));
-        float v = (f[15] * d20 - f[14] * d21) / f[16];
-        float w = (f[13] * d21 - f[14] * d20) / f[16];
-        float u = 1.0f - v - w;
-        return !(u < 0.0f || v < 0.0f || w < 0.0f);
-    }
+    if (type == 3) return tri_inside(f, p);
     return true;
 }
 
@@ -1197,14 +1218,14 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
 #if RT_LEAF_PREFETCH
         // the leaf's records software-pipelined: record i + 1's loads are in flight while
         // record i is tested (a leaf is a chain of dependent loads otherwise)
-        GeoRec gn;
-        if (count > 0) gn = load_rec(A.prims, start);
+        PrimRec gn;
+        if (count > 0) gn = load_prim(A.prims, start);
         for (int i = 0; i < count; ++i) {
-            const GeoRec g = gn;
-            if (i + 1 < count) gn = load_rec(A.prims, start + i + 1);
+            const PrimRec g = gn;
+            if (i + 1 < count) gn = load_prim(A.prims, start + i + 1);
 #else
         for (int i = 0; i < count; ++i) {
-            const GeoRec g = load_rec(A.prims, start + i);
+            const PrimRec g = load_prim(A.prims, start + i);
 #endif
             if (COUNT) wc.tests++;
             if (WSTAT && first_active()) wc.wtests++;
@@ -1428,7 +1449,7 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
         if (count > 0) {
             bool live = lane_in(m) && item_in;
             for (int i = 0; i < count; ++i) {
-                const GeoRec g = load_rec(A.prims, start + i);
+                const PrimRec g = load_prim(A.prims, start + i);
                 if (WSTAT) wc.wtests += lane_id() == 0 ? 1u : 0u;
                 if (live) {
                     if (COUNT) wc.tests++;
@@ -1564,7 +1585,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
     float ld = 0.f;
     if (alive) {
         const V hp = hit_point(ray, best.t);
-        const V hn = shape_normal(load_rec(A.prims, best.slot), hp);
+        const V hn = shape_normal(load_prim(A.prims, best.slot), hp);
         sr = Ray{hp + hn * kp.shadow_off, normalize(kp.light_pos - hp)};
         ld = dist(kp.light_pos, hp);
     }
@@ -1579,9 +1600,10 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
         packet_walk<true, COST || COUNT, COUNT, MT>(A, sr, alive, gmin(ld, 1e20f), dummy, shadow, wc);
     if (COUNT) walk_rec(rec, 2 * depth + 1, w0, wc, clock64() - c0);
     if (alive) {
-        const GeoRec g = load_rec(A.prims, best.slot);
+        const PrimRec g = load_prim(A.prims, best.slot);
         const V hp = hit_point(ray, best.t);
-        alive = shade_bounce(kp, ray, hp, shape_normal(g, hp), load_mat(mat, g.idx), shadow, acc, att, 1e-3f);
+        alive = shade_bounce(kp, ray, hp, shape_normal(g, hp), load_mat(mat, A.prim_shape[best.slot]), shadow, acc,
+                             att, 1e-3f);
     }
 }
 
@@ -1815,12 +1837,7 @@ __global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __re
                              const int* __restrict__ prim_seq, int P, float4* __restrict__ prims) {
     int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= P) return;
-    const float4* src = geo_lin + 5 * static_cast<size_t>(prim_shape[j]);
-    float4* dst = prims + 5 * static_cast<size_t>(j);
-    for (int k = 0; k < 4; ++k) dst[k] = src[k];
-    float4 last = src[4];
-    last.w = __int_as_float(prim_seq[j]);  // f[17]: rank in the reference walk
-    dst[4] = last;
+    store_prim(prims, j, pack_prim(load_rec(geo_lin, prim_shape[j]), prim_seq[j]));
 }
 
 // Dispatch order for the next frame (rt_set_schedule): tiles sorted by the
@@ -1993,9 +2010,7 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
     if (!o.anodes) return;
     for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {
         const int p = m.prim_list[q];
-        GeoRec gp = g;
-        gp.f[17] = __int_as_float(o.prim_seq[p]);  // rank in the reference walk (k_pack_prims)
-        store_geo(o.prims + 5 * static_cast<size_t>(p), gp);
+        store_prim(o.prims, p, pack_prim(g, o.prim_seq[p]));  // rank in the reference walk (k_pack_prims)
     }
     if (fl & AF_CONE)
         for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
@@ -2518,6 +2533,8 @@ int build_upload_accel(rt_ctx* c) {
         }
     }
     if (!codes_ok) return RT_OK;
+    for (size_t i = 0; i < P; ++i)  // PrimRec::st = seq << 2 | type
+        if (A.prim_seq[i] < 0 || A.prim_seq[i] >= (1 << 29)) return RT_OK;
     std::vector<int> ps(2 * (P ? P : 1));
     for (size_t i = 0; i < P; ++i) {
         ps[i] = A.prim_shape[i];
@@ -2528,7 +2545,7 @@ int build_upload_accel(rt_ctx* c) {
         hipMalloc(&c->wnodes, wn.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->tleaf, tl.size() * sizeof(int4)) != hipSuccess ||
         hipMalloc(&c->titems, ti.size() * sizeof(float4)) != hipSuccess ||
-        hipMalloc(&c->prims, 5 * (P ? P : 1) * sizeof(float4)) != hipSuccess ||
+        hipMalloc(&c->prims, 4 * (P ? P : 1) * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->prim_idx_dev, ps.size() * sizeof(int)) != hipSuccess)
         return RT_ERR_NO_MEMORY;
     HIP_TRY(hipMemcpyAsync(c->anodes, an.data(), an.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -2544,7 +2561,7 @@ int build_upload_accel(rt_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));  // the host vectors die here
     c->st_root = use_st ? static_cast<int>(kLocal | static_cast<unsigned>(nw + T.wroot)) : kNoChild;
     c->accel_ok = true;
-    c->record_bytes = (an.size() + ln.size() + wn.size() + tl.size() + ti.size() + 5 * P + 2 * static_cast<size_t>(c->S)) *
+    c->record_bytes = (an.size() + ln.size() + wn.size() + tl.size() + ti.size() + 4 * P + 2 * static_cast<size_t>(c->S)) *
                       sizeof(float4);
     return RT_OK;
 }
@@ -3152,7 +3169,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
 
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
-                          c->boxes_finite, c->split_max, c->split_g};
+                          c->boxes_finite, c->split_max, c->split_g, c->prim_idx_dev};
         // compaction: bounces >= tail_from of the rays still alive run in k_accel_tail
         k2.tail_queue = nullptr;
         // RT_TAIL_AUTO: from bounce 2 on scenes of many scene-tree items (measured: config 5's
