@@ -40,7 +40,13 @@ struct Item {
     float c[3];
     float n[3] = {0, 0, 0};  // MT: the triangle's unit normal, either orientation (hn)
     bool hn = false;
+    bool big = false;  // MT: |e1||e2| > kMtBigX (its 1e-5 floor bound is loose or absent)
 };
+
+// MT triangles with |e1||e2| above this are kept apart from the rest at the
+// first split of a local tree (mt_pad takes a node's worst |e1||e2| with its
+// smallest |e1 x e2|, so mixing them would leave every ancestor unbounded).
+constexpr double kMtBigX = 4.0;
 
 // MT builds (AccelHost::mt): the orientation-free normal cone of the items a
 // predicate selects, as the build's cost model sees it (build_cones_mt computes
@@ -93,7 +99,11 @@ NCone normal_cone(const std::vector<Item>& items, int b, int e, F sel) {
 #endif
 constexpr double kMtNormalBias = RTA_MT_NORMAL_BIAS;
 #ifndef RTA_MT_LEAF
+#if RTA_MT_RAYPAD
+#define RTA_MT_LEAF 2
+#else
 #define RTA_MT_LEAF 6
+#endif
 #endif
 constexpr int kMtLeaf = RTA_MT_LEAF;  // MT local leaves hold at most this many prims
 
@@ -185,6 +195,14 @@ struct LocalBuilder {
         max_depth_seen = std::max(max_depth_seen, depth);
         const int n = e - b;
         if (n <= (out.mt ? kMtLeaf : 4) || budget <= 0) return leaf(b, e);
+        if (out.mt) {
+            const int nb = static_cast<int>(std::count_if(items.begin() + b, items.begin() + e,
+                                                          [](const Item& x) { return x.big; }));
+            if (nb > 0 && nb < n) {
+                auto it = std::partition(items.begin() + b, items.begin() + e, [](const Item& x) { return x.big; });
+                return inner(b, static_cast<int>(it - items.begin()), e, 0, depth, budget);
+            }
+        }
         Box3 box = empty_box();
         float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (int i = b; i < e; ++i) {
@@ -276,6 +294,12 @@ struct LocalBuilder {
             std::nth_element(items.begin() + b, items.begin() + mid, items.begin() + e,
                              [&](const Item& x, const Item& y) { return x.c[axis] < y.c[axis]; });
         }
+        return inner(b, mid, e, axis, depth, budget);
+    }
+
+    int inner(int b, int mid, int e, int axis, int depth, int budget) {
+        Box3 box = empty_box();
+        for (int i = b; i < e; ++i) grow(box, items[i].box);
         const int k = static_cast<int>(out.lbox.size());
         out.lbox.push_back(box);
         out.la.push_back(0);
@@ -391,6 +415,109 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         done[j] = 1;
         return cones[j];
     };
+#if RTA_MT_RAYPAD
+    // Per-ray padding (accel_bound.h, MtTri; accel_math.h mt_pad): the cone's
+    // s = 2 sin(theta/2) bounds |n - axis| for every normal below, so
+    // |cos(d, n)| >= |d . axis| - s; the node constants take the worst triangle.
+    double zlo[3] = {INFINITY, INFINITY, INFINITY}, zhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    std::vector<MtTri> tri(A.prim_shape.size());
+    std::vector<char> has(A.prim_shape.size(), 0);
+    for (size_t p = 0; p < A.prim_shape.size(); ++p) {
+        const FlatShape& s = shapes[A.prim_shape[p]];
+        Box3 b;
+        if (s.type != RT_TRIANGLE || classify_mt_tight(s, b, 0.0, tri[p]) != BOUNDED) continue;
+        has[p] = 1;
+        for (int a = 0; a < 3; ++a) {
+            zlo[a] = std::min(zlo[a], tri[p].p1[a]);
+            zhi[a] = std::max(zhi[a], tri[p].p1[a]);
+        }
+    }
+    for (int a = 0; a < 3; ++a) A.mt_z[a] = std::isfinite(zlo[a]) ? static_cast<float>(0.5 * (zlo[a] + zhi[a])) : 0.f;
+    struct Agg {
+        double cr = INFINITY, X = 0, esum = 0, m = 0;
+    };
+    // slab along the cone axis (mt_slab): min/max of a . vertex over the triangles below
+    auto slab = [&](size_t j, const float* ax, double& w, double& h0) {
+        double lo = INFINITY, hi = -INFINITY;
+        std::function<void(size_t)> rec = [&](size_t b) {
+            if (A.la[b] < 0) {
+                const int st = -A.la[b] - 1, n = A.lb[b];
+                for (int i = 0; i < n; ++i) {
+                    if (!has[st + i]) {  // a sphere (or other shape) below: its hits are not in any slab
+                        lo = -INFINITY;
+                        hi = INFINITY;
+                        continue;
+                    }
+                    const FlatShape& s = shapes[A.prim_shape[st + i]];
+                    for (const rt_vec3& v : {s.triP1, s.triP2, s.triP3}) {
+                        const double x = static_cast<double>(ax[0]) * v.x + static_cast<double>(ax[1]) * v.y +
+                                         static_cast<double>(ax[2]) * v.z;
+                        lo = std::min(lo, x);
+                        hi = std::max(hi, x);
+                    }
+                }
+            } else {
+                rec(static_cast<size_t>(A.la[b]));
+                rec(static_cast<size_t>(A.lb[b] & 0x3fffffff));
+            }
+        };
+        rec(j);
+        const bool fin = std::isfinite(lo) && std::isfinite(hi);
+        w = fin ? 0.5 * (lo + hi) : 0.0;
+        h0 = fin ? 0.5 * (hi - lo) : INFINITY;
+    };
+    std::vector<Agg> agg(M);
+    std::vector<char> adone(M, 0);
+    std::function<const Agg&(size_t)> aget = [&](size_t j) -> const Agg& {
+        if (adone[j]) return agg[j];
+        Agg g;
+        auto merge_in = [&](const Agg& x) {
+            g.cr = std::min(g.cr, x.cr);
+            g.X = std::max(g.X, x.X);
+            g.esum = std::max(g.esum, x.esum);
+            g.m = std::max(g.m, x.m);
+        };
+        if (A.la[j] < 0) {
+            const int st = -A.la[j] - 1, n = A.lb[j];
+            for (int i = 0; i < n; ++i) {
+                if (!has[st + i]) continue;
+                const MtTri& t = tri[st + i];
+                const double dz[3] = {t.p1[0] - A.mt_z[0], t.p1[1] - A.mt_z[1], t.p1[2] - A.mt_z[2]};
+                merge_in(Agg{t.cr, t.X, t.esum, std::sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2])});
+            }
+        } else {
+            merge_in(aget(static_cast<size_t>(A.la[j])));
+            merge_in(aget(static_cast<size_t>(A.lb[j] & 0x3fffffff)));
+        }
+        agg[j] = g;
+        adone[j] = 1;
+        return agg[j];
+    };
+    A.lmt.assign(kMtPadF * M, 0.f);
+    for (size_t j = 0; j < M; ++j) {
+        const GCone& c = get(j);
+        float* o = &A.lcone[4 * j];
+        o[0] = static_cast<float>(c.a[0]);
+        o[1] = static_cast<float>(c.a[1]);
+        o[2] = static_cast<float>(c.a[2]);
+        o[3] = (c.theta < 0 || c.theta >= 1.5) ? 2.f : static_cast<float>(2.0 * std::sin(0.5 * c.theta + 1e-6) + 2e-5);
+        const Agg& g = aget(j);
+        float* m = &A.lmt[kMtPadF * j];
+        if (!(g.X > 0)) {  // no triangle below: pad 0, no slab
+            m[5] = INFINITY;
+            continue;
+        }
+        const double up = 1.0 + 1e-5;
+        m[0] = static_cast<float>(g.cr * (1.0 - 1e-5));
+        m[1] = static_cast<float>(kU * g.X * up);
+        m[2] = static_cast<float>(g.m * up + 1e-5);
+        m[3] = static_cast<float>((18.0 * g.m + 10.5 * g.esum) * up + 1e-5);
+        double w, h0;
+        slab(j, o, w, h0);
+        m[4] = static_cast<float>(w);
+        m[5] = static_cast<float>(h0 * up + 1e-5 * (std::fabs(w) + 1.0));
+    }
+#else
     const double psi = std::asin(kMtCos);
     for (size_t j = 0; j < M; ++j) {
         const GCone& c = get(j);
@@ -401,6 +528,7 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         o[2] = static_cast<float>(c.a[2]);
         o[3] = c.theta < 0 ? -1.f : (t >= 1.5707 ? 2.f : static_cast<float>(std::sin(t)));
     }
+#endif
 }
 
 void build_cones(const FlatShape* shapes, AccelHost& A) {
@@ -948,6 +1076,9 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
             if (mt && mt_normal(shapes[si], nn)) {
                 it.hn = true;
                 for (int a = 0; a < 3; ++a) it.n[a] = static_cast<float>(nn[a]);
+                MtTri mtt;
+                Box3 tb;
+                it.big = classify_mt_tight(shapes[si], tb, 0.0, mtt) == BOUNDED && mtt.X > kMtBigX;
             }
             bounded.push_back(it);
         }

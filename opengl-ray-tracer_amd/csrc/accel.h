@@ -100,6 +100,11 @@ struct AccelHost {
     // enters the subtree whatever its box says (thr = -1: no triangle below, 2:
     // any ray). Reference-node content boxes are not used (flags bit 3 clear).
     bool mt = false;
+    // MT per-ray padding (accel_bound.h, mt_pad): per local node the worst-case
+    // triangle constants below it, kMtPadF floats each (MtPad order), and the
+    // centre Z the origin distance |o - Z| is measured from.
+    std::vector<float> lmt;
+    float mt_z[3] = {0.f, 0.f, 0.f};
 };
 
 // Builds the accelerator for a validated reference tree (see check_tree).

@@ -167,13 +167,71 @@ RTA_HD int classify_mt_triangle(const FlatShape& s, Box3& out, double origin_lim
     return BOUNDED;
 }
 
+// Per-ray Moller-Trumbore padding (AccelHost::lmt, accel_math.h mt_pad). The
+// bound above, taken per ray instead of for the worst origin and |cos| >=
+// kMtCos: with D = |d|, S >= |o - p1|, X = |e1||e2|, c = |cos(d, n)| and
+// A = max(1e-5, D c |e1 x e2|) - 7u D X the smallest |a| an accepted hit can
+// have (|a| = D c |e1 x e2| exactly, the computed one is >= 1e-5 and within
+// 7u D X of it),
+//   X* = p1 + u* e1 + v* e2 lies within Q = eu E1 + ev E2
+//      = u D X (18 S + 10.5 (E1 + E2)) / A of the triangle, and
+//   the computed t is within r |t*| + dl of t*, r = 7.07 u D X / A + 3u,
+//      dl = 9.09 u X S / A (the 2u T part is below the static box padding).
+// For r < 1/2, an accepted hit at t > 0 with distance below l therefore
+// implies that the ray enters the triangle's box padded by
+// P = Q + D dl / (1 - r) before parameter l / (|d| (1 - r)): X* is inside the
+// box padded by Q, and the ray point D dl / (1 - r) before X* (or the origin,
+// when t* is smaller) is then inside the box padded by P. mt_pad takes P
+// twice (kMtSafety) and, per local node, the worst triangle below it: the
+// smallest |e1 x e2| and cosine (the grazing cone), the largest X, E1 + E2 and
+// |p1 - Z|, with S = |o - Z| + |p1 - Z|. No kMtCos, no origin bound beyond
+// the static box's: a ray grazing a node's cone gets the 1e-5 floor's pad, and
+// only a node whose floor is below 2.5e-6 (triangles with X > ~6) is entered
+// whatever its box says.
+struct MtTri {
+    double cr, X, esum, p1[3];
+};
+
+// The static box of a triangle under per-ray MT padding: the triangle's own
+// box with the size/origin padding of `finish`, and its MtTri constants.
+RTA_HD int classify_mt_tight(const FlatShape& s, Box3& out, double origin_lim, MtTri& m) {
+    const float e1f[3] = {s.triP2.x - s.triP1.x, s.triP2.y - s.triP1.y, s.triP2.z - s.triP1.z};
+    const float e2f[3] = {s.triP3.x - s.triP1.x, s.triP3.y - s.triP1.y, s.triP3.z - s.triP1.z};
+    const D3 p1 = d3(s.triP1), e1{e1f[0], e1f[1], e1f[2]}, e2{e2f[0], e2f[1], e2f[2]};
+    if (!finite3(p1) || !finite3(e1) || !finite3(e2)) return UNBOUNDED;
+    const double E1 = sqrt(dot(e1, e1)), E2 = sqrt(dot(e2, e2)), cr = sqrt(dot(cross(e1, e2), cross(e1, e2)));
+    if (!(cr > 0) || !isfinite(cr) || !(E1 * E2 < 1e30)) return UNBOUNDED;
+    m.cr = cr;
+    m.X = E1 * E2;
+    m.esum = E1 + E2;
+    m.p1[0] = p1.x;
+    m.p1[1] = p1.y;
+    m.p1[2] = p1.z;
+    BoxAcc acc;
+    acc.add(p1);
+    acc.add(p1 + e1);
+    acc.add(p1 + e2);
+    out = finish(acc, origin_lim);
+    return BOUNDED;
+}
+
 // UNBOUNDED: no finite bound; BOUNDED: `out` is set; NEVER: the reference test
 // never returns INNER. origin_lim: largest |coordinate| of a ray origin the
 // bound must hold for (0 for the build's first pass, which only measures the
 // scene's magnitude). mt: triangles take the Moller-Trumbore test
 // (classify_mt_triangle; the other shapes' tests do not depend on it).
+#ifndef RTA_MT_RAYPAD
+#define RTA_MT_RAYPAD 1
+#endif
 RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim, bool mt = false) {
-    if (mt && s.type == RT_TRIANGLE) return classify_mt_triangle(s, out, origin_lim);
+    if (mt && s.type == RT_TRIANGLE) {
+#if RTA_MT_RAYPAD
+        MtTri m;
+        return classify_mt_tight(s, out, origin_lim, m);
+#else
+        return classify_mt_triangle(s, out, origin_lim);
+#endif
+    }
     BoxAcc acc;
     switch (s.type) {
         case RT_SPHERE: {

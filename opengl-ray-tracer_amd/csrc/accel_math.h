@@ -40,6 +40,9 @@ struct RayC {
     float dx, dy, dz;  // d / |d|
     float rdl;         // 1 / |d|
     int dq;            // rint(127 d/|d|) as 3 signed bytes, byte 3 = -128 (cone_culls_q)
+    // Moller-Trumbore walks only (mt_ray; dead, so free, in the other instances)
+    float mox, moy, moz;  // the origin
+    float so, on;         // |o - Z| rounded up (mt_origin_dist), |o|_1
 };
 
 // Quantized back-face cones (the barycentric accelerator's wide nodes,
@@ -132,10 +135,80 @@ RTA_HD bool box_enter(const RayC& c, float lx, float ly, float lz, float hx, flo
     return tn <= tf;
 }
 
+// box_enter with the exit parameter too.
+RTA_HD bool box_span(const RayC& c, float lx, float ly, float lz, float hx, float hy, float hz, float tl, float& tn,
+                     float& tf) {
+    const float x0 = std::fma(lx, c.ix, -c.ox), x1 = std::fma(hx, c.ix, -c.ox);
+    const float y0 = std::fma(ly, c.iy, -c.oy), y1 = std::fma(hy, c.iy, -c.oy);
+    const float z0 = std::fma(lz, c.iz, -c.oz), z1 = std::fma(hz, c.iz, -c.oz);
+    tn = std::fmax(std::fmax(std::fmin(x0, x1), std::fmin(y0, y1)), std::fmax(std::fmin(z0, z1), 0.0f));
+    tf = std::fmin(std::fmin(std::fmax(x0, x1), std::fmax(y0, y1)), std::fmin(std::fmax(z0, z1), tl));
+    return tn <= tf;
+}
+
 // Back-face cone (accel.h, build_cones): no shape below can give an INNER hit
 // (N.d > 0 is required) when dot(axis, d/|d|) < thr.
 RTA_HD bool cone_culls(const RayC& c, float ax, float ay, float az, float thr) {
     return std::fma(ax, c.dx, std::fma(ay, c.dy, az * c.dz)) < thr - kConeEps;
+}
+
+constexpr float kU24 = 5.9604645e-08f;
+// |o - Z| rounded up (AccelHost::mt_z), once per ray.
+RTA_HD float mt_origin_dist(float ox, float oy, float oz, const float* z) {
+    const float x = ox - z[0], y = oy - z[1], w = oz - z[2];
+    return 1.0001f * std::sqrt(x * x + y * y + w * w) + 1e-6f;
+}
+
+// The Moller-Trumbore walk's origin terms of RayC.
+RTA_HD void mt_ray(RayC& c, float ox, float oy, float oz, const float* z) {
+    c.mox = ox;
+    c.moy = oy;
+    c.moz = oz;
+    c.so = mt_origin_dist(ox, oy, oz, z);
+    c.on = std::fabs(ox) + std::fabs(oy) + std::fabs(oz);
+}
+
+// Moller-Trumbore per-ray padding (accel_bound.h, the derivation above
+// mt_node_consts). k: the node's grazing cone (axis, s = 2 sin(psi/2) + margin);
+// m: its MtPad constants {cr_min, u X_max, M_max, 18 M_max + 10.5 Esum_max};
+// so: |o - Z| of the ray. Returns false when no finite bound holds (the walk
+// enters at parameter 0); else `pad` to add to the node's static box on every
+// side and `lf` (>= 1) to multiply the distance limit by.
+constexpr int kMtPadF = 6;  // floats per local node in AccelHost::lmt
+RTA_HD bool mt_pad(const RayC& c, float so, const float* k, const float* m, float& pad, float& lf, float& q2,
+                   float& pt) {
+    const float D = 1.0001f / c.rdl;  // |d| (rounded up)
+    const float cn = std::fabs(std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz))) - k[3];
+    const float A = std::fmax(1e-5f, D * std::fmax(cn, 0.0f) * m[0]) - 7.0f * D * m[1];
+    if (!(A > 2.5e-6f)) return false;
+    const float ia = 1.0001f / A;
+    const float r = 7.07f * D * m[1] * ia + 3.0f * kU24;
+    if (!(r < 0.5f)) return false;
+    const float q = D * m[1] * std::fma(18.0f, so, m[3]) * ia;
+    const float dl = 9.09f * m[1] * (so + m[2]) * ia;
+    lf = 1.0001f / (1.0f - r);
+    q2 = 2.0f * q;
+    pt = 2.0f * D * dl * lf;
+    pad = q2 + pt;
+    return pad < 1e30f;
+}
+
+// The node's slab along its cone axis a: every triangle below lies within
+// |a.x - w| <= h0 (m[4] = w, m[5] = h0), and its plane within angle theta of
+// a's, 2 sin(theta/2) <= k[3]. X* (in T's plane, within Q of T) is then within
+// h0 + Q k[3] of w along a, and the ray point the box test stands for (within
+// D dl lf of X* along the ray) within a further D dl lf |a.d/|d||. So the ray
+// segment must meet that slab too: true when [t0, t1] (the box's interval)
+// meets it. q2 = 2Q, pt = 2 D dl lf (mt_pad's two parts of pad); on >= |o|_1.
+RTA_HD bool mt_slab(float ox, float oy, float oz, float on, const RayC& c, const float* k, const float* m,
+                    float q2, float pt, float t0, float t1) {
+    const float dn = std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz));
+    const float s0 = std::fma(k[0], ox, std::fma(k[1], oy, std::fma(k[2], oz, -m[4])));
+    const float hw = std::fma(q2, k[3], m[5]) + pt * std::fabs(dn) + 4.0f * kU24 * (on + std::fabs(m[4])) + 1e-6f;
+    const float iv = c.rdl / dn;  // 1 / (a.d): +-inf when parallel
+    const float ta = (-hw - s0) * iv, tb = (hw - s0) * iv;
+    const float lo = std::fmax(t0, std::fmin(ta, tb)), hi = std::fmin(t1, std::fmax(ta, tb));
+    return !(lo > hi + 1e-4f * std::fabs(hi) + 1e-6f);
 }
 
 }  // namespace rta

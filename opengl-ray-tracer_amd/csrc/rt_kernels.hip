@@ -572,6 +572,7 @@ struct AccelPtrs {
     int split_max;                      // lane_walk_any: split walks of waves with <= this many rays (0: off)
     int split_g;                        // ... over groups of at most this many lanes (a power of two)
     const int* __restrict__ prim_shape; // shape index per prim slot (the winner's material)
+    float mt_z[3];                      // AccelHost::mt_z (Moller-Trumbore per-ray padding)
 };
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
@@ -742,8 +743,11 @@ __device__ __forceinline__ bool first_active() {
 // bits 28-29 stay clear, so kTopLeaf and kItem are never set in a local code).
 __device__ __forceinline__ int top_code(int k, int ia) { return ia < 0 ? static_cast<int>(kTopLeaf | k) : k; }
 
-__device__ __forceinline__ rta::RayC ray_c(const Ray& r, float origin_lim) {
-    return rta::ray_consts(r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, origin_lim);
+template <bool MT = false>
+__device__ __forceinline__ rta::RayC ray_c(const Ray& r, const AccelPtrs& A) {
+    rta::RayC c = rta::ray_consts(r.o.x, r.o.y, r.o.z, r.d.x, r.d.y, r.d.z, A.origin_lim);
+    if (MT) rta::mt_ray(c, r.o.x, r.o.y, r.o.z, A.mt_z);
+    return c;
 }
 
 __device__ __forceinline__ bool box_enter(const rta::RayC& c, float4 lo, float4 hi, float tl, float& te) {
@@ -921,28 +925,59 @@ __device__ __forceinline__ void wide_pair_q(const rta::RayC& c, float tl, f2 lx,
     h1 = (tn[1] <= tf[1]) & !rta::cone_culls_q(w1, c.dq);
 }
 
-// Wide-node record stride in float4: 8 (quantized cones), 11 for the
-// Moller-Trumbore accelerator's float grazing cones.
-constexpr int kWideRec = 8, kWideRecMt = 11;
+// Wide-node record stride in float4: 8 (quantized cones), 17 for the
+// Moller-Trumbore accelerator: boxes (6), float grazing cones (4: axis, s),
+// the per-ray padding constants (6, accel.h AccelHost::lmt) and the codes.
+constexpr int kWideRec = 8, kWideRecMt = 17;
+
+// Float `comp` of child `sl`'s box (0-2 lo.xyz, 3-5 hi.xyz) in wide record w:
+// row comp, lane sl of the SoA records; float comp of the child's 16-float
+// block in the MT records (wide_kids).
+__host__ __device__ __forceinline__ float* wide_box_f(float4* lnodes, int rec, int w, int sl, int comp) {
+    float* base = reinterpret_cast<float*>(lnodes + rec * static_cast<size_t>(w));
+    return rec == kWideRecMt ? base + 16 * sl + comp : base + 4 * comp + sl;
+}
 
 template <bool MT = false>
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
     const float4* q = A.lnodes + (MT ? kWideRecMt : kWideRec) * static_cast<size_t>(uc & 0x3fffffffu);
-    const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
     float t[4];
     bool h[4];
     int cc[4];
     if (MT) {
-        const float4 ax = q[6], ay = q[7], az = q[8], th = q[9], cd = q[10];
+        // per-ray padding (accel_math.h mt_pad / mt_slab; accel_bound.h): each
+        // child's static box grown by its pad, the distance limit by lf, then the
+        // slab along its cone axis; a child without a finite bound is entered at 0.
+        // Record: per child 4 float4 (lo.xyz hi.x | hi.yz axis.xy | axis.z s m0 m1 |
+        // m2 m3 m4 m5), then the codes; one child per iteration keeps the other
+        // children's loads out of the registers.
+        const float4 cd = q[16];
+        t[0] = t[1] = t[2] = t[3] = 0.0f;
+        h[0] = h[1] = h[2] = h[3] = false;
         cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
         cc[3] = __float_as_int(cd.w);
-        wide_pair<MT>(c, tl, (f2){lx.x, lx.y}, (f2){ly.x, ly.y}, (f2){lz.x, lz.y}, (f2){hx.x, hx.y},
-                      (f2){hy.x, hy.y}, (f2){hz.x, hz.y}, (f2){ax.x, ax.y}, (f2){ay.x, ay.y}, (f2){az.x, az.y},
-                      (f2){th.x, th.y}, t[0], t[1], h[0], h[1]);
-        wide_pair<MT>(c, tl, (f2){lx.z, lx.w}, (f2){ly.z, ly.w}, (f2){lz.z, lz.w}, (f2){hx.z, hx.w},
-                      (f2){hy.z, hy.w}, (f2){hz.z, hz.w}, (f2){ax.z, ax.w}, (f2){ay.z, ay.w}, (f2){az.z, az.w},
-                      (f2){th.z, th.w}, t[2], t[3], h[2], h[3]);
+#pragma unroll 1
+        for (int s2 = 0; s2 < 4; ++s2) {
+            const float4 f0 = q[4 * s2], f1 = q[4 * s2 + 1], f2v = q[4 * s2 + 2], f3 = q[4 * s2 + 3];
+            const float k[4] = {f1.z, f1.w, f2v.x, f2v.y};
+            const float m[6] = {f2v.z, f2v.w, f3.x, f3.y, f3.z, f3.w};
+            float pad, lf, q2, pt, tt = 0.0f;
+            bool hh = true;
+            if (rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt)) {
+                float tn, tf;
+                hh = rta::box_span(c, f0.x - pad, f0.y - pad, f0.z - pad, f0.w + pad, f1.x + pad, f1.y + pad,
+                                   tl * lf, tn, tf);
+                if (hh && c.ix != 0.0f) hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
+                tt = tn / lf * 0.99999f;  // the stack's prune compares with tl, not tl * lf
+            }
+            // select-written (a lane-varying index would put t / h in scratch)
+            t[0] = s2 == 0 ? tt : t[0], t[1] = s2 == 1 ? tt : t[1], t[2] = s2 == 2 ? tt : t[2];
+            t[3] = s2 == 3 ? tt : t[3];
+            h[0] = s2 == 0 ? hh : h[0], h[1] = s2 == 1 ? hh : h[1], h[2] = s2 == 2 ? hh : h[2];
+            h[3] = s2 == 3 ? hh : h[3];
+        }
     } else {
+        const float4 lx = q[0], ly = q[1], lz = q[2], hx = q[3], hy = q[4], hz = q[5];
         const float4 cw = q[6], cd = q[7];
         cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
         cc[3] = __float_as_int(cd.w);
@@ -1022,7 +1057,7 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
     if (A.N <= 0 || !active) return;
     const V inv = inv_dir(r.d);
     const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
-    const rta::RayC c = ray_c(r, A.origin_lim);
+    const rta::RayC c = ray_c<MT>(r, A);
     float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
     // sp: the stack top as an element offset (entries x stride), so a push or pop
     // adds or subtracts stride instead of multiplying (v_mul_lo_u32 is quarter rate)
@@ -1339,7 +1374,7 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
     if (A.N <= 0 || m == 0) return;
     const V inv = inv_dir(r.d);
     const bool fast = A.boxes_finite && aabb_fast_ok(r.o, inv);
-    const rta::RayC c = ray_c(r, A.origin_lim);
+    const rta::RayC c = ray_c<MT>(r, A);
     float tl = rta::t_limit(SHADOW ? lim_shadow : b.d, c.rdl);
     WaveStack st{0, 0, 0, 0};
     int cur = 0;
@@ -2016,7 +2051,7 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
         for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
             const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
             if (o.mt)
-                reinterpret_cast<float*>(o.lnodes + kWideRecMt * static_cast<size_t>(w) + 9)[sl] = -4.f;
+                wide_box_f(o.lnodes, kWideRecMt, w, sl, 0)[9] = 2.f;  // s: a full cone (mt_pad's floor)
             else  // never cull
                 reinterpret_cast<int*>(o.lnodes + kWideRec * static_cast<size_t>(w) + 6)[sl] = rta::kConeNever;
         }
@@ -2097,7 +2132,7 @@ __global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ di
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
         const int w = d.x >> 2, sl = d.x & 3;
         const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
-        reinterpret_cast<float*>(lnodes + rec * static_cast<size_t>(w) + lane)[sl] = v;
+        *wide_box_f(lnodes, rec, w, sl, lane) = v;
     }
 }
 
@@ -2108,7 +2143,7 @@ __global__ void k_inf_slots(const int* __restrict__ slots, int n, float4* __rest
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int w = slots[i] >> 2, sl = slots[i] & 3;
-    for (int r = 0; r < 6; ++r) reinterpret_cast<float*>(lnodes + rec * static_cast<size_t>(w) + r)[sl] = r < 3 ? -INFINITY : INFINITY;
+    for (int r = 0; r < 6; ++r) *wide_box_f(lnodes, rec, w, sl, r) = r < 3 ? -INFINITY : INFINITY;
 }
 
 // The scene-tree items' exact boxes (titems) from the grown reference leaves.
@@ -2436,11 +2471,11 @@ int build_upload_accel(rt_ctx* c) {
     auto emit_wide = [&](size_t w, size_t at, const std::vector<int>& wchild, const std::vector<int>& wsub,
                          const std::vector<rta::Box3>& boxes, const std::vector<float>& cones,
                          const std::function<int(int)>& leaf_of, size_t sub_base) {
-        float v[11][4];
+        float v[kWideRecMt][4];
         for (int s2 = 0; s2 < 4; ++s2) {
             const int j = wchild[rta::kWide * w + s2];
             int code = kNoChild;
-            float box[6] = {0, 0, 0, 0, 0, 0}, cone[4] = {0, 0, 0, -4.f};
+            float box[6] = {0, 0, 0, 0, 0, 0}, cone[4] = {0, 0, 0, -4.f}, mtc[rta::kMtPadF] = {0, 0, 0, 0, 0, 0};
             if (j >= 0) {
                 const rta::Box3& bx = boxes[j];
                 for (int a = 0; a < 3; ++a) {
@@ -2448,14 +2483,19 @@ int build_upload_accel(rt_ctx* c) {
                     box[3 + a] = bx.hi[a];
                 }
                 for (int a = 0; a < 4; ++a) cone[a] = cones[4 * j + a];
-                if (!c->cone_cull && cone[3] > rta::kNoPrune) cone[3] = -4.f;
+                if (!c->cone_cull && cone[3] > rta::kNoPrune) cone[3] = A.mt ? 2.f : -4.f;
+                if (A.mt && boxes.data() == A.lbox.data())
+                    for (int a = 0; a < rta::kMtPadF; ++a) mtc[a] = A.lmt[rta::kMtPadF * j + a];
                 const int sub = wsub[rta::kWide * w + s2];
                 code = sub < 0 ? leaf_of(j) : static_cast<int>(kLocal | static_cast<unsigned>(sub_base + sub));
             }
-            for (int a = 0; a < 6; ++a) v[a][s2] = box[a];
-            if (A.mt) {
-                for (int a = 0; a < 4; ++a) v[6 + a][s2] = cone[a];
+            if (A.mt) {  // per child 16 floats: box, cone, the per-ray padding constants
+                float* blk = &v[0][0] + 16 * s2;
+                for (int a = 0; a < 6; ++a) blk[a] = box[a];
+                for (int a = 0; a < 4; ++a) blk[6 + a] = cone[a];
+                for (int a = 0; a < rta::kMtPadF; ++a) blk[10 + a] = mtc[a];
             } else {
+                for (int a = 0; a < 6; ++a) v[a][s2] = box[a];
                 v[6][s2] = bits_f(j < 0 ? rta::kConeNever : rta::cone_word(cone[0], cone[1], cone[2], cone[3]));
             }
             v[rec - 1][s2] = bits_f(code);
@@ -3169,7 +3209,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
 
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
-                          c->boxes_finite, c->split_max, c->split_g, c->prim_idx_dev};
+                          c->boxes_finite, c->split_max, c->split_g, c->prim_idx_dev,
+                          {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}};
         // compaction: bounces >= tail_from of the rays still alive run in k_accel_tail
         k2.tail_queue = nullptr;
         // RT_TAIL_AUTO: from bounce 2 on scenes of many scene-tree items (measured: config 5's

@@ -29,6 +29,8 @@ V fv(rt_vec3 v) { return {v.x, v.y, v.z}; }
 struct Best { float d; int seq; V p; int shape; };
 
 bool g_mt = false;  // Moller-Trumbore triangles (out_info[6] = 1)
+const bool g_slab = std::getenv("ACNOSLAB") == nullptr;
+constexpr int kMtF = rta::kMtPadF;
 
 // INNER hit of a shape, GLSL semantics (barycentric, or Moller-Trumbore when g_mt), or false.
 bool isect(const FlatShape& s, V o, V d, V& p) {
@@ -129,12 +131,14 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         nodes[k].boundsMax.y, nodes[k].boundsMax.z})
             if (std::isnan(v)) boxes_finite = false;
     constexpr int kSceneBase = 1 << 29;
-    long long tests = 0, scene_rays = 0;
+    long long tests = 0, scene_rays = 0, pops = 0, forced = 0;
     for (int r = 0; r < R; ++r) {
         long long nodes_before = 0;
         V ro = mk(o[3 * r], o[3 * r + 1], o[3 * r + 2]), rd = mk(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
         V inv = mk(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
         const rta::RayC rc = rta::ray_consts(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, A.origin_lim);
+        const float so = rta::mt_origin_dist(ro.x, ro.y, ro.z, A.mt_z);
+        const float on = std::fabs(ro.x) + std::fabs(ro.y) + std::fabs(ro.z);
         for (int pass = 0; pass < 2; ++pass) {
             const bool shadow = pass == 1;
             Best b{1e20f, 0x7fffffff, mk(0, 0, 0), -1};
@@ -170,6 +174,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                 };
                 if (std::getenv("ACDBG")) std::printf("pop %d lim %g best %d %g\n", code, l, b.shape, b.d);
                 ++nodes_before;
+                ++pops;
                 if (code <= -kSceneBase) {
                     // scene-tree wide node: padded boxes and cones; an item tests its
                     // reference leaf's exact box before its shapes
@@ -215,7 +220,25 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         if (j < 0) continue;
                         const float* k = &A.lcone[4 * j];
                         if (g_mt) {
+#if RTA_MT_RAYPAD
+                            float pad, lf, q2, pt;
+                            if (rta::mt_pad(rc, so, k, &A.lmt[kMtF * j], pad, lf, q2, pt)) {
+                                rta::Box3 b = A.lbox[j];
+                                for (int a = 0; a < 3; ++a) {
+                                    b.lo[a] -= pad;
+                                    b.hi[a] += pad;
+                                }
+                                float tn, tf;
+                                if (!rta::box_span(rc, b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2],
+                                                   rta::t_limit(l * lf, rc.rdl), tn, tf))
+                                    continue;
+                                if (g_slab && rc.ix != 0.0f && !rta::mt_slab(ro.x, ro.y, ro.z, on, rc, k, &A.lmt[kMtF * j], q2, pt, tn, tf)) continue;
+                            } else {
+                                ++forced;
+                            }
+#else
                             if (!grazing(rc, k) && !padded(rc, A.lbox[j], l)) continue;
+#endif
                         } else {
                             if (!padded(rc, A.lbox[j], l)) continue;
                             if (rta::cone_culls_q(rta::cone_word(k[0], k[1], k[2], k[3]), rc.dq)) continue;  // the device's quantized cone
@@ -231,6 +254,8 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
         }
     }
     out_info[4] = static_cast<int>(tests / (R > 0 ? R : 1));
+    out_info[5] = static_cast<int>(pops / (R > 0 ? R : 1));
+    if (std::getenv("ACSTAT")) std::printf("pops/ray %.1f forced/ray %.2f tests/ray %.1f\n", double(pops) / R, double(forced) / R, double(tests) / R);
     out_info[9] = A.st.wroot >= 0 ? 1 : 0;
     out_info[10] = static_cast<int>(scene_rays);
     out_info[11] = A.st.nested;

@@ -29,4 +29,4 @@ keys = ["VGPRs", "AGPRs", "SGPRs", "ScratchSize [bytes/lane]", "VGPRs Spill", "S
         "Occupancy [waves/SIMD]", "LDS Size [bytes/block]"]
 print("%-34s" % "kernel" + "".join("%9s" % k.split(" ")[0][:8] for k in keys))
 for r in rows:
-    print("%-34s" % r["name"][:34] + "".join("%9s" % r.get(k, "-") for k in keys))
+    print("%-34s" % (r["name"] if "-full" in sys.argv[0:1] or __import__("os").environ.get("FULL") else r["name"][:34]) + "".join("%9s" % r.get(k, "-") for k in keys))
