@@ -43,6 +43,7 @@ struct RayC {
     // Moller-Trumbore walks only (mt_ray; dead, so free, in the other instances)
     float mox, moy, moz;  // the origin
     float so, on;         // |o - Z| rounded up (mt_origin_dist), |o|_1
+    float dlen;           // |d| rounded up
 };
 
 // Quantized back-face cones (the barycentric accelerator's wide nodes,
@@ -166,6 +167,17 @@ RTA_HD void mt_ray(RayC& c, float ox, float oy, float oz, const float* z) {
     c.moz = oz;
     c.so = mt_origin_dist(ox, oy, oz, z);
     c.on = std::fabs(ox) + std::fabs(oy) + std::fabs(oz);
+    c.dlen = 1.0001f / c.rdl;
+}
+
+// 1/x within 1 ulp (v_rcp_f32 on the device); every use below carries a
+// relative margin of 1e-4 or more, so the rounding does not matter.
+RTA_HD float rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
 }
 
 // Moller-Trumbore per-ray padding (accel_bound.h, the derivation above
@@ -177,16 +189,16 @@ RTA_HD void mt_ray(RayC& c, float ox, float oy, float oz, const float* z) {
 constexpr int kMtPadF = 6;  // floats per local node in AccelHost::lmt
 RTA_HD bool mt_pad(const RayC& c, float so, const float* k, const float* m, float& pad, float& lf, float& q2,
                    float& pt) {
-    const float D = 1.0001f / c.rdl;  // |d| (rounded up)
+    const float D = c.dlen;
     const float cn = std::fabs(std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz))) - k[3];
     const float A = std::fmax(1e-5f, D * std::fmax(cn, 0.0f) * m[0]) - 7.0f * D * m[1];
     if (!(A > 2.5e-6f)) return false;
-    const float ia = 1.0001f / A;
+    const float ia = 1.0001f * rcp(A);
     const float r = 7.07f * D * m[1] * ia + 3.0f * kU24;
     if (!(r < 0.5f)) return false;
     const float q = D * m[1] * std::fma(18.0f, so, m[3]) * ia;
     const float dl = 9.09f * m[1] * (so + m[2]) * ia;
-    lf = 1.0001f / (1.0f - r);
+    lf = 1.0001f * rcp(1.0f - r);
     q2 = 2.0f * q;
     pt = 2.0f * D * dl * lf;
     pad = q2 + pt;
@@ -205,7 +217,7 @@ RTA_HD bool mt_slab(float ox, float oy, float oz, float on, const RayC& c, const
     const float dn = std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz));
     const float s0 = std::fma(k[0], ox, std::fma(k[1], oy, std::fma(k[2], oz, -m[4])));
     const float hw = std::fma(q2, k[3], m[5]) + pt * std::fabs(dn) + 4.0f * kU24 * (on + std::fabs(m[4])) + 1e-6f;
-    const float iv = c.rdl / dn;  // 1 / (a.d): +-inf when parallel
+    const float iv = c.rdl * rcp(dn);  // 1 / (a.d): +-inf when parallel
     const float ta = (-hw - s0) * iv, tb = (hw - s0) * iv;
     const float lo = std::fmax(t0, std::fmin(ta, tb)), hi = std::fmin(t1, std::fmax(ta, tb));
     return !(lo > hi + 1e-4f * std::fabs(hi) + 1e-6f);

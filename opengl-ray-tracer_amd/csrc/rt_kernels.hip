@@ -929,6 +929,10 @@ __device__ __forceinline__ void wide_pair_q(const rta::RayC& c, float tl, f2 lx,
 // Moller-Trumbore accelerator: boxes (6), float grazing cones (4: axis, s),
 // the per-ray padding constants (6, accel.h AccelHost::lmt) and the codes.
 constexpr int kWideRec = 8, kWideRecMt = 17;
+#ifndef RT_MT_UNROLL
+#define RT_MT_UNROLL 4  // MT wide_kids: children per unrolled step (r03j: 1 -> 4 car MT -15 %)
+#endif
+constexpr int kMtUnroll = RT_MT_UNROLL;
 
 // Float `comp` of child `sl`'s box (0-2 lo.xyz, 3-5 hi.xyz) in wide record w:
 // row comp, lane sl of the SoA records; float comp of the child's 16-float
@@ -949,14 +953,14 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
         // child's static box grown by its pad, the distance limit by lf, then the
         // slab along its cone axis; a child without a finite bound is entered at 0.
         // Record: per child 4 float4 (lo.xyz hi.x | hi.yz axis.xy | axis.z s m0 m1 |
-        // m2 m3 m4 m5), then the codes; one child per iteration keeps the other
-        // children's loads out of the registers.
+        // m2 m3 m4 m5), then the codes. Results select-written (kMtUnroll < 4 would
+        // index them by a loop variable).
         const float4 cd = q[16];
         t[0] = t[1] = t[2] = t[3] = 0.0f;
         h[0] = h[1] = h[2] = h[3] = false;
         cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
         cc[3] = __float_as_int(cd.w);
-#pragma unroll 1
+#pragma unroll kMtUnroll
         for (int s2 = 0; s2 < 4; ++s2) {
             const float4 f0 = q[4 * s2], f1 = q[4 * s2 + 1], f2v = q[4 * s2 + 2], f3 = q[4 * s2 + 3];
             const float k[4] = {f1.z, f1.w, f2v.x, f2v.y};
@@ -968,7 +972,7 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
                 hh = rta::box_span(c, f0.x - pad, f0.y - pad, f0.z - pad, f0.w + pad, f1.x + pad, f1.y + pad,
                                    tl * lf, tn, tf);
                 if (hh && c.ix != 0.0f) hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
-                tt = tn / lf * 0.99999f;  // the stack's prune compares with tl, not tl * lf
+                tt = tn * rta::rcp(lf) * 0.99999f;  // the stack's prune compares with tl, not tl * lf
             }
             // select-written (a lane-varying index would put t / h in scratch)
             t[0] = s2 == 0 ? tt : t[0], t[1] = s2 == 1 ? tt : t[1], t[2] = s2 == 2 ? tt : t[2];

@@ -136,9 +136,9 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
         long long nodes_before = 0;
         V ro = mk(o[3 * r], o[3 * r + 1], o[3 * r + 2]), rd = mk(d[3 * r], d[3 * r + 1], d[3 * r + 2]);
         V inv = mk(1.0f / rd.x, 1.0f / rd.y, 1.0f / rd.z);
-        const rta::RayC rc = rta::ray_consts(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, A.origin_lim);
-        const float so = rta::mt_origin_dist(ro.x, ro.y, ro.z, A.mt_z);
-        const float on = std::fabs(ro.x) + std::fabs(ro.y) + std::fabs(ro.z);
+        rta::RayC rc = rta::ray_consts(ro.x, ro.y, ro.z, rd.x, rd.y, rd.z, A.origin_lim);
+        rta::mt_ray(rc, ro.x, ro.y, ro.z, A.mt_z);  // the device's MT ray terms
+        const float so = rc.so, on = rc.on;
         for (int pass = 0; pass < 2; ++pass) {
             const bool shadow = pass == 1;
             Best b{1e20f, 0x7fffffff, mk(0, 0, 0), -1};
