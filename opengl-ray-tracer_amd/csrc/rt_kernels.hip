@@ -954,7 +954,8 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
         // slab along its cone axis; a child without a finite bound is entered at 0.
         // Record: per child 4 float4 (lo.xyz hi.x | hi.yz axis.xy | axis.z s m0 m1 |
         // m2 m3 m4 m5), then the codes. Results select-written (kMtUnroll < 4 would
-        // index them by a loop variable).
+        // index them by a loop variable). Pairs of children on packed f32
+        // instructions (as wide_pair) spilled 40-140 VGPRs in every MT instance (r03).
         const float4 cd = q[16];
         t[0] = t[1] = t[2] = t[3] = 0.0f;
         h[0] = h[1] = h[2] = h[3] = false;
@@ -971,7 +972,8 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
                 float tn, tf;
                 hh = rta::box_span(c, f0.x - pad, f0.y - pad, f0.z - pad, f0.w + pad, f1.x + pad, f1.y + pad,
                                    tl * lf, tn, tf);
-                if (hh && c.ix != 0.0f) hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
+                if (hh && c.ix != 0.0f && m[5] < 3e38f)
+                    hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
                 tt = tn * rta::rcp(lf) * 0.99999f;  // the stack's prune compares with tl, not tl * lf
             }
             // select-written (a lane-varying index would put t / h in scratch)

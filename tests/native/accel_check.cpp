@@ -131,6 +131,12 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         nodes[k].boundsMax.y, nodes[k].boundsMax.z})
             if (std::isnan(v)) boxes_finite = false;
     constexpr int kSceneBase = 1 << 29;
+    // ACSTAT: wide-node visits per depth below the local roots
+    std::vector<int> wdepth(A.wchild.size() / rta::kWide, 0);
+    for (size_t w = 0; w < wdepth.size(); ++w)
+        for (int s2 = 0; s2 < rta::kWide; ++s2)
+            if (A.wsub[rta::kWide * w + s2] >= 0) wdepth[A.wsub[rta::kWide * w + s2]] = wdepth[w] + 1;
+    long long per_depth[64] = {0}, forced_depth[64] = {0};
     long long tests = 0, scene_rays = 0, pops = 0, forced = 0;
     for (int r = 0; r < R; ++r) {
         long long nodes_before = 0;
@@ -215,6 +221,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     // wide local node (accel.h, build_wide): each child's padded
                     // box and back-face cone, tested at the wide node
                     const int w = -code - 1;
+                    ++per_depth[std::min(63, wdepth[w])];
                     for (int s2 = 0; s2 < rta::kWide; ++s2) {
                         const int j = A.wchild[rta::kWide * w + s2];
                         if (j < 0) continue;
@@ -232,9 +239,10 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                                 if (!rta::box_span(rc, b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2],
                                                    rta::t_limit(l * lf, rc.rdl), tn, tf))
                                     continue;
-                                if (g_slab && rc.ix != 0.0f && !rta::mt_slab(ro.x, ro.y, ro.z, on, rc, k, &A.lmt[kMtF * j], q2, pt, tn, tf)) continue;
+                                if (g_slab && rc.ix != 0.0f && A.lmt[kMtF * j + 5] < 3e38f && !rta::mt_slab(ro.x, ro.y, ro.z, on, rc, k, &A.lmt[kMtF * j], q2, pt, tn, tf)) continue;
                             } else {
                                 ++forced;
+                                ++forced_depth[std::min(63, wdepth[w])];
                             }
 #else
                             if (!grazing(rc, k) && !padded(rc, A.lbox[j], l)) continue;
@@ -255,6 +263,9 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
     }
     out_info[4] = static_cast<int>(tests / (R > 0 ? R : 1));
     out_info[5] = static_cast<int>(pops / (R > 0 ? R : 1));
+    if (std::getenv("ACSTAT"))
+        for (int k = 0; k < 64; ++k)
+            if (per_depth[k]) std::printf("depth %d: %.2f visits/ray %.2f forced\n", k, double(per_depth[k]) / R, double(forced_depth[k]) / R);
     if (std::getenv("ACSTAT")) std::printf("pops/ray %.1f forced/ray %.2f tests/ray %.1f\n", double(pops) / R, double(forced) / R, double(tests) / R);
     out_info[9] = A.st.wroot >= 0 ? 1 : 0;
     out_info[10] = static_cast<int>(scene_rays);
