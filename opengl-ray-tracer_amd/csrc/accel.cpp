@@ -46,7 +46,10 @@ struct Item {
 // MT triangles with |e1||e2| above this are kept apart from the rest at the
 // first split of a local tree (mt_pad takes a node's worst |e1||e2| with its
 // smallest |e1 x e2|, so mixing them would leave every ancestor unbounded).
-constexpr double kMtBigX = 4.0;
+#ifndef RTA_MT_BIG_X
+#define RTA_MT_BIG_X 4.0
+#endif
+constexpr double kMtBigX = RTA_MT_BIG_X;
 
 
 // MT builds (AccelHost::mt): the orientation-free normal cone of the items a
