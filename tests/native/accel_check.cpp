@@ -31,6 +31,7 @@ struct Best { float d; int seq; V p; int shape; };
 bool g_mt = false;  // Moller-Trumbore triangles (out_info[6] = 1)
 const bool g_slab = std::getenv("ACNOSLAB") == nullptr;
 constexpr int kMtF = rta::kMtPadF;
+float g_pad_scale = 1.0f;  // out_info[7] == 777: the MT per-ray padding switched off (the test's teeth)
 
 // INNER hit of a shape, GLSL semantics (barycentric, or Moller-Trumbore when g_mt), or false.
 bool isect(const FlatShape& s, V o, V d, V& p) {
@@ -119,6 +120,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                 int* out_shadow, int* out_info) {
     rta::AccelHost A;
     g_mt = out_info[6] != 0;
+    g_pad_scale = out_info[7] == 777 ? 0.0f : 1.0f;
     if (!rta::build_accel(shapes, S, nodes, N, idx, I, 8, 64, A, g_mt)) return -1;
     out_info[0] = static_cast<int>(A.lbox.size());
     out_info[1] = A.always_prims;
@@ -230,6 +232,10 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
 #if RTA_MT_RAYPAD
                             float pad, lf, q2, pt;
                             if (rta::mt_pad(rc, so, k, &A.lmt[kMtF * j], pad, lf, q2, pt)) {
+                                if (g_pad_scale != 1.0f) {  // mutation check only (out_info[7] = 777)
+                                    pad *= g_pad_scale, q2 *= g_pad_scale, pt *= g_pad_scale;
+                                    lf = 1.0f;
+                                }
                                 rta::Box3 b = A.lbox[j];
                                 for (int a = 0; a < 3; ++a) {
                                     b.lo[a] -= pad;

@@ -43,7 +43,7 @@ def _p(a):
     return C.c_void_p(a.ctypes.data) if a.size else None
 
 
-def compare(lib, fs, o, d, lim, tree=1, mt=0):
+def compare(lib, fs, o, d, lim, tree=1, mt=0, mutate=False):
     fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)  # enforce record layout
     R = len(o)
     o = np.ascontiguousarray(o, np.float32)
@@ -54,6 +54,14 @@ def compare(lib, fs, o, d, lim, tree=1, mt=0):
     info = np.zeros(12, np.int32)
     info[8] = tree
     info[6] = mt
+    if mutate:  # accel_check without the MT per-ray padding: return the mismatch count
+        info[7] = 777
+        assert lib.accel_check(*[_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes), _p(fs.indices),
+                                 len(fs.indices), _p(o), _p(d), _p(lim), R], *[_p(x) for x in outs], _p(info)) == 0
+        assert oracle.lib().orc_trace_rays_mt(_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes),
+                                              _p(fs.indices), len(fs.indices), _p(o), _p(d), _p(lim), R,
+                                              *[_p(x) for x in refs], mt) == 0
+        return int((outs[0] != refs[0]).sum() + (outs[2] != refs[2]).sum())
     args = [_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes), _p(fs.indices), len(fs.indices),
             _p(o), _p(d), _p(lim), R]
     assert lib.accel_check(*args, *[_p(x) for x in outs], _p(info)) == 0
@@ -459,3 +467,111 @@ def test_quantized_cones_conservative():
     r = subprocess.run([os.path.join(ROOT, "tests", "native", "build", "cone_check")], capture_output=True,
                        text=True, timeout=120)
     assert r.returncode == 0 and "cone_check ok" in r.stdout, r.stdout + r.stderr
+
+
+def _mt_stress_scene(seed):
+    """Triangles the per-ray MT padding (accel_math.h mt_pad) is most exposed to:
+    sizes from 1e-3 to 30 units (|e1||e2| on both sides of the big-triangle split,
+    kMtBigX), needles, nearly coplanar sheets (thin slabs, mt_slab) and spheres in
+    the same leaves; one leaf, so the whole scene sits under one local BVH."""
+    rng = np.random.default_rng(seed)
+    sc = rtamd.Scene()
+    for i in range(700):
+        c = rng.uniform(-15, 15, 3)
+        s = 10 ** rng.uniform(-3, 1.5)
+        v = c + rng.normal(size=(3, 3)) * s
+        if i % 7 == 0:  # needle
+            v[2] = v[0] + (v[1] - v[0]) * 0.5 + rng.normal(size=3) * s * 1e-3
+        sc.add_triangle(v[0], v[1], v[2])
+    for k in range(4):  # sheets: many small triangles in (almost) one plane
+        n = rng.normal(size=3)
+        n /= np.linalg.norm(n)
+        a = np.cross(n, rng.normal(size=3))
+        a /= np.linalg.norm(a)
+        b = np.cross(n, a)
+        o = rng.uniform(-10, 10, 3)
+        for i in range(150):
+            p = o + a * rng.uniform(-8, 8) + b * rng.uniform(-8, 8)
+            q = [p + a * rng.uniform(-.5, .5) + b * rng.uniform(-.5, .5) + n * rng.normal() * 1e-4 for _ in range(2)]
+            sc.add_triangle(p, q[0], q[1])
+    for i in range(20):
+        sc.add_sphere(rng.uniform(-15, 15, 3), rng.uniform(0.2, 2.0))
+    sc.set_camera((0, -10, 60), 60, 16 / 9)
+    sc.LookAt((0, 0, 0))
+    sc.set_light((10, -30, 20), (1, 1, 1), 40)
+    sc.buildBVH(1)
+    return sc.serializeScene()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_mt_per_ray_padding_adversarial(check_lib, seed):
+    """The per-ray MT padding (r03) on a scene built to stress it: grazing rays
+    with |cos| from 1e-7 to 1e-1 to random triangles, from origins 1 to 300 units
+    away (the pad grows with |o - Z|), rays in the sheets' planes, and camera
+    rays. The accelerated walk must pick the reference MT walk's shape and
+    shadow answer for every one (tests/native/accel_check.cpp vs the oracle)."""
+    fs = _mt_stress_scene(seed)
+    rng = np.random.default_rng(seed)
+    idx = np.where(fs.shapes["type"] == 3)[0]
+    o, d = [], []
+    for _ in range(3000):
+        tri = fs.shapes[idx[rng.integers(len(idx))]]
+        p = [tri[k].astype(np.float64) for k in ("triP1", "triP2", "triP3")]
+        n = np.cross(p[1] - p[0], p[2] - p[0])
+        ln = np.linalg.norm(n)
+        if not ln > 0:
+            continue
+        n /= ln
+        x = rng.dirichlet([1, 1, 1]) @ np.stack(p) + rng.normal(size=3) * 10 ** rng.uniform(-4, 0)
+        t = np.cross(n, rng.normal(size=3))
+        v = t / np.linalg.norm(t) + rng.choice([1, -1]) * 10 ** rng.uniform(-7, -1) * n
+        v /= np.linalg.norm(v)
+        o.append(x - v * 10 ** rng.uniform(0, 2.5))
+        d.append(v)
+    co, cd = camera_rays(fs, 48, 27)
+    O = np.concatenate([np.array(o), co])
+    D = np.concatenate([np.array(d), cd])
+    compare(check_lib, fs, O, D, rng.uniform(0.5, 400, len(O)), 1, mt=1)
+
+
+def test_mt_per_ray_padding_has_teeth(check_lib):
+    """Rays aimed just outside a triangle's edge (in its plane, 1e-2 to 3 edge
+    lengths out), grazing it (|cos| 1e-7 to 1e-4) from 60-130 units away: the
+    reference MT test still accepts ~5 % of them, with the hit beyond the
+    triangle's static box (accel_bound.h classify_mt_tight). The accelerated walk
+    must pick the reference's shape for all of them; with the per-ray padding
+    switched off in the emulator (mutation) it must not."""
+    rng = np.random.default_rng(3)
+    sc = rtamd.Scene()
+    for _ in range(300):  # sparse: the stray is usually the only hit
+        c = rng.uniform(-40, 40, 3)
+        v = c + rng.normal(size=(3, 3)) * 10 ** rng.uniform(-1, 0.7)
+        sc.add_triangle(v[0], v[1], v[2])
+    sc.set_camera((0, -10, 60), 60, 16 / 9)
+    sc.LookAt((0, 0, 0))
+    sc.set_light((10, -30, 20), (1, 1, 1), 40)
+    sc.buildBVH(1)
+    fs = sc.serializeScene()
+    idx = np.where(fs.shapes["type"] == 3)[0]
+    o, d = [], []
+    for _ in range(30000):
+        tri = fs.shapes[idx[rng.integers(len(idx))]]
+        p = [tri[k].astype(np.float64) for k in ("triP1", "triP2", "triP3")]
+        n = np.cross(p[1] - p[0], p[2] - p[0])
+        n /= np.linalg.norm(n)
+        e = rng.integers(3)
+        a, b, c3 = p[e], p[(e + 1) % 3], p[(e + 2) % 3]
+        m = a + (b - a) * rng.uniform(0, 1)
+        out = m - c3
+        out -= n * np.dot(out, n)
+        out /= np.linalg.norm(out)
+        x = m + out * 10 ** rng.uniform(-2, 0.5) * np.linalg.norm(b - a)
+        t = np.cross(n, rng.normal(size=3))
+        v = t / np.linalg.norm(t) + rng.choice([1, -1]) * 10 ** rng.uniform(-7, -4) * n
+        v /= np.linalg.norm(v)
+        o.append(x - v * rng.uniform(60, 130))
+        d.append(v)
+    O, D = np.array(o), np.array(d)
+    lim = np.full(len(O), 1e20)
+    compare(check_lib, fs, O, D, lim, 1, mt=1)
+    assert compare(check_lib, fs, O, D, lim, 1, mt=1, mutate=True) > 0
