@@ -435,6 +435,7 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         Box3 b;
         if (s.type != RT_TRIANGLE || classify_mt_tight(s, b, 0.0, tri[p]) != BOUNDED) continue;
         has[p] = 1;
+        if (tri[p].X > kMtBigX) continue;  // Z: the centre of the bulk, not of a large ground quad
         for (int a = 0; a < 3; ++a) {
             zlo[a] = std::min(zlo[a], tri[p].p1[a]);
             zhi[a] = std::max(zhi[a], tri[p].p1[a]);
