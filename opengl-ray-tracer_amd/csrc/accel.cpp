@@ -91,29 +91,23 @@ NCone normal_cone(const std::vector<Item>& items, int b, int e, F sel) {
 
 // MT: a normal split is taken while it costs less than kMtNormalBias times the
 // spatial one, and local leaves hold up to kMtLeaf prims. The cost model prices
-// grazing for uniformly spread directions; camera and reflection rays are not.
-// Measured on the car's MT frame (tools/abf.py --mt, profiles/r02zz3_abf_mt_*):
-// spatial splits only 16.7 ms; bias 1 / leaf 4: 14.4; bias 2 / leaf 4: 9.27 (leaf 2:
-// 10.7, leaf 1: 14.4); bias 4 / leaf 4: 9.17; bias 4 / leaf 6: 9.06 (kept); bias 8 /
-// leaf 6: 9.11; bias 4 / leaf 8: 9.43. Closest-hit tests per car camera ray
-// (tests/native/accel_check): 801 spatial only, 502 at bias 2 / leaf 4, 642 kept
-// (bigger leaves test more and visit fewer nodes, which is what costs on the GPU).
+// grazing for uniformly spread directions (kMtBuildPsi); camera and reflection
+// rays are not. Round 2 (forced grazing entry) measured bias 4 best against 1, 2
+// and 8 (profiles/r02zz3_abf_mt_*); round 3 (per-ray padding) re-measured leaves
+// of 2 against 1 and 4 (profiles/r03j_ab_mt_variants.txt), and the bias and
+// kMtBuildPsi as neutral in the CPU emulation (node steps per car camera ray).
 #ifndef RTA_MT_NORMAL_BIAS
 #define RTA_MT_NORMAL_BIAS 4.0
 #endif
 constexpr double kMtNormalBias = RTA_MT_NORMAL_BIAS;
 #ifndef RTA_MT_LEAF
-#if RTA_MT_RAYPAD
 #define RTA_MT_LEAF 2
-#else
-#define RTA_MT_LEAF 6
 #endif
-#endif
-constexpr int kMtLeaf = RTA_MT_LEAF;
+constexpr int kMtLeaf = RTA_MT_LEAF;  // MT local leaves hold at most this many prims
 #ifndef RTA_MT_BUILD_PSI
 #define RTA_MT_BUILD_PSI 0.032
 #endif
-constexpr double kMtBuildPsi = RTA_MT_BUILD_PSI;  // the cost model's grazing margin (asin(kMtCos) + 2 mrad)  // MT local leaves hold at most this many prims
+constexpr double kMtBuildPsi = RTA_MT_BUILD_PSI;  // the cost model's grazing margin (rad)
 
 struct LocalBuilder {
     AccelHost& out;
@@ -423,7 +417,6 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         done[j] = 1;
         return cones[j];
     };
-#if RTA_MT_RAYPAD
     // Per-ray padding (accel_bound.h, MtTri; accel_math.h mt_pad): the cone's
     // s = 2 sin(theta/2) bounds |n - axis| for every normal below, so
     // |cos(d, n)| >= |d . axis| - s; the node constants take the worst triangle.
@@ -529,18 +522,6 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         // sin > 0.3, or of nodes thicker along the axis than 1/4 of their box
         // raises the car's node steps per camera ray from 79 to 94)
     }
-#else
-    const double psi = std::asin(kMtCos);
-    for (size_t j = 0; j < M; ++j) {
-        const GCone& c = get(j);
-        float* o = &A.lcone[4 * j];
-        const double t = c.theta + psi + kConeMargin;
-        o[0] = static_cast<float>(c.a[0]);
-        o[1] = static_cast<float>(c.a[1]);
-        o[2] = static_cast<float>(c.a[2]);
-        o[3] = c.theta < 0 ? -1.f : (t >= 1.5707 ? 2.f : static_cast<float>(std::sin(t)));
-    }
-#endif
 }
 
 void build_cones(const FlatShape* shapes, AccelHost& A) {

@@ -93,12 +93,12 @@ struct AccelHost {
     // its cones are in st_cone (4 per binary node, as lcone).
     SceneTree st;
     std::vector<float> st_cone;
-    // Built for the Moller-Trumbore triangle test (build_accel mt): triangle boxes
-    // from classify_mt_triangle, no back-face culling, and the cones of lcone /
-    // st_cone are GRAZING cones: a ray with |dot(axis, d/|d|)| < thr might meet a
-    // triangle below at |cos| < kMtCos, where its box does not hold, so the walk
-    // enters the subtree whatever its box says (thr = -1: no triangle below, 2:
-    // any ray). Reference-node content boxes are not used (flags bit 3 clear).
+    // Built for the Moller-Trumbore triangle test (build_accel mt): static triangle
+    // boxes (classify_mt_tight), grown per ray by the MT error bound (lmt below,
+    // accel_math.h mt_pad / mt_slab); no back-face culling, and the cones of lcone
+    // are GRAZING cones: axis and s = 2 sin(psi/2) over the triangle normals below,
+    // either orientation (s = 2: any direction). Reference-node content boxes are
+    // not used (flags bit 3 clear) and no scene tree is built.
     bool mt = false;
     // MT per-ray padding (accel_bound.h, mt_pad): per local node the worst-case
     // triangle constants below it, kMtPadF floats each (MtPad order), and the

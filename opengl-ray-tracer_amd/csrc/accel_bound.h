@@ -44,20 +44,11 @@ constexpr double kCosRef = 0.5;      // below it the padding scales with 1/cos
 constexpr double kSphereErr = 4e-6;  // k of the sphere-root error above, with room
 constexpr double kOriginRel = 4.0;   // origin_lim = kOriginRel * (scene magnitude + 1)
 constexpr double kOriginErr = 4e-6;  // padding per unit of origin_lim (origin-relative error above)
-// Moller-Trumbore bounds (classify with mt): they hold for rays whose direction
-// makes |cos| >= kMtCos with the triangle's normal; the walk enters every
-// subtree holding a triangle such a ray might graze (accel.h, the MT cones).
-#ifndef RTA_MT_COS
-#define RTA_MT_COS 0.03
-#endif
+// Origin bound of an MT accelerator (in place of kOriginRel): rays from farther
+// take the always-enter mode and a camera beyond it renders the frame on k_packet.
 #ifndef RTA_MT_ORIGIN_REL
 #define RTA_MT_ORIGIN_REL 3.0
 #endif
-constexpr double kMtCos = RTA_MT_COS;
-constexpr double kMtSafety = 2.0;
-// Origin bound of an MT accelerator (in place of kOriginRel): the error of the
-// MT hit point grows with |o - p1|; rays from farther take the always-enter
-// mode and a camera beyond it renders the frame on k_packet.
 constexpr double kOriginRelMt = RTA_MT_ORIGIN_REL;
 constexpr double kU = 5.9604644775390625e-08;  // 2^-24
 
@@ -122,54 +113,15 @@ RTA_HD Box3 finish(const BoxAcc& acc, double origin_lim, double amp = 1.0) {
     return acc.padded(amp * (kPadRel * (acc.extent() + acc.mag() + 1.0) + kOriginErr * origin_lim) + 1e-6);
 }
 
-// The Moller-Trumbore test (gpu_shader.comp:170-195) accepts a hit when
+// Moller-Trumbore (gpu_shader.comp:170-195) accepts a hit when
 // |a| = |e1 . (d x e2)| >= 1e-5, an absolute threshold, and reports o + t d with
-// t, u, v each computed through f = 1/a. With |d| in [0.5, 2] (the padded
-// walk's range, accel_math.h), |o_i| <= L = origin_lim, s = o - p1 and
-// u = 2^-24 (first-order float error bounds of the dot and cross products):
-//   |da|  <= 7u D |e1||e2|                       (a, D = max |d| = 2)
-//   eps_u <= (9u D |s| |e2| + 1.5 * 7u D |e1||e2|) / A,  eps_v likewise with |e1|
-//   |t - t*| <= ((9 |s| + 7 D T) u |e1||e2|) / A + 2u T
-// where A = |a| - |da| and T bounds t*. The exact hit X* = p1 + u* e1 + v* e2
-// then lies within eps_u |e1| + eps_v |e2| of the triangle and the reported
-// point within D |t - t*| + 2u(|o| + D T) of X*. For grazing rays A can be as
-// small as 1e-5 and the stray reaches a triangle-size (measured: 0.5 units on
-// the car's half-unit triangles, tests/test_accel_cpu.py); the bound is
-// therefore taken for |cos(d, n)| >= kMtCos, A >= 0.5 |e1 x e2| kMtCos, and the
-// walk enters every subtree such a ray might graze regardless of its box.
-RTA_HD int classify_mt_triangle(const FlatShape& s, Box3& out, double origin_lim) {
-    const float e1f[3] = {s.triP2.x - s.triP1.x, s.triP2.y - s.triP1.y, s.triP2.z - s.triP1.z};
-    const float e2f[3] = {s.triP3.x - s.triP1.x, s.triP3.y - s.triP1.y, s.triP3.z - s.triP1.z};
-    const D3 p1 = d3(s.triP1), e1{e1f[0], e1f[1], e1f[2]}, e2{e2f[0], e2f[1], e2f[2]};
-    if (!finite3(p1) || !finite3(e1) || !finite3(e2)) return UNBOUNDED;
-    const double E1 = sqrt(dot(e1, e1)), E2 = sqrt(dot(e2, e2)), cr = sqrt(dot(cross(e1, e2), cross(e1, e2)));
-    if (!(cr > 0) || !isfinite(cr)) return UNBOUNDED;
-    const double D = 2.0;
-    const double A = fmax(1e-5, 0.5 * cr * kMtCos) - 7 * kU * D * E1 * E2;
-    if (!(A > 0.5e-5)) return UNBOUNDED;
-    const double Sm = sqrt(3.0) * origin_lim + sqrt(dot(p1, p1));
-    const double eu = (9 * kU * D * Sm * E2 + 1.5 * 7 * kU * D * E1 * E2) / A;
-    const double ev = (9 * kU * D * Sm * E1 + 1.5 * 7 * kU * D * E1 * E2) / A;
-    if (!(eu < 0.5 && ev < 0.5)) return UNBOUNDED;
-    const double T = 2.0 * (Sm + (1 + eu) * E1 + (1 + ev) * E2);
-    const double dt = 1.01 * ((9 * Sm + 7 * D * T) * kU * E1 * E2 / A + 2 * kU * T);
-    const double pad = kMtSafety * (eu * E1 + ev * E2 + D * dt + 2 * kU * (sqrt(3.0) * origin_lim + D * (T + dt)));
-    if (!isfinite(pad) || pad > 1e3 * (E1 + E2 + 1.0)) return UNBOUNDED;
-    BoxAcc acc;
-    acc.add(p1);
-    acc.add(p1 + e1);
-    acc.add(p1 + e2);
-    out = finish(acc, origin_lim);
-    for (int i = 0; i < 3; ++i) {
-        out.lo[i] = nextafterf(static_cast<float>(static_cast<double>(out.lo[i]) - pad), -INFINITY);
-        out.hi[i] = nextafterf(static_cast<float>(static_cast<double>(out.hi[i]) + pad), INFINITY);
-    }
-    return BOUNDED;
-}
-
-// Per-ray Moller-Trumbore padding (AccelHost::lmt, accel_math.h mt_pad). The
-// bound above, taken per ray instead of for the worst origin and |cos| >=
-// kMtCos: with D = |d|, S >= |o - p1|, X = |e1||e2|, c = |cos(d, n)| and
+// t, u, v each computed through f = 1/a, so on grazing rays from afar the hit
+// can stray far from the triangle (tests/test_accel_cpu.py). The accelerator
+// bounds the stray per ray (AccelHost::lmt, accel_math.h mt_pad). First-order
+// float error bounds of the dot and cross products (u = 2^-24; |da| <= 7u D X,
+// eu <= (9u D S E2 + 1.5 * 7u D X) / A, ev likewise with E1; the round-2 form of
+// this bound took the worst origin and |cos| >= 0.03 and forced entry below):
+// with D = |d|, S >= |o - p1|, X = |e1||e2|, c = |cos(d, n)| and
 // A = max(1e-5, D c |e1 x e2|) - 7u D X the smallest |a| an accepted hit can
 // have (|a| = D c |e1 x e2| exactly, the computed one is >= 1e-5 and within
 // 7u D X of it),
@@ -182,9 +134,9 @@ RTA_HD int classify_mt_triangle(const FlatShape& s, Box3& out, double origin_lim
 // P = Q + D dl / (1 - r) before parameter l / (|d| (1 - r)): X* is inside the
 // box padded by Q, and the ray point D dl / (1 - r) before X* (or the origin,
 // when t* is smaller) is then inside the box padded by P. mt_pad takes P
-// twice (kMtSafety) and, per local node, the worst triangle below it: the
+// twice (safety 2) and, per local node, the worst triangle below it: the
 // smallest |e1 x e2| and cosine (the grazing cone), the largest X, E1 + E2 and
-// |p1 - Z|, with S = |o - Z| + |p1 - Z|. No kMtCos, no origin bound beyond
+// |p1 - Z|, with S = |o - Z| + |p1 - Z|. No |cos| threshold, no origin bound beyond
 // the static box's: a ray grazing a node's cone gets the 1e-5 floor's pad, and
 // only a node whose floor is below 2.5e-6 (triangles with X > ~6) is entered
 // whatever its box says.
@@ -219,18 +171,12 @@ RTA_HD int classify_mt_tight(const FlatShape& s, Box3& out, double origin_lim, M
 // never returns INNER. origin_lim: largest |coordinate| of a ray origin the
 // bound must hold for (0 for the build's first pass, which only measures the
 // scene's magnitude). mt: triangles take the Moller-Trumbore test
-// (classify_mt_triangle; the other shapes' tests do not depend on it).
-#ifndef RTA_MT_RAYPAD
-#define RTA_MT_RAYPAD 1
-#endif
+// (classify_mt_tight, the static part of their bound; the other shapes' tests
+// do not depend on it).
 RTA_HD int classify(const FlatShape& s, Box3& out, double origin_lim, bool mt = false) {
     if (mt && s.type == RT_TRIANGLE) {
-#if RTA_MT_RAYPAD
         MtTri m;
         return classify_mt_tight(s, out, origin_lim, m);
-#else
-        return classify_mt_triangle(s, out, origin_lim);
-#endif
     }
     BoxAcc acc;
     switch (s.type) {

@@ -857,51 +857,12 @@ __device__ __forceinline__ void cas(Kids4& k, int i, int j) {
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
-// MT (AccelHost::mt): the cone is a grazing cone; a child the ray might graze
-// (|dot| < thr) is entered at parameter 0 whatever its box, and nothing is culled
-// by facing (Moller-Trumbore has no back-face test).
-template <bool MT = false>
-__device__ __forceinline__ void wide_pair(const rta::RayC& c, float tl, f2 lx, f2 ly, f2 lz, f2 hx, f2 hy, f2 hz,
-                                          f2 ax, f2 ay, f2 az, f2 th, float& t0, float& t1, bool& h0, bool& h1) {
-    const f2 ix = {c.ix, c.ix}, iy = {c.iy, c.iy}, iz = {c.iz, c.iz};
-    const f2 ox = {-c.ox, -c.ox}, oy = {-c.oy, -c.oy}, oz = {-c.oz, -c.oz};
-    const f2 x0 = fma2(lx, ix, ox), x1 = fma2(hx, ix, ox);
-    const f2 y0 = fma2(ly, iy, oy), y1 = fma2(hy, iy, oy);
-    const f2 z0 = fma2(lz, iz, oz), z1 = fma2(hz, iz, oz);
-    const f2 dz = {c.dz, c.dz}, dy = {c.dy, c.dy}, dx = {c.dx, c.dx};
-    const f2 dn = fma2(ax, dx, fma2(ay, dy, az * dz));
-    const f2 thr = th - (f2){rta::kConeEps, rta::kConeEps};
-    float tn[2], tf[2], te[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        // kNoPrune children (accel.h): no distance limit, entered at parameter 0
-        const bool np = th[k] < -6.0f;
-        tn[k] = fmaxf(fmaxf(fminf(x0[k], x1[k]), fminf(y0[k], y1[k])), fmaxf(fminf(z0[k], z1[k]), 0.0f));
-        // min(tz, np ? inf : tl) as a select of two mins: a min fed by a select gets an
-        // extra canonicalising max on gfx950 (IEEE mode), one per child on the walk's path
-        const float tz = fmaxf(z0[k], z1[k]);
-        tf[k] = fminf(fminf(fmaxf(x0[k], x1[k]), fmaxf(y0[k], y1[k])), np ? fminf(tz, INFINITY) : fminf(tz, tl));
-        te[k] = np ? 0.0f : tn[k];
-    }
-    if (MT) {
-        const bool g0 = __builtin_fabsf(dn[0]) < th[0] + rta::kConeEps, g1 = __builtin_fabsf(dn[1]) < th[1] + rta::kConeEps;
-        t0 = g0 ? 0.0f : te[0];
-        t1 = g1 ? 0.0f : te[1];
-        h0 = (tn[0] <= tf[0]) | g0;
-        h1 = (tn[1] <= tf[1]) | g1;
-        return;
-    }
-    t0 = te[0];
-    t1 = te[1];
-    h0 = (tn[0] <= tf[0]) & !(dn[0] < thr[0]);
-    h1 = (tn[1] <= tf[1]) & !(dn[1] < thr[1]);
-}
-
 // The barycentric accelerator's wide node, 8 float4 = 128 B (one cache line):
-// the four children's boxes as above, one quantized back-face cone word per
-// child (accel_math.h, cone_word; kConeNp marks a kNoPrune child) and the child
-// codes. Same boxes, entry parameters and limits as wide_pair; the cone test is
-// one dot4 per child.
+// the four children's boxes as six rows (lo.x of the four, lo.y, ... hi.z), one
+// quantized back-face cone word per child (accel_math.h, cone_word; kConeNp
+// marks a kNoPrune child: entered at parameter 0, no distance limit) and the
+// child codes. Same slab operations as rta::box_enter; the cone test is one
+// dot4 per child.
 __device__ __forceinline__ void wide_pair_q(const rta::RayC& c, float tl, f2 lx, f2 ly, f2 lz, f2 hx, f2 hy, f2 hz,
                                             int w0, int w1, float& t0, float& t1, bool& h0, bool& h1) {
     const f2 ix = {c.ix, c.ix}, iy = {c.iy, c.iy}, iz = {c.iz, c.iz};
@@ -955,7 +916,7 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
         // Record: per child 4 float4 (lo.xyz hi.x | hi.yz axis.xy | axis.z s m0 m1 |
         // m2 m3 m4 m5), then the codes. Results select-written (kMtUnroll < 4 would
         // index them by a loop variable). Pairs of children on packed f32
-        // instructions (as wide_pair) spilled 40-140 VGPRs in every MT instance (r03).
+        // instructions (as wide_pair_q) spilled 40-140 VGPRs in every MT instance (r03).
         const float4 cd = q[16];
         t[0] = t[1] = t[2] = t[3] = 0.0f;
         h[0] = h[1] = h[2] = h[3] = false;

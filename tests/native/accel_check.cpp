@@ -96,12 +96,6 @@ bool ref_aabb(V o, V inv, const rt_vec3& lo, const rt_vec3& hi) {
 }
 
 // The device walk's conservative tests (accel_math.h), same float operations.
-// MT grazing cone (accel.h, AccelHost::mt): the device's test in wide_pair.
-bool grazing(const rta::RayC& c, const float* k) {
-    const float dn = std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz));
-    return std::fabs(dn) < k[3] + rta::kConeEps;
-}
-
 bool padded(const rta::RayC& c, const rta::Box3& b, float l) {
     float te;
     return rta::box_enter(c, b.lo[0], b.lo[1], b.lo[2], b.hi[0], b.hi[1], b.hi[2], rta::t_limit(l, c.rdl), te);
@@ -191,12 +185,9 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         const int j = A.st.wchild[rta::kWide * w + s2];
                         if (j < 0) continue;
                         const float* k = &A.st_cone[4 * j];
-                        if (g_mt) {
-                            if (!grazing(rc, k) && !padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
-                        } else {
-                            if (!padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
-                            if (rta::cone_culls_q(rta::cone_word(k[0], k[1], k[2], k[3]), rc.dq)) continue;  // the device's quantized cone
-                        }
+                        // (MT accelerators build no scene tree)
+                        if (!padded(rc, A.st.box[j], k[3] <= rta::kNoPrune ? INFINITY : l)) continue;
+                        if (rta::cone_culls_q(rta::cone_word(k[0], k[1], k[2], k[3]), rc.dq)) continue;  // the device's quantized cone
                         const int sub = A.st.wsub[rta::kWide * w + s2];
                         if (sub >= 0) {
                             st.push_back(-(sub + 1) - kSceneBase);
@@ -229,7 +220,6 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                         if (j < 0) continue;
                         const float* k = &A.lcone[4 * j];
                         if (g_mt) {
-#if RTA_MT_RAYPAD
                             float pad, lf, q2, pt;
                             if (rta::mt_pad(rc, so, k, &A.lmt[kMtF * j], pad, lf, q2, pt)) {
                                 if (g_pad_scale != 1.0f) {  // mutation check only (out_info[7] = 777)
@@ -250,9 +240,6 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                                 ++forced;
                                 ++forced_depth[std::min(63, wdepth[w])];
                             }
-#else
-                            if (!grazing(rc, k) && !padded(rc, A.lbox[j], l)) continue;
-#endif
                         } else {
                             if (!padded(rc, A.lbox[j], l)) continue;
                             if (rta::cone_culls_q(rta::cone_word(k[0], k[1], k[2], k[3]), rc.dq)) continue;  // the device's quantized cone
