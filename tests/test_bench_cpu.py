@@ -83,7 +83,9 @@ def test_inflight_plan_and_hardware_queues():
     """Frames in flight per workload, and the hardware-queue count raised to 2F (<= 32)
     so that the F renderer streams and torch's own stream do not share queues."""
     # car, 1 GPU: 2 frames in flight, the box's 4 queues suffice
-    assert bench.plan_inflight(0, 1920, 1080, 1, False, False, "4") == (2, None)
+    assert bench.plan_inflight(0, 1920, 1080, 1, False, False, "4") == (3, "6")
+    # 3840x2160: 2 frames
+    assert bench.plan_inflight(0, 3840, 2160, 1, False, False, "4") == (2, None)
     # 800x600: 4 frames, 8 queues
     assert bench.plan_inflight(0, 800, 600, 1, False, False, "4") == (4, "8")
     # a rank's 1/8 stripe share over rt_group: 8 frames, 16 queues
