@@ -180,10 +180,10 @@ RTA_HD float rcp(float x) {
 #endif
 }
 
-// Moller-Trumbore per-ray padding (accel_bound.h, the derivation above
-// mt_node_consts). k: the node's grazing cone (axis, s = 2 sin(psi/2) + margin);
-// m: its MtPad constants {cr_min, u X_max, M_max, 18 M_max + 10.5 Esum_max};
-// so: |o - Z| of the ray. Returns false when no finite bound holds (the walk
+// Moller-Trumbore per-ray padding (the derivation above accel_bound.h MtTri).
+// k: the node's grazing cone (axis, s = 2 sin(psi/2) + margin); m: its
+// AccelHost::lmt constants {cr_min, u X_max, M_max, 18 M_max + 10.5 Esum_max,
+// w, h0} (M = |p1 - Z|; w, h0: mt_slab); so: |o - Z| of the ray. Returns false when no finite bound holds (the walk
 // enters at parameter 0); else `pad` to add to the node's static box on every
 // side and `lf` (>= 1) to multiply the distance limit by.
 constexpr int kMtPadF = 6;  // floats per local node in AccelHost::lmt
@@ -208,7 +208,7 @@ RTA_HD bool mt_pad(const RayC& c, float so, const float* k, const float* m, floa
 // The node's slab along its cone axis a: every triangle below lies within
 // |a.x - w| <= h0 (m[4] = w, m[5] = h0), and its plane within angle theta of
 // a's, 2 sin(theta/2) <= k[3]. X* (in T's plane, within Q of T) is then within
-// h0 + Q k[3] of w along a, and the ray point the box test stands for (within
+// h0 + Q k[3] of w along a (taken with 2Q, as the box takes it), and the ray point the box test stands for (within
 // D dl lf of X* along the ray) within a further D dl lf |a.d/|d||. So the ray
 // segment must meet that slab too: true when [t0, t1] (the box's interval)
 // meets it. q2 = 2Q, pt = 2 D dl lf (mt_pad's two parts of pad); on >= |o|_1.
