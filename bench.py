@@ -15,8 +15,8 @@ CHILD process (before touching the GPU) and exits with its return code; under
 torchrun it checks that WORLD_SIZE == N.
 
 Modes (--mode auto = frames at N = 1, strong at N > 1):
-  frames  one GPU renders whole frames (frames in flight: --inflight, auto 2 at
-          1080p, up to 4 for frames too small to fill the GPU);
+  frames  one GPU renders whole frames (frames in flight: --inflight, auto 3 at
+          1080p, 2 at 4K, up to 4 for frames too small to fill the GPU);
   strong  the north star's multi-GPU frame: every step renders ONE
           1920x1080 frame split over the N GPUs by interleaved 8-row stripes and
           gathers it to rank 0 through the C ABI's rt_group (ncclSend/ncclRecv
@@ -93,8 +93,9 @@ def parse(argv=None):
                     help="config 3: the four wheels turn every frame (updateWheelAnimations, src/main.cpp:1084-1109) "
                          "and the tree is refit on the device (rt_animate) inside the timed step")
     ap.add_argument("--inflight", type=int, default=0,
-                    help="frames in flight per GPU; 0 = auto: 2, or up to 4 while the GPU's share of a frame "
-                         "has fewer than 16k 8x8 tiles (too few waves to fill it)")
+                    help="frames in flight per GPU; 0 = auto: 3 below 64k 8x8 tiles (1080p), 2 above (4K), up "
+                         "to 4 while the GPU's share of a frame has fewer than 16k tiles; strong mode over "
+                         "rt_group: at least that, up to 8 for a rank's small share")
     ap.add_argument("--mode", default="auto", choices=["auto", "frames", "strong", "weak"])
     ap.add_argument("--gather", default="auto", choices=["auto", "rt", "torch"],
                     help="strong mode's fan-in: rt = rt_group (RCCL send/recv, C ABI); torch = "
@@ -272,7 +273,7 @@ def pmc_entry(key):
         return json.load(f).get(key)
 
 
-def roofline(info, kname, k_ms, pixels, b_ref, pmc):
+def roofline(info, kname, k_ms, pixels, b_ref, pmc, share=None):
     """The render kernel against its rooflines (see the module docstring).
 
     HBM: achieved = DRAM bytes per launch (PMC) / this run's kernel time; frac vs 8 TB/s.
@@ -280,10 +281,17 @@ def roofline(info, kname, k_ms, pixels, b_ref, pmc):
     VALU and SALU instruction counts against the CU's issue rates give a floor per
     launch; issue.frac = that floor / this run's kernel time. `bound` names what
     binds: "hbm" if the HBM fraction is the larger, else "latency" -- neither pipe
-    is saturated, and waves wait on dependent fetches (issue.wait_frac)."""
+    is saturated, and waves wait on dependent fetches (issue.wait_frac).
+
+    share (strong lines): this rank renders that fraction of the frame's rows with
+    the same kernel, and `pmc` is the workload's single-GPU entry. Its DRAM bytes
+    are not this launch's (traffic null; achieved from the compulsory bytes), and
+    its issue floors are scaled by the share: interleaved 8-row stripes give each
+    rank the same mix of sky and car rows (tools/pmc_summary.py has no per-rank
+    entry; PMC passes need a process of their own per GPU)."""
     compulsory = 16.0 * pixels + float(info.get("record_bytes", 0))
     k_s = k_ms * 1e-3
-    measured = pmc.get("bytes") if pmc else None
+    measured = pmc.get("bytes") if pmc and share is None else None
     achieved = (measured if measured else compulsory) / k_s / 1e9
     frac = achieved / HBM_PEAK_GBS
     out = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -300,6 +308,11 @@ def roofline(info, kname, k_ms, pixels, b_ref, pmc):
            "reference_equivalent_GBps": b_ref / k_s / 1e9,
            "kernel": kname, "kernel_ms": k_ms}
     iss = pmc.get("issue") if pmc else None
+    if iss and share is not None and iss.get("valu_floor_ms") is not None:
+        iss = dict(iss, valu_floor_ms=iss["valu_floor_ms"] * share, salu_floor_ms=iss["salu_floor_ms"] * share,
+                   row_share=share,
+                   basis=f"single-GPU PMC of the same kernel ({pmc['source']}), issue floors x this rank's "
+                         f"row share {share:.4f}")
     if iss:
         out["issue"] = dict(iss)
         if iss.get("valu_floor_ms") is not None:
@@ -333,10 +346,11 @@ def plan_inflight(inflight, W, H, world, strong, use_group, exported):
     tiles = ((W + 7) // 8) * ((share_rows + 7) // 8)
     if inflight > 0:
         F = inflight
-    elif use_group:
-        F = min(8, max(2, -(-32768 // tiles)))
-    else:  # 3 below 64k tiles: the 1080p car 0.1883 -> 0.1860 ms with 3 (4: 0.205; r03t)
+    else:
+        # 3 below 64k tiles: the 1080p car 0.1883 -> 0.1860 ms with 3 (4: 0.205; r03t)
         F = min(4, max(3 if tiles < 65536 else 2, -(-16384 // tiles) + 1))
+        if use_group:  # at least the frames mode's F (one rank: the same frame), more for small shares
+            F = min(8, max(F, -(-32768 // tiles)))
     if strong and not use_group:
         F = 1  # the torch path gathers one shared buffer per step
     have = int(exported) if str(exported).isdigit() else 4
@@ -567,21 +581,42 @@ def main():
     # SURVEY §8(d)'s frame: upload + dispatch + completion, one at a time, FPS = 1 / median.
     # Each frame waits for its completion (the reference's loop, src/main.cpp:290-462), with
     # rt_set_latency_mode on: the setting for a host that waits for every frame.
+    # The host sees a frame's end through the renderer's own wait (rt_sync / the group's
+    # bounded rt_group_sync), which polls the stream instead of sleeping on the runtime's
+    # completion interrupt. Over rt_group every rank starts each frame after a barrier,
+    # so rank 0's frame includes the slowest peer's stripes crossing its link.
     serial_frames = []
-    if not use_group or world == 1:
-        if not use_group:
-            ctx.set_latency_mode(1)
+    if not (strong and not use_group):  # the torch-gather rehearsal has no waited-frame figure
+        for c_ in ctxs:
+            c_.set_latency_mode(1)
+
+        def wait_frame():
+            if grp is not None:
+                group_sync()
+            else:
+                ctx.sync()
+
         for i in range(a.warmup):
             frame(i, 1)
-        torch.cuda.synchronize()
+            wait_frame()
         for i in range(a.steps):
+            if world > 1:
+                dist.barrier()
+                torch.cuda.synchronize()
             t0 = time.perf_counter()
             frame(i, 1)
-            torch.cuda.synchronize()
+            wait_frame()
             serial_frames.append(time.perf_counter() - t0)
-        if not use_group:
-            ctx.set_latency_mode(0)
-        ctx.kernel_times()
+        for c_ in ctxs:
+            c_.set_latency_mode(0)
+            c_.kernel_times()
+        if grp is not None:
+            grp.phase_times()
+    serial_med_ranks = None
+    if serial_frames and world > 1:
+        med = [None] * world
+        dist.all_gather_object(med, float(np.median(serial_frames)) * 1e3)
+        serial_med_ranks = med
     # the same one-at-a-time frames with rt_set_latency_mode (what a host that waits for
     # each frame would set); reported beside serial_ms_per_step, not used for the roofline
     serial_lat = None
@@ -619,7 +654,9 @@ def main():
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
         suffix = "".join(f"_{n}" for n, on in (("brute", a.brute), ("mt", a.mt), ("fresnel", a.fresnel),
                                                   ("variant", a.variant), ("animate", a.animate)) if on)
-        pmc = pmc_entry(f"config{a.config}_n{world}_{a.kernel}{suffix}") if not strong else None
+        # strong lines: the same kernel over this rank's rows; the single-GPU entry with its
+        # issue floors scaled by the row share (roofline docstring)
+        pmc = pmc_entry(f"config{a.config}_n{1 if strong else world}_{a.kernel}{suffix}")
         out = {
             "metric": METRIC,
             "value": rays_step * a.steps / elapsed / 1e6,
@@ -633,9 +670,12 @@ def main():
             "serial_ms_per_step": (serial if serial is not None else elapsed) / a.steps * 1e3,
             "serial_ms_per_step_latency_mode": (serial_lat / a.steps * 1e3) if serial_lat is not None else None,
             "serial_frame_ms_median": float(np.median(serial_frames)) * 1e3 if serial_frames else None,
-            "serial_frame_median_mode": ("each frame waited for (host sync), rt_set_latency_mode on"
-                                         if serial_frames and not use_group else
-                                         "each frame waited for (host sync)" if serial_frames else None),
+            "serial_frame_median_mode": (("each frame waited for (rt_sync: host polls the stream), "
+                                          "rt_set_latency_mode on") if serial_frames and not use_group else
+                                         ("each frame waited for on every rank (rt_group_sync), ranks start "
+                                          "each frame after a barrier, rt_set_latency_mode on; rank 0's median")
+                                         if serial_frames else None),
+            "serial_frame_ms_median_per_rank": serial_med_ranks,
             "fps_serial_median": 1.0 / float(np.median(serial_frames)) if serial_frames else None,
             "higher_is_better": True,
             "scaling": "strong" if strong else "weak",
@@ -664,7 +704,7 @@ def main():
             "kernel_ms_mean": k_ms,
             "kernel_ms_median": k_med,
             "kernel_ms_mean_inflight": float(np.mean(kt_if)) if len(kt_if) else float("nan"),
-            "roofline": roofline(info, kname, k_ms, rows * W, b_ref_rank, pmc),
+            "roofline": roofline(info, kname, k_ms, rows * W, b_ref_rank, pmc, share=rows / H if strong else None),
             "accel": info,
             "cpu_baseline": None,
             "parity": None,

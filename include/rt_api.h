@@ -163,8 +163,12 @@ int rt_dispatch_rows(struct rt_ctx* ctx, int width, int height, int y0, int stri
  * the reference's image2D rgba32f) or RT_FORMAT_RGB32F (12 B per pixel, packed;
  * the alpha the reference stores is always 1, gpu_shader.comp:437,623). The
  * multi-GPU gather (rt_group.h) sends RGB32F: 25 % fewer bytes over xGMI.
- * pitch >= 12*width and 4-byte aligned for RGB32F. */
-enum rt_format { RT_FORMAT_RGBA32F = 0, RT_FORMAT_RGB32F = 1 };
+ * pitch >= 12*width and 4-byte aligned for RGB32F.
+ * RT_FORMAT_RGBA32F_IMAGE: RGBA32F written at each row's IMAGE row y, not at its
+ * compact row r: dst is the whole width x height surface (pitch >= 16*width),
+ * and rows the call does not render are left untouched. rt_group's rank 0
+ * renders its stripes straight into the gathered frame this way. */
+enum rt_format { RT_FORMAT_RGBA32F = 0, RT_FORMAT_RGB32F = 1, RT_FORMAT_RGBA32F_IMAGE = 2 };
 int rt_dispatch_rows_fmt(struct rt_ctx* ctx, int width, int height, int y0, int stripe, int step, int out_rows,
                          float* dst, size_t pitch, int format);
 

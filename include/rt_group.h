@@ -9,12 +9,13 @@
  * first `share` stripes of every period, rank r >= 1 the stripe share - 1 + r.
  * With share 1 (the default) that is the interleave
  *     { image row y : (y / stripe) mod P == r }.
- * Each rank renders (rt_dispatch_rows_ex) into a compact packed-RGB buffer
- * (12 B per pixel: the alpha is always 1); rank 0 renders straight into its
- * staging buffer. One fan-in per frame brings the other ranks' rows to rank 0 —
- * grouped ncclSend/ncclRecv over xGMI (RCCL) or device copies — and a kernel on
- * rank 0 scatters the stripes back into image order in rank 0's pitched
- * RGBA32F surface. Interleaving balances sky rows against rows through the car
+ * Each rank r >= 1 renders (rt_dispatch_rows_ex) into a compact packed-RGB
+ * buffer (12 B per pixel: the alpha is always 1); rank 0 renders its stripes
+ * straight into its pitched RGBA32F surface at their image rows
+ * (RT_FORMAT_RGBA32F_IMAGE). One fan-in per frame brings the other ranks' rows
+ * to rank 0 — grouped ncclSend/ncclRecv over xGMI (RCCL) or device copies — and
+ * a kernel on rank 0 scatters them into image order in that surface. A group of
+ * one rank renders the single-GPU frame with no fan-in and no scatter. Interleaving balances sky rows against rows through the car
  * without any per-frame planning; no other collective runs.
  *
  * Two ways to build a group:
@@ -138,8 +139,11 @@ typedef struct rt_group_phases {
 int rt_group_phase_times(struct rt_group* g, rt_group_phases* out);
 
 /* Rank 0's surface of the LAST dispatched frame (each frame slot has its own;
- * RT_ERR_INVALID in a process without rank 0). read_image waits (bounded) and
- * copies the whole frame; width/height must equal the last dispatch's. */
+ * RT_ERR_INVALID in a process without rank 0, RT_ERR_COMM once the group is
+ * broken). read_image waits (bounded) and copies the whole frame; width/height
+ * must equal the last dispatch's. device_image returns the surface without
+ * waiting: its contents are the frame only after rt_group_sync, and stay so
+ * until `frames` (rt_group_set_frames) more dispatches, which reuse the slot. */
 int rt_group_read_image(struct rt_group* g, float* host_dst, size_t pitch, int width, int height);
 int rt_group_device_image(struct rt_group* g, void** ptr, size_t* pitch);
 

@@ -123,7 +123,8 @@ struct KParams {
     int tail_rx, tail_regions;               // 64x64-pixel regions: per row, total (one counter each)
     int tail_counters;                       // counters per set (>= tail_regions; all zeroed for the next)
     int tail_max_lanes;                      // a wave queues its rays only if at most this many are alive
-    int rgb;                                 // 1: packed RGB32F output, 12 B per pixel (rt_dispatch_rows_fmt)
+    int rgb;                                 // output format (rt_dispatch_rows_fmt): 0 RGBA32F, 1 packed RGB32F
+                                             // (12 B per pixel), 2 RGBA32F at the image row (RT_FORMAT_RGBA32F_IMAGE)
     float shadow_off;                        // k_accel's shadow-ray offset: 1e-3 (BVH branch, gpu_shader.comp:469);
                                              // 1e-5 when it renders the brute branch (:565, rt_ctx::brute)
 };
@@ -306,14 +307,17 @@ __device__ __forceinline__ PrimRec load_prim(const float4* __restrict__ base, in
 
 // Writes the pixel for output row r, column x.
 __device__ __forceinline__ void store_px(const KParams& kp, int r, int x, float4 v) {
-    if (kp.rgb) {  // alpha is always 1 (gpu_shader.comp:437,623): the multi-GPU gather sends 12 B per pixel
+    if (kp.rgb == 1) {  // alpha is always 1 (gpu_shader.comp:437,623): the multi-GPU gather sends 12 B per pixel
         float* p = reinterpret_cast<float*>(kp.dst + static_cast<size_t>(r) * kp.pitch) + 3 * x;
         __builtin_nontemporal_store(v.x, p);
         __builtin_nontemporal_store(v.y, p + 1);
         __builtin_nontemporal_store(v.z, p + 2);
         return;
     }
-    float4* row = reinterpret_cast<float4*>(kp.dst + static_cast<size_t>(r) * kp.pitch);
+    // RT_FORMAT_RGBA32F_IMAGE (rgb == 2): the pixel goes to its image row of a whole
+    // W x H surface (rt_group's rank 0 renders its stripes straight into the frame)
+    const int row_i = kp.rgb == 2 ? image_row(kp, r) : r;
+    float4* row = reinterpret_cast<float4*>(kp.dst + static_cast<size_t>(row_i) * kp.pitch);
     // streaming store (one global_store_dwordx4 ... nt): the kernel never reads the image
     // back, so it should not displace the scene records from L2 (config 3 -1.1 %, config 2 -1.7 %)
     __builtin_nontemporal_store(v.x, &row[x].x);

@@ -8,12 +8,15 @@
 // stripe share - 1 + r (rt_group_set_root_share; share 1 = the plain interleave
 // { y : (y / stripe) mod P == r }). Every rank renders through
 // rt_dispatch_rows_ex into a compact packed-RGB buffer (alpha is always 1, so
-// 12 B per pixel); rank 0 renders straight into its staging buffer, since its
-// own rows never move. The fan-in is one grouped ncclSend/ncclRecv per frame
-// (each peer's rows to rank 0 over its own xGMI link), or, in one process with
-// repeated devices, peer copies into rank 0's staging. k_unstripe then scatters
-// the slots back into image order in rank 0's pitched surface: one coalesced
-// read and one streaming write per pixel (25 + 33 MB at 1080p, ~10 us).
+// 12 B per pixel), except rank 0, which renders its stripes straight into the
+// frame at their image rows (RT_FORMAT_RGBA32F_IMAGE): its rows never move. The
+// fan-in is one grouped ncclSend/ncclRecv per frame (each peer's rows to rank
+// 0's staging over its own xGMI link), or, in one process with repeated
+// devices, peer copies into rank 0's staging. k_unstripe then scatters the
+// peers' rows into image order in rank 0's pitched surface: one coalesced read
+// and one streaming write per pixel of (P - 1) / (share + P - 1) of the frame.
+// With one rank there is no fan-in and no unstripe: the group's frame is the
+// single-GPU frame.
 //
 // Frames in flight (rt_group_set_frames): every member holds F slots -- a
 // context, a render stream and the frame's buffers -- and ONE communicator with
@@ -44,7 +47,7 @@ struct Slot {
     hipStream_t stream = nullptr;  // this slot's render (and, on rank 0, unstripe) stream
     float* buf = nullptr;          // ranks >= 1: compact stripes, rows x W packed RGB32F (12 B per pixel)
     size_t buf_cap = 0;            // bytes
-    float* staging = nullptr;      // rank 0: its rows, then P - 1 slots of rows1 x W packed RGB
+    float* staging = nullptr;      // rank 0: P - 1 slots of rows1 x W packed RGB, one per peer
     size_t staging_cap = 0;
     float* img = nullptr;          // rank 0: this slot's gathered frame (RGBA32F, pitched)
     size_t img_pitch = 0;
@@ -86,19 +89,20 @@ Rows rank_rows(int height, int nranks, int s, int k, int rank) {
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// out[y][x]: stripe band = y / s sits at position c = band % Q of its period
-// (Q = k + P - 1). c < k: rank 0's slot (offset 0), compact row (band / Q) * k * s
-// + c * s + y % s; otherwise rank c - k + 1's slot, at rows0 + (c - k) * rows1
-// rows from the start, compact row (band / Q) * s + y % s. The slots hold packed
-// RGB (rt_dispatch_rows_ex RGB32F), the image RGBA with alpha 1.
-__global__ __launch_bounds__(256) void k_unstripe(const float* __restrict__ staging, int rows0, int rows1, int width,
-                                                   int s, int k, int q, f4v* __restrict__ img, size_t pitch_f4) {
+// The peers' rows into image order. Staging holds P - 1 slots of rows1 packed-RGB
+// rows (rt_dispatch_rows_ex RGB32F), one per rank r >= 1 in rank order; compact
+// row cr of rank r is image row (k - 1 + r) * s + (cr / s) * (k + P - 1) * s + cr % s
+// (rank_rows). Rows past a rank's count map to y >= height and are skipped. One
+// coalesced read and one streaming RGBA store (alpha 1) per pixel.
+__global__ __launch_bounds__(256) void k_unstripe(const float* __restrict__ staging, int rows1, int width, int height,
+                                                   int s, int k, int P, f4v* __restrict__ img, size_t pitch_f4) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
-    const int y = blockIdx.y;
+    const int by = blockIdx.y;  // (rank - 1) * rows1 + compact row
     if (x >= width) return;
-    const int band = y / s, c = band % q, cyc = band / q;
-    const int r = c < k ? cyc * k * s + c * s + (y - band * s) : rows0 + (c - k) * rows1 + cyc * s + (y - band * s);
-    const float* p = staging + 3 * (static_cast<size_t>(r) * width + x);
+    const int rank = 1 + by / rows1, cr = by - (rank - 1) * rows1;
+    const int y = (k - 1 + rank) * s + (cr / s) * (k + P - 1) * s + cr % s;
+    if (y >= height) return;
+    const float* p = staging + 3 * (static_cast<size_t>(by) * width + x);
     const f4v v = {__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2),
                    1.0f};
     __builtin_nontemporal_store(v, &img[static_cast<size_t>(y) * pitch_f4 + x]);
@@ -390,8 +394,24 @@ int rt_group_info(rt_group* g, int* nranks, int* nlocal, int* transport) {
 int rt_group_set_frames(rt_group* g, int frames) {
     if (!g || frames < 1 || frames > kMaxFrames || g->have_scene || g->next > 0) return RT_ERR_INVALID;
     if (g->broken) return RT_ERR_COMM;
-    for (Member& b : g->m)
+    for (Member& b : g->m) {
         while (static_cast<int>(b.slot.size()) < frames) G_TRY(add_slot(b));
+        // fewer slots than before: nothing has been dispatched or uploaded yet, so the
+        // extra ones go (each_ctx and pending() iterate every slot a member holds)
+        while (static_cast<int>(b.slot.size()) > frames) {
+            Slot& s = b.slot.back();
+            G_HIP(hipSetDevice(b.device));
+            if (s.ctx) rt_destroy(s.ctx);
+            hipFree(s.buf);
+            hipFree(s.staging);
+            hipFree(s.img);
+            if (s.rendered) hipEventDestroy(s.rendered);
+            if (s.fanned) hipEventDestroy(s.fanned);
+            if (s.released) hipEventDestroy(s.released);
+            if (s.stream) hipStreamDestroy(s.stream);
+            b.slot.pop_back();
+        }
+    }
     g->frames = frames;
     return RT_OK;
 }
@@ -431,13 +451,25 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         stripe > 65535 / (g->share + g->nranks - 1))
         return RT_ERR_INVALID;
     if (g->broken) return RT_ERR_COMM;
+    // Every error from here on goes through fail(): in a multi-rank RCCL group the
+    // peers may already wait on this frame's fan-in, so the communicator is aborted.
+#define F_HIP(x)                                                     \
+    do {                                                             \
+        if ((x) != hipSuccess) return fail(g, RT_ERR_DEVICE);        \
+    } while (0)
+#define F_TRY(x)                                  \
+    do {                                          \
+        const int rc__ = (x);                     \
+        if (rc__ != RT_OK) return fail(g, rc__);  \
+    } while (0)
     const int P = g->nranks, k = g->share;
     const int j = static_cast<int>(g->next % g->frames);
     const size_t row_b = static_cast<size_t>(width) * 12;  // packed RGB32F
-    const int rows0 = rank_rows(height, P, stripe, k, 0).rows;
     const int rows1 = P > 1 ? rank_rows(height, P, stripe, k, 1).rows : 0;  // the most among ranks >= 1
+    if (static_cast<long long>(P - 1) * rows1 > 65535) return RT_ERR_INVALID;  // k_unstripe's grid
     const size_t slot_b = std::max<size_t>(1, static_cast<size_t>(rows1) * row_b);
-    const size_t stage = static_cast<size_t>(rows0) * row_b + static_cast<size_t>(P - 1) * rows1 * row_b;
+    // rank 0's staging holds the peers' rows only: its own go straight into the frame
+    const size_t stage = static_cast<size_t>(P - 1) * rows1 * row_b;
     // (Re)size slot j's buffers; a resize waits for the frames that still use them.
     bool resize = false;
     for (Member& b : g->m) {
@@ -446,15 +478,15 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
                  (b.rank == 0 && (s.staging_cap < stage || s.img_w != width || s.img_h != height));
     }
     if (resize) {
-        G_TRY(wait_all(g));
+        G_TRY(wait_all(g));  // aborts the communicators itself on a timeout or an RCCL error
         for (Member& b : g->m) {
             Slot& s = b.slot[j];
-            G_HIP(hipSetDevice(b.device));
+            F_HIP(hipSetDevice(b.device));
             if (b.rank != 0) {
-                G_TRY(grow(s.buf, s.buf_cap, slot_b));
+                F_TRY(grow(s.buf, s.buf_cap, slot_b));
                 continue;
             }
-            G_TRY(grow(s.staging, s.staging_cap, std::max<size_t>(stage, 16)));
+            F_TRY(grow(s.staging, s.staging_cap, std::max<size_t>(stage, 16)));
             if (s.img_w != width || s.img_h != height) {
                 hipFree(s.img);
                 s.img = nullptr;
@@ -462,7 +494,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
                 size_t pitch = 0;
                 if (hipMallocPitch(reinterpret_cast<void**>(&s.img), &pitch, static_cast<size_t>(width) * 16,
                                    height) != hipSuccess)
-                    return RT_ERR_NO_MEMORY;
+                    return fail(g, RT_ERR_NO_MEMORY);
                 s.img_pitch = pitch;
                 s.img_w = width;
                 s.img_h = height;
@@ -470,52 +502,55 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         }
     }
     PhaseRec& ph = g->ring[g->ring_pos];
-    if (ph.pending) {  // kPhaseRing frames ago: read its times (it has long finished)
-        hipSetDevice(g->m[g->tm].device);
-        if (hipEventSynchronize(ph.ev[ph.has_unstripe ? 5 : (ph.has_fan ? 3 : 1)]) != hipSuccess)
-            return fail(g, RT_ERR_DEVICE);
+    if (ph.pending) {
+        // kPhaseRing frames ago. Nothing makes the host wait between dispatches, so that
+        // frame may still be pending (a peer that never posts its send): never block on
+        // it unbounded -- the group's bounded wait decides (RT_ERR_TIMEOUT, comms aborted).
+        F_HIP(hipSetDevice(g->m[g->tm].device));
+        const hipError_t q = hipEventQuery(ph.ev[ph.has_unstripe ? 5 : (ph.has_fan ? 3 : 1)]);
+        if (q == hipErrorNotReady) G_TRY(wait_all(g));
+        else if (q != hipSuccess) return fail(g, RT_ERR_DEVICE);
         harvest(g, ph);
     }
     ph.has_fan = ph.has_unstripe = false;
-    // 1. every local rank renders its stripes on slot j's stream (rank 0 straight into
-    //    its staging rows; the others into buf, once the fan-in of the frame that
-    //    last used the slot has sent it)
+    // 1. every local rank renders its stripes on slot j's stream: rank 0 straight into
+    //    slot j's surface at their image rows, the others into buf once the fan-in of
+    //    the frame that last used the slot has sent it
     for (size_t mi = 0; mi < g->m.size(); ++mi) {
         Member& b = g->m[mi];
         Slot& s = b.slot[j];
         const bool timed = static_cast<int>(mi) == g->tm;
-        if (hipSetDevice(b.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        F_HIP(hipSetDevice(b.device));
         if (s.used && b.rank != 0) {
             // RCCL: released on this member's fan-in stream; copies: rank 0's copy of it
             const hipEvent_t free_ev = g->transport == RT_GATHER_COPY ? g->m[g->root].slot[j].fanned : s.released;
-            if (hipStreamWaitEvent(s.stream, free_ev, 0) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            F_HIP(hipStreamWaitEvent(s.stream, free_ev, 0));
         }
-        if (timed && hipEventRecord(ph.ev[0], s.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (timed) F_HIP(hipEventRecord(ph.ev[0], s.stream));
         const Rows w = rank_rows(height, P, stripe, k, b.rank);
         if (w.rows > 0) {
-            float* dst = b.rank == 0 ? s.staging : s.buf;
-            const int rc = rt_dispatch_rows_ex(s.ctx, width, height, w.y0, w.stripe, w.period, w.rows, dst, row_b,
-                                               RT_FORMAT_RGB32F);
+            const int rc = b.rank == 0 ? rt_dispatch_rows_ex(s.ctx, width, height, w.y0, w.stripe, w.period, w.rows,
+                                                             s.img, s.img_pitch, RT_FORMAT_RGBA32F_IMAGE)
+                                       : rt_dispatch_rows_ex(s.ctx, width, height, w.y0, w.stripe, w.period, w.rows,
+                                                             s.buf, row_b, RT_FORMAT_RGB32F);
             if (rc != RT_OK) return fail(g, rc);
         }
-        if (timed && hipEventRecord(ph.ev[1], s.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
-        if (hipEventRecord(s.rendered, s.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        if (timed) F_HIP(hipEventRecord(ph.ev[1], s.stream));
+        F_HIP(hipEventRecord(s.rendered, s.stream));
     }
-    auto slot_ptr = [&](int rank) {  // rank's rows in slot j's staging buffer
-        return reinterpret_cast<char*>(g->m[g->root].slot[j].staging) +
-               (rank == 0 ? 0 : static_cast<size_t>(rows0) * row_b + static_cast<size_t>(rank - 1) * rows1 * row_b);
+    auto slot_ptr = [&](int rank) {  // rank's rows in slot j's staging buffer (rank >= 1)
+        return reinterpret_cast<char*>(g->m[g->root].slot[j].staging) + static_cast<size_t>(rank - 1) * rows1 * row_b;
     };
     // 2. fan-in to rank 0's staging on the members' fan-in streams, in frame order
     if (g->transport == RT_GATHER_RCCL && P > 1) {
         for (size_t mi = 0; mi < g->m.size(); ++mi) {
             Member& b = g->m[mi];
             Slot& s = b.slot[j];
-            if (hipSetDevice(b.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            F_HIP(hipSetDevice(b.device));
             // a sender waits for its rows; rank 0 for the previous unstripe of this slot's staging
             const hipEvent_t before = b.rank == 0 ? (s.used ? s.released : nullptr) : s.rendered;
-            if (before && hipStreamWaitEvent(b.cstream, before, 0) != hipSuccess) return fail(g, RT_ERR_DEVICE);
-            if (static_cast<int>(mi) == g->tm && hipEventRecord(ph.ev[2], b.cstream) != hipSuccess)
-                return fail(g, RT_ERR_DEVICE);
+            if (before) F_HIP(hipStreamWaitEvent(b.cstream, before, 0));
+            if (static_cast<int>(mi) == g->tm) F_HIP(hipEventRecord(ph.ev[2], b.cstream));
         }
         if (ncclGroupStart() != ncclSuccess) return fail(g, RT_ERR_COMM);
         for (Member& b : g->m) {
@@ -539,53 +574,59 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         for (size_t mi = 0; mi < g->m.size(); ++mi) {
             Member& b = g->m[mi];
             Slot& s = b.slot[j];
-            if (hipSetDevice(b.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            F_HIP(hipSetDevice(b.device));
             if (static_cast<int>(mi) == g->tm) {
-                if (hipEventRecord(ph.ev[3], b.cstream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+                F_HIP(hipEventRecord(ph.ev[3], b.cstream));
                 ph.has_fan = true;
             }
-            if (hipEventRecord(s.fanned, b.cstream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+            F_HIP(hipEventRecord(s.fanned, b.cstream));
             if (b.rank != 0) {
-                if (hipEventRecord(s.released, b.cstream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+                F_HIP(hipEventRecord(s.released, b.cstream));
                 s.used = true;
             }
         }
     } else if (g->transport == RT_GATHER_COPY && P > 1) {
         Member& r = g->m[g->root];
         Slot& rs = r.slot[j];
-        G_HIP(hipSetDevice(r.device));
-        if (rs.used) G_HIP(hipStreamWaitEvent(r.cstream, rs.released, 0));
-        if (g->tm == g->root) G_HIP(hipEventRecord(ph.ev[2], r.cstream));
+        F_HIP(hipSetDevice(r.device));
+        if (rs.used) F_HIP(hipStreamWaitEvent(r.cstream, rs.released, 0));
+        if (g->tm == g->root) F_HIP(hipEventRecord(ph.ev[2], r.cstream));
         for (Member& b : g->m) {
             if (b.rank == 0) continue;
             const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, b.rank).rows) * row_b;
-            G_HIP(hipStreamWaitEvent(r.cstream, b.slot[j].rendered, 0));
-            if (n) G_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank), r.device, b.slot[j].buf, b.device, n, r.cstream));
+            F_HIP(hipStreamWaitEvent(r.cstream, b.slot[j].rendered, 0));
+            if (n) F_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank), r.device, b.slot[j].buf, b.device, n, r.cstream));
             b.slot[j].used = true;  // its next render waits for rs.fanned
         }
         if (g->tm == g->root) {
-            G_HIP(hipEventRecord(ph.ev[3], r.cstream));
+            F_HIP(hipEventRecord(ph.ev[3], r.cstream));
             ph.has_fan = true;
         }
-        G_HIP(hipEventRecord(rs.fanned, r.cstream));
+        F_HIP(hipEventRecord(rs.fanned, r.cstream));
     }
-    // 3. rank 0: stripes back into image order, into slot j's surface
+    // 3. rank 0: the peers' stripes into image order, into slot j's surface (its own
+    //    rows are there already; with one rank there is nothing to move)
     if (g->root >= 0) {
         Member& r = g->m[g->root];
         Slot& rs = r.slot[j];
-        if (hipSetDevice(r.device) != hipSuccess) return fail(g, RT_ERR_DEVICE);
-        if (P > 1 && hipStreamWaitEvent(rs.stream, rs.fanned, 0) != hipSuccess) return fail(g, RT_ERR_DEVICE);
-        if (g->tm == g->root && hipEventRecord(ph.ev[4], rs.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
-        hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, height), dim3(256), 0, rs.stream, rs.staging, rows0,
-                           rows1, width, stripe, k, k + P - 1, reinterpret_cast<f4v*>(rs.img), rs.img_pitch / 16);
-        if (hipGetLastError() != hipSuccess) return fail(g, RT_ERR_DEVICE);
-        if (g->tm == g->root) {
-            if (hipEventRecord(ph.ev[5], rs.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
-            ph.has_unstripe = true;
+        F_HIP(hipSetDevice(r.device));
+        if (P > 1 && rows1 > 0) {
+            F_HIP(hipStreamWaitEvent(rs.stream, rs.fanned, 0));
+            if (g->tm == g->root) F_HIP(hipEventRecord(ph.ev[4], rs.stream));
+            hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, (P - 1) * rows1), dim3(256), 0, rs.stream,
+                               rs.staging, rows1, width, height, stripe, k, P, reinterpret_cast<f4v*>(rs.img),
+                               rs.img_pitch / 16);
+            F_HIP(hipGetLastError());
+            if (g->tm == g->root) {
+                F_HIP(hipEventRecord(ph.ev[5], rs.stream));
+                ph.has_unstripe = true;
+            }
         }
-        if (hipEventRecord(rs.released, rs.stream) != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        F_HIP(hipEventRecord(rs.released, rs.stream));
         rs.used = true;
     }
+#undef F_HIP
+#undef F_TRY
     ph.pending = true;
     g->ring_pos = (g->ring_pos + 1) % kPhaseRing;
     g->last_slot = j;
@@ -671,6 +712,7 @@ int rt_group_read_image(rt_group* g, float* dst, size_t pitch, int width, int he
 
 int rt_group_device_image(rt_group* g, void** p, size_t* pitch) {
     if (!g || g->root < 0 || !p || !pitch || g->last_slot < 0) return RT_ERR_INVALID;
+    if (g->broken) return RT_ERR_COMM;
     const Slot& s = g->m[g->root].slot[g->last_slot];
     if (!s.img) return RT_ERR_INVALID;
     *p = s.img;

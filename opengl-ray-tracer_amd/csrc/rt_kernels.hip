@@ -38,6 +38,7 @@
 #include "accel_math.h"
 #include "lbvh.h"
 #include "rt_device.h"
+#include "group_wait.h"
 
 using namespace rtd;
 
@@ -2831,7 +2832,8 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int perio
     if (!c->have_scene || !c->have_cam || !c->have_light) return RT_ERR_NO_SCENE;
     const size_t px = format == RT_FORMAT_RGB32F ? 12 : 16, align = format == RT_FORMAT_RGB32F ? 4 : 16;
     if (width <= 0 || height <= 0 || stripe <= 0 || period < stripe || out_rows < 0 || y0 < 0 || !dst ||
-        (format != RT_FORMAT_RGBA32F && format != RT_FORMAT_RGB32F) || pitch < static_cast<size_t>(width) * px ||
+        (format != RT_FORMAT_RGBA32F && format != RT_FORMAT_RGB32F && format != RT_FORMAT_RGBA32F_IMAGE) ||
+        pitch < static_cast<size_t>(width) * px ||
         (pitch % align) != 0 || (reinterpret_cast<uintptr_t>(dst) % align) != 0)
         return RT_ERR_INVALID;
     std::memset(&kp, 0, sizeof kp);
@@ -2869,7 +2871,7 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int perio
     kp.dst = reinterpret_cast<char*>(dst);
     kp.pitch = pitch;
     kp.shadow_off = 1e-3f;
-    kp.rgb = format == RT_FORMAT_RGB32F ? 1 : 0;
+    kp.rgb = format;  // RT_FORMAT_*: 0 RGBA32F, 1 RGB32F, 2 RGBA32F at the image row
     kp.heavy_k = 0;
     kp.heavy_parts = 1;
     kp.lane_k = 0;
@@ -3007,7 +3009,7 @@ int render(rt_ctx* c, const KParams& kp) {
         KParams kn;
         const int rc = fill_kparams(nxt, kt.width, kt.height, kt.y0, kt.stripe, kt.period, kt.out_rows,
                                     reinterpret_cast<float*>(kt.dst), kt.pitch, kn,
-                                    kt.rgb ? RT_FORMAT_RGB32F : RT_FORMAT_RGBA32F);
+                                    kt.rgb);
         if (rc != RT_OK) return rc;
         kn.shadow_off = off;
         t = nxt;
@@ -3698,8 +3700,18 @@ int rt_dispatch(rt_ctx* c, int width, int height, int y0, int y1) {
 int rt_sync(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return RT_OK;
+    // A host that waits for every frame (the reference's loop, src/main.cpp:290-462)
+    // waits ~0.25 ms per frame: poll the stream back to back (yielding the core) for
+    // the first rtg::kSpinMs, so the frame's end is seen within a poll, instead of
+    // the runtime's interrupt-driven wake-up; past that, nap between polls
+    // (csrc/group_wait.h). No deadline: a single context has no peer to wait on.
+    const rtg::WaitResult w = rtg::wait_bounded(
+        [c] {
+            const hipError_t e = hipStreamQuery(c->stream);
+            return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+        },
+        [] { return false; }, 0.0);
+    return w == rtg::kWaitDone ? RT_OK : RT_ERR_DEVICE;
 }
 
 int rt_read_image(rt_ctx* c, float* dst, size_t pitch, int width, int height) {

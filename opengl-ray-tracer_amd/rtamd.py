@@ -233,6 +233,7 @@ GROUP_SYMBOLS = {
     "rt_group_device_image": (_I, [_P, _P, _P]),
 }
 GATHER_AUTO, GATHER_RCCL, GATHER_COPY = 0, 1, 2
+FORMAT_RGBA32F, FORMAT_RGB32F, FORMAT_RGBA32F_IMAGE = 0, 1, 2  # rt_format
 GROUP_ID_BYTES = 128
 
 
@@ -516,10 +517,12 @@ class ComputeShader:
         self._chk(self._lib.rt_dispatch_rows_fmt(self._h, width, height, y0, stripe, step, out_rows,
                                                  C.c_void_p(dst_ptr), pitch, 1), "rt_dispatch_rows_fmt")
 
-    def dispatch_rows_ex(self, width, height, y0, stripe, period, out_rows, dst_ptr, pitch, rgb=False):
-        """rt_dispatch_rows_ex: stripes of `stripe` rows from y0, one every `period` rows."""
+    def dispatch_rows_ex(self, width, height, y0, stripe, period, out_rows, dst_ptr, pitch, rgb=False, fmt=None):
+        """rt_dispatch_rows_ex: stripes of `stripe` rows from y0, one every `period` rows.
+        fmt: FORMAT_RGBA32F / FORMAT_RGB32F / FORMAT_RGBA32F_IMAGE (default: RGB32F if rgb)."""
+        f = int(fmt) if fmt is not None else int(bool(rgb))
         self._chk(self._lib.rt_dispatch_rows_ex(self._h, width, height, y0, stripe, period, out_rows,
-                                                C.c_void_p(dst_ptr), pitch, int(bool(rgb))), "rt_dispatch_rows_ex")
+                                                C.c_void_p(dst_ptr), pitch, f), "rt_dispatch_rows_ex")
 
     def sync(self):
         self._chk(self._lib.rt_sync(self._h), "rt_sync")

@@ -18,6 +18,13 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
 
 
+# bench.py runs F = 3 frames in flight at 1080p on 2F hardware queues
+# (bench.plan_inflight); the GPU tests that mirror it need the same, and HIP reads
+# the count once, when the runtime starts (before any test touches the GPU).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 6:
+    os.environ["GPU_MAX_HW_QUEUES"] = "6"
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 

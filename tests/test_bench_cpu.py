@@ -90,6 +90,9 @@ def test_inflight_plan_and_hardware_queues():
     assert bench.plan_inflight(0, 800, 600, 1, False, False, "4") == (4, "8")
     # a rank's 1/8 stripe share over rt_group: 8 frames, 16 queues
     assert bench.plan_inflight(0, 1920, 1080, 8, True, True, "4") == (8, "16")
+    # one rank over rt_group renders the single-GPU frame: the frames mode's F (round 3 gave it 2)
+    assert bench.plan_inflight(0, 1920, 1080, 1, True, True, "4") == (3, "6")
+    assert bench.plan_inflight(0, 1920, 1080, 2, True, True, "4") == (3, "6")
     # torch-gather strong path: one frame
     assert bench.plan_inflight(0, 1920, 1080, 2, True, False, "4") == (1, None)
     # an explicit F; never above 32 queues; an export that already suffices is kept
@@ -129,3 +132,18 @@ def test_roofline_names_the_binding_resource():
     # an HBM-heavy kernel keeps "hbm"
     r2 = bench.roofline(info, "k", 0.3, 1920 * 1080, 0.0, {"bytes": 2e9, "source": "x", "issue": iss})
     assert r2["bound"] == "hbm"
+
+
+def test_strong_roofline_is_latency_with_scaled_issue_floors():
+    """A strong line's kernel renders 1/P of the rows: the single-GPU PMC entry's
+    DRAM bytes are not its own (traffic null), its issue floors scale by the row
+    share, and the line names the latency bound rather than defaulting to hbm."""
+    info = {"record_bytes": 1_000_000}
+    iss = {"valu_floor_ms": 0.08, "salu_floor_ms": 0.07, "wait_frac": 0.3, "valu_busy": 0.6}
+    pmc = {"bytes": 39e6, "source": "x", "issue": iss}
+    r = bench.roofline(info, "k_accel", 0.05, 1920 * 135, 1e11, pmc, share=0.125)
+    assert r["traffic"] is None and r["traffic_over_algorithmic"] is None
+    assert r["achieved"] == pytest.approx((16 * 1920 * 135 + 1e6) / 0.05e-3 / 1e9)
+    assert r["issue"]["valu_floor_ms"] == pytest.approx(0.01) and r["issue"]["row_share"] == 0.125
+    assert r["issue"]["frac"] == pytest.approx(0.01 / 0.05)
+    assert r["bound"] == "latency" and "row share" in r["issue"]["basis"]

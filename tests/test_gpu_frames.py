@@ -396,6 +396,30 @@ def test_rgb_format_equals_rgba(ctx):
         ctx.dispatch_rows_rgb(W, H, y0, 8, 1, rows, out.data_ptr(), W * 12 - 4)
 
 
+@pytest.mark.parametrize("y0,stripe,period,rows", [(0, 16, 24, 720), (8, 8, 64, 136), (0, 1080, 1080, 1080)],
+                         ids=["root_share2_of_3", "rank1_of_8", "all_rows"])
+def test_image_rows_format_writes_in_place(ctx, y0, stripe, period, rows):
+    """RT_FORMAT_RGBA32F_IMAGE (rt_group's rank 0): each rendered row lands at its
+    image row of a whole W x H surface, equal to the single dispatch there, and every
+    other row keeps what was in it."""
+    W, H = 1920, 1080
+    fs = rtamd.generate(3, 0, W, H)
+    rgba = render(ctx, fs, W, H, 3)
+    out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.dispatch_rows_ex(W, H, y0, stripe, period, rows, out.data_ptr(), W * 16, fmt=rtamd.FORMAT_RGBA32F_IMAGE)
+    ctx.sync()
+    got = out.cpu().numpy()
+    mine = np.array([y0 + (r // stripe) * period + r % stripe for r in range(rows)])
+    mine = mine[mine < H]
+    assert np.array_equal(got[mine], rgba[mine])
+    rest = np.setdiff1d(np.arange(H), mine)
+    assert (got[rest] == -7.0).all()
+    with pytest.raises(rtamd.RTError):  # the pitch must hold 16 B per pixel
+        ctx.dispatch_rows_ex(W, H, y0, stripe, period, rows, out.data_ptr(), W * 12,
+                             fmt=rtamd.FORMAT_RGBA32F_IMAGE)
+
+
 # --------------------------------------------------------------------------
 # The reference's default scene (SCENE = 3, generateScene3, src/main.cpp:1196-1229)
 
@@ -440,14 +464,20 @@ def car_full_ref():
 
 
 def test_bench_steady_state_frames_vs_oracle(car_full_ref):
-    """What bench.py times: two contexts on their own streams, frames dealt
-    round-robin with nothing waited on between them, the cost-ordered schedule
-    (re-derived every 8th dispatch; the dispatches between run the counter-free
-    instance with the auto lane_k slots), 1920x1080, depth 3. Each of the 24
-    frames goes to its own buffer and every one is checked against one full-frame
-    oracle render (gpu_shader.comp:433-624)."""
+    """What bench.py times: F contexts on their own streams (F = the bench's own
+    plan, 3 at 1080p), frames dealt round-robin with nothing waited on between
+    them, the cost-ordered schedule (re-derived every 8th dispatch; the dispatches
+    between run the counter-free instance with the auto lane_k slots), 1920x1080,
+    depth 3, on 2F hardware queues (tests/conftest.py raises GPU_MAX_HW_QUEUES
+    before the runtime starts, as bench.py does). Each of the 24 frames goes to its
+    own buffer and every one is checked against one full-frame oracle render
+    (gpu_shader.comp:433-624)."""
+    import bench
     fs, ref = car_full_ref
-    W, H, F, n = 1920, 1080, 2, 24
+    W, H, n = 1920, 1080, 24
+    F, _ = bench.plan_inflight(0, W, H, 1, False, False, "4")
+    assert F == 3
+    assert int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) >= 2 * F
     streams = [torch.cuda.Stream() for _ in range(F)]
     ctxs = []
     try:
@@ -512,7 +542,7 @@ def _in_flight_check(ctx, g, fs, W, H, stripe):
         assert np.array_equal(img, refs[(n - 1) % len(cams)]), f"{n} frames in flight"
 
 
-@pytest.mark.parametrize("ranks,frames,share", [(8, 3, 1), (4, 8, 2), (2, 2, 1)])
+@pytest.mark.parametrize("ranks,frames,share", [(8, 3, 1), (4, 8, 2), (2, 2, 1), (8, 8, 1), (8, 8, 2)])
 def test_group_frames_in_flight_copy(ctx, ranks, frames, share):
     W, H = 480, 270
     fs = rtamd.generate(3, 0, W, H)
@@ -543,6 +573,7 @@ def test_rccl_rank_group_frames_in_flight(ctx):
         g.check()
         g.sync()
         ph = g.phase_times()
-        assert ph["frames"] > 0 and ph["render_ms"] > 0 and ph["unstripe_ms"] > 0
+        # one rank renders the single-GPU frame straight into its surface: no fan-in, no scatter
+        assert ph["frames"] > 0 and ph["render_ms"] > 0 and ph["unstripe_ms"] == 0 and ph["fanin_ms"] == 0
     finally:
         g.close()
