@@ -90,8 +90,9 @@ def parse(argv=None):
     ap.add_argument("--mt", action="store_true", help="useMollerTrumbore = 1 (gpu_shader.comp:170-195)")
     ap.add_argument("--fresnel", action="store_true", help="useFresnel = 1 (gpu_shader.comp:500-509)")
     ap.add_argument("--animate", action="store_true",
-                    help="config 3: the four wheels turn every frame (updateWheelAnimations, src/main.cpp:1084-1109) "
-                         "and the tree is refit on the device (rt_animate) inside the timed step")
+                    help="the reference's animations, refit on the device (rt_animate) inside the timed step: "
+                         "config 2 = scene 1's three bouncing spheres (bounceSphere, src/main.cpp:438-445); "
+                         "configs 3/4 = the car's four wheels turning (updateWheelAnimations, :1084-1109)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU; 0 = auto: 3 below 64k 8x8 tiles (1080p), 2 above (4K), up "
                          "to 4 while the GPU's share of a frame has fewer than 16k tiles; strong mode over "
@@ -263,6 +264,48 @@ def wheel_frames(fs, n):
                               + cen[w]).astype(np.float32)
         frames.append(rec)
     return ids, frames
+
+
+# bounceSphere(sphere, currentFrame, amplitude, frequency) on scene 1's first three
+# spheres (src/main.cpp:438-445; animatedIndices, :600-616)
+BOUNCES = ((10.0, 1.0), (7.0, 0.8), (15.0, 1.5))
+
+
+def sphere_frames(fs, n):
+    """Records of scene 1's three bouncing spheres for n frames 1/60 s apart:
+    centre.y = origin.y + amplitude * sin(frequency * t) in float32, as bounceSphere
+    sets it (src/main.cpp:1079-1082); the generator's shapes 0-2 are those spheres
+    (csrc/scene.cpp scene1_spheres). n = 512 frames spans 8.5 s, a full period of
+    the slowest bounce (2 pi / 0.8 s)."""
+    import numpy as np
+    ids = np.arange(3, dtype=np.int32)
+    base = fs.shapes[ids].copy()
+    if not (base["type"] == 0).all():
+        raise SystemExit("--animate on config 2: shapes 0-2 must be scene 1's spheres")
+    frames = []
+    for f in range(n):
+        t = np.float32(f / 60.0)
+        rec = base.copy()
+        for k, (amp, fr) in enumerate(BOUNCES):
+            rec["sphereCenter"][k][1] = base["sphereCenter"][k][1] + np.float32(amp) * np.sin(np.float32(fr) * t)
+        frames.append(rec)
+    return ids, frames
+
+
+def animated_oracle_scene(fs, ids, frames, applied):
+    """The scene one renderer holds after rt_animate was given frames[j] for every j in
+    `applied` (in that order): the last frame's records, and the node boxes updateBVH
+    grew to hold every frame's records (grow-only, src/main.cpp:1068-1077; restated
+    by oracle.update_bvh). Growing is a union, so each distinct frame is applied once."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (checker only)
+    import rtamd  # noqa: E402
+    fk = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    for j in sorted(set(applied)):
+        fk.shapes[ids] = frames[j]
+        oracle.update_bvh(fk, ids)
+    fk.shapes[ids] = frames[applied[-1]]
+    return fk
 
 
 def pmc_entry(key):
@@ -465,12 +508,16 @@ def main():
     rays_step, b_ref_rank, rows = count_work()
 
     cam, light = fs.camera, fs.light
-    anim = wheel_frames(fs, 64) if a.animate else None
-    if anim is not None:
-        if use_group or a.config not in (3, 4):
-            raise SystemExit("--animate: configs 3/4 on one GPU or weak mode")
+    anim = None
+    if a.animate:
+        if use_group or a.config not in (2, 3, 4):
+            raise SystemExit("--animate: configs 2/3/4 on one GPU or weak mode")
+        # the published scenes' animations (README.md:4): scene 1's bouncing spheres
+        # (config 2), scene 2's turning wheels (configs 3/4)
+        anim = sphere_frames(fs, 512) if a.config == 2 else wheel_frames(fs, 64)
         for c_ in ctxs:
             c_.set_animated(anim[0])
+    applied = [[] for _ in ctxs]  # per renderer: the animation frames it was given, in order
 
     def frame(i, inflight):
         if use_group:
@@ -485,6 +532,7 @@ def main():
         c_.set_light(light)
         if anim is not None:
             c_.animate(anim[1][i % len(anim[1])])  # updateScene + updateBVH on the device
+            applied[i % inflight].append(i % len(anim[1]))
         buf = bufs[i % inflight]
         c_.dispatch_rows(W, H, plan.y0(prank), a.stripe, plan.world, rows, buf.data_ptr(), W * 16)
         if strong:
@@ -688,7 +736,10 @@ def main():
             "config": {"workload": f"config {a.config}: {desc}" + (" (222-strip road)" if a.variant else ""),
                        "width": W, "height": H, "maxBounces": mb, "useBVH": int(not a.brute),
                        "useFresnel": int(a.fresnel), "triangle_test": "moller-trumbore" if a.mt else "barycentric",
-                       "animate": "wheels turn, device refit per frame" if a.animate else None, "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
+                       "animate": (None if not a.animate else
+                                   "scene 1's three spheres bounce (bounceSphere, src/main.cpp:438-445), "
+                                   "device refit per frame" if a.config == 2 else
+                                   "wheels turn (updateWheelAnimations), device refit per frame"), "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
                        "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel, "walk": a.walk,
                        "parallelism": (f"row-stripes{a.stripe}x{world}+gather" if strong else
                                        f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"
@@ -715,6 +766,28 @@ def main():
                                                (not a.brute, a.fresnel, a.mt))
             out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2, cfg, a.variant,
                                                                             W, H)
+        if mode == "frames" and anim is not None:
+            # every renderer's last timed frame against the oracle rendering that
+            # renderer's scene: the last animated records and the boxes grown by every
+            # frame it was given (outside the timed region; whole frames)
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle  # noqa: E402  (checker only)
+            torch.cuda.synchronize()
+            checks = []
+            for k, b_ in enumerate(bufs):
+                if not applied[k]:
+                    continue
+                fk = animated_oracle_scene(fs, anim[0], anim[1], applied[k])
+                ref, _ = oracle.render(fk, W, H, oracle.params(W, H, mb, not a.brute, a.fresnel, a.mt), threads=thr)
+                checks.append(parity_check([b_.cpu().numpy()], 0, ref, ""))
+            out["parity"] = {"max_abs": max(c["max_abs"] for c in checks),
+                             "bad_pixels": sum(c["bad_pixels"] for c in checks), "frames_checked": len(checks),
+                             "tol": PARITY_TOL, "rows_checked": [0, H],
+                             "against": ("oracle/rt_oracle.c (GLSL restated) on each renderer's animated scene: "
+                                         "its last frame's records, node boxes grown by oracle.update_bvh "
+                                         "(updateBVH restated) over every frame it was given"),
+                             "animation_frames_applied": [len(x) for x in applied],
+                             "ok": all(c["ok"] for c in checks)}
         if mode == "frames" and anim is None:
             # the timed frames themselves, against the oracle (outside the timed region)
             if out["cpu_baseline"] is not None:

@@ -147,3 +147,30 @@ def test_strong_roofline_is_latency_with_scaled_issue_floors():
     assert r["issue"]["valu_floor_ms"] == pytest.approx(0.01) and r["issue"]["row_share"] == 0.125
     assert r["issue"]["frac"] == pytest.approx(0.01 / 0.05)
     assert r["bound"] == "latency" and "row share" in r["issue"]["basis"]
+
+
+def test_bouncing_spheres_and_their_oracle_scene():
+    """bench --animate on config 2: scene 1's spheres 0-2 bounce as bounceSphere sets
+    them (src/main.cpp:438-445, 1079-1082), and the oracle scene of a renderer that was
+    given frames j1, j2, ... holds the last frame's records and node boxes grown to
+    every frame's spheres (updateBVH is grow-only)."""
+    fs = rtamd.generate(2, 0, 800, 600)
+    ids, frames = bench.sphere_frames(fs, 512)
+    assert list(ids) == [0, 1, 2] and len(frames) == 512
+    base = fs.shapes[ids]
+    for f in (0, 1, 77, 511):
+        t = np.float32(f / 60.0)
+        for k, (amp, fr) in enumerate(bench.BOUNCES):
+            want = base["sphereCenter"][k][1] + np.float32(amp) * np.sin(np.float32(fr) * t)
+            assert frames[f]["sphereCenter"][k][1] == want
+            assert np.array_equal(frames[f]["sphereCenter"][k][[0, 2]], base["sphereCenter"][k][[0, 2]])
+    applied = [3, 100, 250, 7]
+    fk = bench.animated_oracle_scene(fs, ids, frames, applied)
+    assert np.array_equal(fk.shapes[ids], frames[7]) and np.array_equal(fk.shapes[3:], fs.shapes[3:])
+    assert np.array_equal(fs.shapes[ids], base)  # the caller's scene is untouched
+    root = fk.nodes[-1]
+    for j in applied:
+        c, r = frames[j]["sphereCenter"], frames[j]["sphereRadius"]
+        assert (root["boundsMin"] <= (c - r[:, None]).min(0)).all()
+        assert (root["boundsMax"] >= (c + r[:, None]).max(0)).all()
+    assert (fk.nodes["boundsMin"] <= fs.nodes["boundsMin"]).all()  # grow-only

@@ -21,3 +21,8 @@ for f in ("bench_r04a", "bench_r04a_strong1"):
                                      "serial_frame_ms_median", "kernel_ms_mean", "group_phases_ms", "parity")})
     print("   roofline", {k: d["roofline"].get(k) for k in ("bound", "frac", "traffic")})
 PY
+for c in 2 3; do
+  timeout -k 10 300 python bench.py --config $c --animate --no-cpu --steps 100 --warmup 10 > gpurun_out/bench_r04a_anim_c$c.json 2> gpurun_out/bench_r04a_anim_c$c.err; rc=$?
+  echo "bench animate c$c rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/bench_r04a_anim_c$c.err; exit $rc; }
+  python -c "import json; d=json.load(open('gpurun_out/bench_r04a_anim_c$c.json')); print({k: d.get(k) for k in ('ms_per_step','serial_ms_per_step','serial_frame_ms_median','parity')})"
+done
