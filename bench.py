@@ -549,6 +549,18 @@ def main():
             print(f"bench.py rank {rank}: {e}", file=sys.stderr, flush=True)
             os._exit(4)
 
+    def set_timing(on):
+        """The renderers' device-time events (rt_set_kernel_timing; over rt_group also the
+        phase events, rt_group_set_phase_timing). Each is a timestamped marker on the
+        stream: a production loop records none, and they cost the car ~2 % in flight and
+        ~5 us per waited frame (tools/group_cost.py, profiles/r04_group_cost.json). The
+        passes that report device times record them; the timed frames and the waited
+        frames do not."""
+        for c_ in ctxs:
+            c_.set_kernel_timing(on)
+        if grp is not None:
+            grp.set_phase_timing(on)
+
     def timed(inflight):
         """Wall time of a.steps frames between barriers, max over ranks."""
         for i in range(a.warmup * inflight):
@@ -613,19 +625,22 @@ def main():
         share_probe = {}
         steps = a.steps
         a.steps = max(4, 2 * F)
+        set_timing(False)  # as the measured pass runs
         # rank 0's rows never cross a link: with more peers a larger share moves fewer bytes
         for k in ((1,) if world == 1 else (1, 2) if world < 4 else (1, 2, 3, 4)):
             grp.set_root_share(k)
             share_probe[k] = timed(F) / a.steps * 1e3
         a.steps = steps
+        set_timing(True)
         best = min(share_probe, key=share_probe.get)
         grp.set_root_share(best)
         share = best
         share_probe = {str(k): v for k, v in share_probe.items()}
         rays_step, b_ref_rank, rows = count_work()  # this rank's rows at the chosen share
 
-    serial = timed(1) if F > 1 else None
+    serial = timed(1) if F > 1 else None  # device times recorded: the roofline's kernel time
     serial_kt = ctx.kernel_times() if F > 1 else None
+    set_timing(F == 1)  # F = 1 (the profilers' --inflight 1): the main pass is the device-time pass
     # SURVEY §8(d)'s frame: upload + dispatch + completion, one at a time, FPS = 1 / median.
     # Each frame waits for its completion (the reference's loop, src/main.cpp:290-462), with
     # rt_set_latency_mode on: the setting for a host that waits for every frame.
@@ -674,6 +689,14 @@ def main():
         ctx.set_latency_mode(0)
         ctx.kernel_times()
     elapsed = timed(F)
+    if F > 1:
+        # the same frames in flight again with the device-time events, for the phase
+        # times and kernel_ms_mean_inflight only (not timed)
+        set_timing(True)
+        steps = a.steps
+        a.steps = max(2 * F, steps // 2)
+        timed(F)
+        a.steps = steps
 
     kt_if = np.concatenate([c_.kernel_times() for c_ in ctxs])
     rank_phases = None

@@ -198,6 +198,13 @@ int rt_collect_stats(struct rt_ctx* ctx, int width, int height, int y0, int stri
 int rt_collect_stats_ex(struct rt_ctx* ctx, int width, int height, int y0, int stripe,
                         int period, int out_rows, rt_stats* out);
 
+/* Record the device-time events around each render dispatch (default 1), which
+ * rt_kernel_times / rt_last_kernel_ms read. Each is a timestamped marker on the
+ * stream, and a host that waits for every frame pays for them (~4 us per waited
+ * car frame, tools/group_cost.py). 0: no events; rt_kernel_times then reports
+ * no dispatches. Same image either way. */
+int rt_set_kernel_timing(struct rt_ctx* ctx, int on);
+
 /* Device time of the last render kernel in ms (HIP events on the context stream). */
 int rt_last_kernel_ms(struct rt_ctx* ctx, float* ms);
 

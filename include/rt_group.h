@@ -132,6 +132,9 @@ int rt_group_check(struct rt_group* g);
  * rendered, or on rank 0 the slot free -- to the last byte sent / received, so it
  * includes waiting for the slowest peer), rank 0's unstripe, and render start to
  * the frame's last event. Waits (bounded) for the outstanding frames. */
+/* Record the phase events above (default 1). 0: a frame records only the events
+ * its fan-in needs (none with one rank), and rt_group_phase_times reports 0 frames. */
+int rt_group_set_phase_timing(struct rt_group* g, int on);
 typedef struct rt_group_phases {
     int frames;
     float render_ms, fanin_ms, unstripe_ms, frame_ms;

@@ -36,6 +36,7 @@
 #include "../../include/rt_api.h"
 #include "../../include/rt_group.h"
 #include "group_wait.h"
+#include "rt_internal.h"
 
 namespace {
 
@@ -122,6 +123,7 @@ struct rt_group {
     bool have_scene = false;
     bool broken = false;        // an RCCL group after an abort: every call fails
     double timeout_ms = 60000;  // rt_group_set_timeout
+    bool phase_timing = true;   // rt_group_set_phase_timing
     // phase times of member `tm` (rank 0 when local, else the first member)
     int tm = 0;
     std::vector<PhaseRec> ring;
@@ -149,13 +151,12 @@ namespace {
 int add_slot(Member& b) {
     b.slot.emplace_back();
     Slot& s = b.slot.back();
-    G_TRY(rt_create(&s.ctx, b.device));
     G_HIP(hipSetDevice(b.device));
     G_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     G_HIP(hipEventCreateWithFlags(&s.rendered, hipEventDisableTiming));
     G_HIP(hipEventCreateWithFlags(&s.fanned, hipEventDisableTiming));
     G_HIP(hipEventCreateWithFlags(&s.released, hipEventDisableTiming));
-    return rt_set_stream(s.ctx, s.stream);
+    return rtx::create_ctx(&s.ctx, b.device, s.stream);  // straight on the slot's stream (rt_internal.h)
 }
 
 int add_member(rt_group* g, int rank, int device) {
@@ -506,10 +507,21 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         // kPhaseRing frames ago. Nothing makes the host wait between dispatches, so that
         // frame may still be pending (a peer that never posts its send): never block on
         // it unbounded -- the group's bounded wait decides (RT_ERR_TIMEOUT, comms aborted).
+        // Only that frame's last event is waited for (the host may run up to kPhaseRing
+        // frames ahead; draining every stream here would empty the pipeline).
         F_HIP(hipSetDevice(g->m[g->tm].device));
-        const hipError_t q = hipEventQuery(ph.ev[ph.has_unstripe ? 5 : (ph.has_fan ? 3 : 1)]);
-        if (q == hipErrorNotReady) G_TRY(wait_all(g));
-        else if (q != hipSuccess) return fail(g, RT_ERR_DEVICE);
+        const hipEvent_t last = ph.ev[ph.has_unstripe ? 5 : (ph.has_fan ? 3 : 1)];
+        const rtg::WaitResult w = rtg::wait_bounded(
+            [last] {
+                const hipError_t e = hipEventQuery(last);
+                return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+            },
+            [g] { return comm_error(g); }, g->timeout_ms);
+        if (w == rtg::kWaitDeviceError) return fail(g, RT_ERR_DEVICE);
+        if (w != rtg::kWaitDone) {
+            abort_comms(g);
+            return w == rtg::kWaitTimeout ? RT_ERR_TIMEOUT : RT_ERR_COMM;
+        }
         harvest(g, ph);
     }
     ph.has_fan = ph.has_unstripe = false;
@@ -519,7 +531,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     for (size_t mi = 0; mi < g->m.size(); ++mi) {
         Member& b = g->m[mi];
         Slot& s = b.slot[j];
-        const bool timed = static_cast<int>(mi) == g->tm;
+        const bool timed = g->phase_timing && static_cast<int>(mi) == g->tm;
         F_HIP(hipSetDevice(b.device));
         if (s.used && b.rank != 0) {
             // RCCL: released on this member's fan-in stream; copies: rank 0's copy of it
@@ -536,7 +548,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             if (rc != RT_OK) return fail(g, rc);
         }
         if (timed) F_HIP(hipEventRecord(ph.ev[1], s.stream));
-        F_HIP(hipEventRecord(s.rendered, s.stream));
+        if (P > 1) F_HIP(hipEventRecord(s.rendered, s.stream));  // the fan-in waits for it
     }
     auto slot_ptr = [&](int rank) {  // rank's rows in slot j's staging buffer (rank >= 1)
         return reinterpret_cast<char*>(g->m[g->root].slot[j].staging) + static_cast<size_t>(rank - 1) * rows1 * row_b;
@@ -550,7 +562,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             // a sender waits for its rows; rank 0 for the previous unstripe of this slot's staging
             const hipEvent_t before = b.rank == 0 ? (s.used ? s.released : nullptr) : s.rendered;
             if (before) F_HIP(hipStreamWaitEvent(b.cstream, before, 0));
-            if (static_cast<int>(mi) == g->tm) F_HIP(hipEventRecord(ph.ev[2], b.cstream));
+            if (g->phase_timing && static_cast<int>(mi) == g->tm) F_HIP(hipEventRecord(ph.ev[2], b.cstream));
         }
         if (ncclGroupStart() != ncclSuccess) return fail(g, RT_ERR_COMM);
         for (Member& b : g->m) {
@@ -575,7 +587,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             Member& b = g->m[mi];
             Slot& s = b.slot[j];
             F_HIP(hipSetDevice(b.device));
-            if (static_cast<int>(mi) == g->tm) {
+            if (g->phase_timing && static_cast<int>(mi) == g->tm) {
                 F_HIP(hipEventRecord(ph.ev[3], b.cstream));
                 ph.has_fan = true;
             }
@@ -590,7 +602,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         Slot& rs = r.slot[j];
         F_HIP(hipSetDevice(r.device));
         if (rs.used) F_HIP(hipStreamWaitEvent(r.cstream, rs.released, 0));
-        if (g->tm == g->root) F_HIP(hipEventRecord(ph.ev[2], r.cstream));
+        if (g->phase_timing && g->tm == g->root) F_HIP(hipEventRecord(ph.ev[2], r.cstream));
         for (Member& b : g->m) {
             if (b.rank == 0) continue;
             const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, b.rank).rows) * row_b;
@@ -598,7 +610,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             if (n) F_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank), r.device, b.slot[j].buf, b.device, n, r.cstream));
             b.slot[j].used = true;  // its next render waits for rs.fanned
         }
-        if (g->tm == g->root) {
+        if (g->phase_timing && g->tm == g->root) {
             F_HIP(hipEventRecord(ph.ev[3], r.cstream));
             ph.has_fan = true;
         }
@@ -612,22 +624,25 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         F_HIP(hipSetDevice(r.device));
         if (P > 1 && rows1 > 0) {
             F_HIP(hipStreamWaitEvent(rs.stream, rs.fanned, 0));
-            if (g->tm == g->root) F_HIP(hipEventRecord(ph.ev[4], rs.stream));
+            if (g->phase_timing && g->tm == g->root) F_HIP(hipEventRecord(ph.ev[4], rs.stream));
             hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, (P - 1) * rows1), dim3(256), 0, rs.stream,
                                rs.staging, rows1, width, height, stripe, k, P, reinterpret_cast<f4v*>(rs.img),
                                rs.img_pitch / 16);
             F_HIP(hipGetLastError());
-            if (g->tm == g->root) {
+            if (g->phase_timing && g->tm == g->root) {
                 F_HIP(hipEventRecord(ph.ev[5], rs.stream));
                 ph.has_unstripe = true;
             }
         }
-        F_HIP(hipEventRecord(rs.released, rs.stream));
-        rs.used = true;
+        // the next fan-in into this slot's staging waits for it (one rank: no fan-in)
+        if (P > 1) {
+            F_HIP(hipEventRecord(rs.released, rs.stream));
+            rs.used = true;
+        }
     }
 #undef F_HIP
 #undef F_TRY
-    ph.pending = true;
+    ph.pending = g->phase_timing;
     g->ring_pos = (g->ring_pos + 1) % kPhaseRing;
     g->last_slot = j;
     ++g->next;
@@ -654,6 +669,12 @@ int rt_group_collect_stats(rt_group* g, int width, int height, int stripe, rt_st
         const uint64_t* a = reinterpret_cast<const uint64_t*>(&st);
         for (size_t i = 0; i < sizeof st / sizeof(uint64_t); ++i) o[i] += a[i];
     }
+    return RT_OK;
+}
+
+int rt_group_set_phase_timing(rt_group* g, int on) {
+    if (!g) return RT_ERR_INVALID;
+    g->phase_timing = on != 0;
     return RT_OK;
 }
 

@@ -39,6 +39,7 @@
 #include "lbvh.h"
 #include "rt_device.h"
 #include "group_wait.h"
+#include "rt_internal.h"
 
 using namespace rtd;
 
@@ -2171,6 +2172,7 @@ struct rt_ctx {
     // per-dispatch event pairs since the last rt_kernel_times call
     std::vector<hipEvent_t> ring0, ring1;
     int ring_used = 0;
+    bool timing = true;  // rt_set_kernel_timing: record the ring's events around each render
     // scene
     float4 *geo_lin = nullptr, *geo_leaf = nullptr, *mat = nullptr, *nodes = nullptr;
     int S = 0, N = 0, I = 0, max_stack = 1;
@@ -2889,10 +2891,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats);
 // A sub-context on this context's stream (brute / mtc), created on first use.
 rt_ctx* sub_ctx(rt_ctx* c, rt_ctx*& sub, bool& stale) {
     if (!sub) {
-        if (rt_create(&sub, c->device) != RT_OK) return nullptr;
-        hipStreamDestroy(sub->stream);
-        sub->stream = c->stream;
-        sub->own_stream = false;
+        if (rtx::create_ctx(&sub, c->device, c->stream) != RT_OK) return nullptr;
         stale = true;
     }
     return sub;
@@ -3016,6 +3015,12 @@ int render(rt_ctx* c, const KParams& kp) {
         kt = kn;
     }
     if (t == c || !accel_usable(t, kt)) return launch(c, kp, false);
+    t->timing = false;  // the sub-context's own events would not be read: this context's time it
+    if (!c->timing) {
+        const int rc = launch(t, kt, false);
+        c->last_kind = t->last_kind;
+        return rc;
+    }
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (c->ring_used < static_cast<int>(c->ring0.size())) {
         e0 = c->ring0[c->ring_used];
@@ -3043,12 +3048,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     if (kind == RT_KERNEL_AUTO) kind = usable ? RT_KERNEL_ACCEL : RT_KERNEL_PACKET;
     if (kind == RT_KERNEL_ACCEL && !usable) kind = RT_KERNEL_PACKET;  // same image either way
     const size_t lds = static_cast<size_t>(kp.max_stack) * kBlock * sizeof(int);
+    const bool rec = !stats && c->timing;  // rt_set_kernel_timing
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
-    if (!stats && c->ring_used < static_cast<int>(c->ring0.size())) {
+    if (rec && c->ring_used < static_cast<int>(c->ring0.size())) {
         e0 = c->ring0[c->ring_used];
         e1 = c->ring1[c->ring_used];
     }
-    if (!stats) HIP_TRY(hipEventRecord(e0, c->stream));
+    if (rec) HIP_TRY(hipEventRecord(e0, c->stream));
     bool order_after = false;  // e1 already recorded between the render and the order kernel
     if (stats) {
         hipLaunchKernelGGL(k_lane<true>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
@@ -3252,7 +3258,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         if (k2.tile_cost) {
             // the next frame's order; stream-ordered after this dispatch (and after its
             // end event, so rt_kernel_times is the render kernel alone), before the next
-            if (!stats) HIP_TRY(hipEventRecord(e1, c->stream));
+            if (rec) HIP_TRY(hipEventRecord(e1, c->stream));
             order_after = true;
             unsigned* set = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
             unsigned* next = c->sched_sets + (1 - c->sched_parity) * sched_set_words(c->sched_cap);
@@ -3269,7 +3275,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
     }
     c->last_kind = stats ? RT_KERNEL_LANE : kind;
     HIP_TRY(hipGetLastError());
-    if (!stats) {
+    if (rec) {
         if (!order_after) HIP_TRY(hipEventRecord(e1, c->stream));
         c->last0 = e0;
         c->last1 = e1;
@@ -3298,7 +3304,11 @@ const char* rt_status_string(int s) {
     }
 }
 
-int rt_create(rt_ctx** out, int device) {
+int rt_create(rt_ctx** out, int device) { return rtx::create_ctx(out, device, nullptr); }
+
+}  // extern "C"
+
+int rtx::create_ctx(rt_ctx** out, int device, hipStream_t stream) {
     if (!out) return RT_ERR_INVALID;
     *out = nullptr;
     int n = 0;
@@ -3306,14 +3316,15 @@ int rt_create(rt_ctx** out, int device) {
     rt_ctx* c = new (std::nothrow) rt_ctx();
     if (!c) return RT_ERR_NO_MEMORY;
     c->device = device;
-    if (set_dev(c) != RT_OK || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+    c->stream = stream;
+    if (set_dev(c) != RT_OK || (!stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->stats_dev, ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->tile_counter, 16) != hipSuccess) {
         rt_destroy(c);
         return RT_ERR_DEVICE;
     }
-    c->own_stream = true;
+    c->own_stream = !stream;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, device) == hipSuccess)
@@ -3330,6 +3341,8 @@ int rt_create(rt_ctx** out, int device) {
     *out = c;
     return RT_OK;
 }
+
+extern "C" {
 
 int rt_destroy(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
@@ -3878,6 +3891,12 @@ extern "C" int rt_debug_sched_period(rt_ctx* c, int period) {
 extern "C" int rt_debug_lane_stack(rt_ctx* c, int n) {
     if (!c || n < 0 || n > kMaxStack) return RT_ERR_INVALID;
     c->lane_stack_override = n;
+    return RT_OK;
+}
+
+extern "C" int rt_set_kernel_timing(rt_ctx* c, int on) {
+    if (!c) return RT_ERR_INVALID;
+    c->timing = on != 0;
     return RT_OK;
 }
 

@@ -204,6 +204,7 @@ RT_SYMBOLS = {
     "rt_read_indices": (_I, [_P, _P, _I]),
     "rt_set_schedule": (_I, [_P, _I]),
     "rt_set_latency_mode": (_I, [_P, _I]),
+    "rt_set_kernel_timing": (_I, [_P, _I]),
     "rt_set_tail": (_I, [_P, _I]),
     "rt_status_string": (C.c_char_p, [_I]),
 }
@@ -220,6 +221,7 @@ GROUP_SYMBOLS = {
     "rt_group_set_frames": (_I, [_P, _I]),
     "rt_group_frames": (_I, [_P]),
     "rt_group_set_timeout": (_I, [_P, C.c_double]),
+    "rt_group_set_phase_timing": (_I, [_P, _I]),
     "rt_group_check": (_I, [_P]),
     "rt_group_phase_times": (_I, [_P, _P]),
     "rt_group_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
@@ -598,6 +600,10 @@ class ComputeShader:
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(lanes)), "rt_debug_tail_lanes")
 
+    def set_kernel_timing(self, on):
+        """rt_set_kernel_timing: record the device-time events around each dispatch (default on)."""
+        self._chk(self._lib.rt_set_kernel_timing(self._h, int(bool(on))), "rt_set_kernel_timing")
+
     def set_latency_mode(self, on):
         """rt_set_latency_mode: tune for one frame at a time (split walks, heaviest tiles as 2 waves)."""
         self._chk(self._lib.rt_set_latency_mode(self._h, int(bool(on))), "rt_set_latency_mode")
@@ -818,6 +824,10 @@ class Group:
     def check(self):
         """Non-blocking RCCL asynchronous-error poll (rt_group_check)."""
         self._chk(self._lib.rt_group_check(self._h), "rt_group_check")
+
+    def set_phase_timing(self, on):
+        """rt_group_set_phase_timing: record the render / fan-in / unstripe events (default on)."""
+        self._chk(self._lib.rt_group_set_phase_timing(self._h, int(bool(on))), "rt_group_set_phase_timing")
 
     def phase_times(self):
         """Mean device ms of render / fan-in / unstripe / whole frame since the last call."""
