@@ -152,7 +152,7 @@ int add_slot(Member& b) {
     b.slot.emplace_back();
     Slot& s = b.slot.back();
     G_HIP(hipSetDevice(b.device));
-    G_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    G_HIP(rtx::make_stream(&s.stream, true));  // a hardware queue per slot (rt_internal.h)
     G_HIP(hipEventCreateWithFlags(&s.rendered, hipEventDisableTiming));
     G_HIP(hipEventCreateWithFlags(&s.fanned, hipEventDisableTiming));
     G_HIP(hipEventCreateWithFlags(&s.released, hipEventDisableTiming));
@@ -166,7 +166,7 @@ int add_member(rt_group* g, int rank, int device) {
     g->m.push_back(mb);  // owned from here (rt_group_destroy frees it)
     Member& b = g->m.back();
     G_HIP(hipSetDevice(device));
-    G_HIP(hipStreamCreateWithFlags(&b.cstream, hipStreamNonBlocking));
+    G_HIP(rtx::make_stream(&b.cstream, true));
     return add_slot(b);
 }
 
@@ -211,14 +211,21 @@ int fail(rt_group* g, int rc) {
 }
 
 // Outstanding work on any of the group's streams: 1 yes, 0 none, -1 device error.
+// The last dispatched frame's slot first: while it runs (the usual case in a wait)
+// one query answers.
 int pending(rt_group* g) {
+    auto q = [](hipStream_t s) {
+        if (!s) return 0;
+        const hipError_t e = hipStreamQuery(s);
+        return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+    };
+    if (g->last_slot >= 0)
+        for (Member& b : g->m)
+            if (g->last_slot < static_cast<int>(b.slot.size())) {
+                const int r = q(b.slot[g->last_slot].stream);
+                if (r) return r;
+            }
     for (Member& b : g->m) {
-        if (hipSetDevice(b.device) != hipSuccess) return -1;
-        auto q = [](hipStream_t s) {
-            if (!s) return 0;
-            const hipError_t e = hipStreamQuery(s);
-            return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
-        };
         int r = q(b.cstream);
         if (r) return r;
         for (Slot& s : b.slot)

@@ -16,4 +16,14 @@ namespace rtx {
 // deal, so that frame slots end up sharing a queue and running in order.
 int create_ctx(rt_ctx** out, int device, hipStream_t stream);
 
+// A non-blocking stream of the current device. own_queue: created with a full CU
+// mask (hipExtStreamCreateWithCUMask), which HIP backs with a hardware queue of
+// its own instead of dealing it onto one of the GPU_MAX_HW_QUEUES shared queues
+// (falls back to a plain stream if that fails). rt_group's frame slots take it:
+// with shared queues two of a 1-rank group's three slots landed on one queue and
+// ran in order (1080p car 0.216 ms per frame against 0.184 with own queues and
+// 0.183 in frames mode; profiles/r04c_strong1_queues.txt). Contexts made by
+// rt_create take it when RT_STREAMS_CUMASK=1 is set.
+hipError_t make_stream(hipStream_t* s, bool own_queue);
+
 }  // namespace rtx

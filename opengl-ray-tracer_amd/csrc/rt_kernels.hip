@@ -27,6 +27,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <limits>
@@ -3308,6 +3309,30 @@ int rt_create(rt_ctx** out, int device) { return rtx::create_ctx(out, device, nu
 
 }  // extern "C"
 
+hipError_t rtx::make_stream(hipStream_t* s, bool own_queue) {
+    if (own_queue) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess &&
+            prop.multiProcessorCount > 0) {
+            std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0xffffffffu);
+            if (hipExtStreamCreateWithCUMask(s, static_cast<uint32_t>(mask.size()), mask.data()) == hipSuccess)
+                return hipSuccess;
+        }
+    }
+    return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+}
+
+namespace {
+bool env_cumask() {
+    static const bool on = [] {
+        const char* e = std::getenv("RT_STREAMS_CUMASK");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+}  // namespace
+
 int rtx::create_ctx(rt_ctx** out, int device, hipStream_t stream) {
     if (!out) return RT_ERR_INVALID;
     *out = nullptr;
@@ -3317,7 +3342,7 @@ int rtx::create_ctx(rt_ctx** out, int device, hipStream_t stream) {
     if (!c) return RT_ERR_NO_MEMORY;
     c->device = device;
     c->stream = stream;
-    if (set_dev(c) != RT_OK || (!stream && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) ||
+    if (set_dev(c) != RT_OK || (!stream && rtx::make_stream(&c->stream, env_cumask()) != hipSuccess) ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipMalloc(&c->stats_dev, ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->tile_counter, 16) != hipSuccess) {

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <vector>
 
 #include "../../opengl-ray-tracer_amd/csrc/group_wait.h"
 
@@ -38,21 +39,22 @@ int main() {
     EXPECT(wait_bounded([] { return 0; }, [] { return true; }, 1000.0) == kWaitDone);
     // a frame that ends 300 us in is seen within a poll, not after a nap (round 3's
     // back-off slept 20 -> 320 us between polls: a 0.27 ms frame was seen at ~0.35 ms)
-    double late_max = 0.0;
-    for (int rep = 0; rep < 20; ++rep) {
+    // (median of 21 waits: a loaded host may deschedule the polling thread now and then)
+    std::vector<double> late;
+    for (int rep = 0; rep < 21; ++rep) {
         const auto t1 = clk::now();
         const auto end = t1 + std::chrono::microseconds(300);
-        auto seen = t1;
         EXPECT(wait_bounded([&] { return clk::now() < end ? 1 : 0; }, [] { return false; }, 1000.0) == kWaitDone);
-        seen = clk::now();
-        late_max = std::max(late_max, std::chrono::duration<double, std::micro>(seen - end).count());
+        late.push_back(std::chrono::duration<double, std::micro>(clk::now() - end).count());
     }
-    EXPECT(late_max < 100.0);
+    std::sort(late.begin(), late.end());
+    const double late_max = late[late.size() / 2];
+    EXPECT(late_max < 50.0);
     // past the spin phase the wait naps (a hung fan-in does not burn a core): a 50 ms
     // timeout with a 5 ms spin polls far fewer times than a busy loop would
     long polls = 0;
     EXPECT(wait_bounded([&] { ++polls; return 1; }, [] { return false; }, 50.0, 5.0) == kWaitTimeout);
-    std::printf("%s (%.1f ms timeout case, frame end seen at most %.1f us late, %ld polls in 50 ms)\n",
+    std::printf("%s (%.1f ms timeout case, frame end seen a median %.1f us late, %ld polls in 50 ms)\n",
                 fails ? "wait_check FAILED" : "wait_check ok", ms, late_max, polls);
     return fails ? 1 : 0;
 }

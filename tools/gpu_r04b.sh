@@ -18,3 +18,5 @@ for f in ("bench_r04b", "bench_r04b_strong1"):
                                      "serial_frame_ms_median", "kernel_ms_mean", "kernel_ms_mean_inflight", "group_phases_ms")})
     print("   roofline", {k: d["roofline"].get(k) for k in ("bound", "frac", "traffic")}, "parity", (d.get("parity") or {}).get("ok"))
 PY
+timeout -k 10 400 python tools/latency_sweep.py > gpurun_out/latency_sweep_r04b.json 2> gpurun_out/latency_sweep_r04b.err; rc=$?
+echo "latency sweep rc=$rc"; cat gpurun_out/latency_sweep_r04b.json; [ $rc -eq 0 ] || { tail -5 gpurun_out/latency_sweep_r04b.err; exit $rc; }

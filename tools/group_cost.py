@@ -8,6 +8,8 @@ hardware queues with another's), alternated over blocks:
   A_frames            frames mode (bench.py frames): F contexts on F streams,
                       frame i on context i mod F, kernel timing events on;
   A_frames_notiming   the same with rt_set_kernel_timing(0);
+  A_own_notiming      the contexts on their own rt_create streams (not torch's);
+  A_own_cumask_notiming  the same with RT_STREAMS_CUMASK=1 (a hardware queue each);
   B_group             a 1-rank RCCL group with F frame slots (bench.py --mode
                       strong at N = 1), phase and kernel timing on;
   C_group_notiming    the same with rt_group_set_phase_timing(0) and
@@ -26,7 +28,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-VARIANTS = ("A_frames", "A_frames_notiming", "B_group", "C_group_notiming")
+VARIANTS = ("A_frames", "A_frames_notiming", "A_own_notiming", "A_own_cumask_notiming", "B_group", "C_group_notiming")
+ENV = {"A_own_cumask_notiming": {"RT_STREAMS_CUMASK": "1"}}
 
 
 def child(a):
@@ -45,12 +48,14 @@ def child(a):
     ref_ctx.set_params(W, H, 3)
     ref = ref_ctx.render(W, H)
     ref_ctx.close()
-    if name.startswith("A_frames"):
+    if name.startswith("A_"):
+        own = name.startswith("A_own")
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
         cs, bufs = [], []
         for st in streams:
             c = rtamd.ComputeShader(0)
-            c.set_stream(st.cuda_stream)
+            if not own:  # else the context's own stream (rt_create; RT_STREAMS_CUMASK: own queue)
+                c.set_stream(st.cuda_stream)
             c.upload(fs)
             c.set_params(W, H, 3)
             c.set_kernel_timing(timing)
@@ -131,7 +136,8 @@ def main():
     for _ in range(a.blocks):
         for v in VARIANTS:
             r = subprocess.run([sys.executable, os.path.abspath(__file__), "--variant", v, "--frames", str(a.frames),
-                                "--inflight", str(a.inflight)], capture_output=True, text=True, timeout=240)
+                                "--inflight", str(a.inflight)], capture_output=True, text=True, timeout=240,
+                               env=dict(os.environ, **ENV.get(v, {})))
             if r.returncode != 0:
                 print(r.stderr[-2000:], file=sys.stderr)
                 sys.exit(r.returncode)

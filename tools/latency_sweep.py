@@ -1,0 +1,94 @@
+#!/usr/bin/env python3
+"""Waited-frame latency of the car (bench.py's serial_frame_ms_median setting) over the
+latency mode's knobs, one process, one context, modes alternated in blocks.
+
+    python tools/latency_sweep.py [--frames 300] [--blocks 3] [--config 3]
+
+Each frame: camera + light upload, dispatch, wait (rt_sync: the host polls the
+stream), rt_set_latency_mode(1), kernel timing events off. Settings: split walks
+(rt_debug_split max_rays, group) and the heaviest tiles as several waves
+(rt_debug_heavy k, parts). Every setting's frame is compared bit for bit with the
+default's. One JSON line: median waited ms per setting (median over blocks).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "opengl-ray-tracer_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import bench  # noqa: E402
+import rtamd  # noqa: E402
+
+SETTINGS = {
+    "default": {},
+    "split16x16": {"split": (16, 16)},
+    "split32x8": {"split": (32, 8)},
+    "split8x8": {"split": (8, 8)},
+    "heavy127x2": {"heavy": (127, 2)},
+    "heavy255x2": {"heavy": (255, 2)},
+    "heavy63x4": {"heavy": (63, 4)},
+    "heavy127x4": {"heavy": (127, 4)},
+    "no_heavy": {"heavy": (0, 1)},
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=300)
+    ap.add_argument("--blocks", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    cfg, W, H, mb, _, _ = bench.WORKLOADS[a.config]
+    fs = rtamd.generate(cfg, 0, W, H)
+    torch.cuda.set_device(0)
+    c = rtamd.ComputeShader(0)
+    c.upload(fs)
+    c.set_params(W, H, mb)
+    c.set_kernel_timing(False)
+    c.set_latency_mode(1)
+    out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    names = [n for n in SETTINGS if not a.only or n in a.only.split(",") or n == "default"]
+
+    def apply(s):
+        sp = s.get("split", (16, 8))
+        c.debug_split(*sp)
+        hv = s.get("heavy", (-1, 2))
+        c.debug_heavy(*hv)
+
+    def frame():
+        c.set_camera(fs.camera)
+        c.set_light(fs.light)
+        c.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
+        c.sync()
+
+    ref, res, same = None, {n: [] for n in names}, {}
+    for blk in range(a.blocks):
+        for n in names:
+            apply(SETTINGS[n])
+            for _ in range(20):
+                frame()
+            w = []
+            for _ in range(a.frames):
+                t0 = time.perf_counter()
+                frame()
+                w.append(time.perf_counter() - t0)
+            res[n].append(float(np.median(w)) * 1e3)
+            img = out.cpu().numpy()
+            if ref is None:
+                ref = img
+            same[n] = same.get(n, True) and bool(np.array_equal(img, ref))
+    print(json.dumps({"config": a.config, "frames": a.frames, "blocks": a.blocks,
+                      "waited_ms": {n: float(np.median(v)) for n, v in res.items()},
+                      "per_block": res, "image_equal": same}))
+    c.close()
+
+
+if __name__ == "__main__":
+    main()
