@@ -30,11 +30,23 @@ SETTINGS = {
     "split16x16": {"split": (16, 16)},
     "split32x8": {"split": (32, 8)},
     "split8x8": {"split": (8, 8)},
+    "split16x32": {"split": (16, 32)},
+    "split32x16": {"split": (32, 16)},
     "heavy127x2": {"heavy": (127, 2)},
     "heavy255x2": {"heavy": (255, 2)},
     "heavy63x4": {"heavy": (63, 4)},
+    "heavy31x4": {"heavy": (31, 4)},
+    "heavy63x8": {"heavy": (63, 8)},
+    "heavy31x8": {"heavy": (31, 8)},
     "heavy127x4": {"heavy": (127, 4)},
     "no_heavy": {"heavy": (0, 1)},
+    "h63x4_s16x16": {"heavy": (63, 4), "split": (16, 16)},
+    "h255x2_s16x16": {"heavy": (255, 2), "split": (16, 16)},
+    "h63x4_s32x16": {"heavy": (63, 4), "split": (32, 16)},
+    "h31x8_s16x16": {"heavy": (31, 8), "split": (16, 16)},
+    "lanek506": {"lane_k": (506, 2)},
+    "lanek126": {"lane_k": (126, 2)},
+    "lanek0": {"lane_k": (0, 0)},
 }
 
 
@@ -57,10 +69,9 @@ def main():
     names = [n for n in SETTINGS if not a.only or n in a.only.split(",") or n == "default"]
 
     def apply(s):
-        sp = s.get("split", (16, 8))
-        c.debug_split(*sp)
-        hv = s.get("heavy", (-1, 2))
-        c.debug_heavy(*hv)
+        c.debug_split(*s.get("split", (16, 8)))
+        c.debug_heavy(*s.get("heavy", (-1, 2)))
+        c.debug_lane_k(*s.get("lane_k", (-1, 2)))
 
     def frame():
         c.set_camera(fs.camera)
