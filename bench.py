@@ -675,6 +675,21 @@ def main():
             c_.kernel_times()
         if grp is not None:
             grp.phase_times()
+    # The same waited frames from a C++ host (librthost.so rth_render_loop: the reference's
+    # render loop over the C ABI, as a C++ host would run it, without the interpreter
+    # between the calls). This is the figure reported as serial_frame_ms_median; the
+    # Python loop's figure above is kept beside it.
+    serial_frames_py = serial_frames
+    serial_frames_host = []
+    if grp is None and anim is None and not strong:
+        for c_ in ctxs:
+            c_.set_latency_mode(1)
+        rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, a.warmup, True)
+        serial_frames_host = list(rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, a.steps,
+                                                    True) * 1e-3)
+        for c_ in ctxs:
+            c_.set_latency_mode(0)
+        serial_frames = serial_frames_host
     serial_med_ranks = None
     if serial_frames and world > 1:
         med = [None] * world
@@ -741,8 +756,12 @@ def main():
             "serial_ms_per_step": (serial if serial is not None else elapsed) / a.steps * 1e3,
             "serial_ms_per_step_latency_mode": (serial_lat / a.steps * 1e3) if serial_lat is not None else None,
             "serial_frame_ms_median": float(np.median(serial_frames)) * 1e3 if serial_frames else None,
-            "serial_frame_median_mode": (("each frame waited for (rt_sync: host polls the stream), "
-                                          "rt_set_latency_mode on") if serial_frames and not use_group else
+            "serial_frame_ms_median_python": float(np.median(serial_frames_py)) * 1e3 if serial_frames_py else None,
+            "serial_frame_median_mode": (("C++ host loop (librthost.so rth_render_loop: camera + light upload, "
+                                          "dispatch, rt_sync per frame), rt_set_latency_mode on"
+                                          ) if serial_frames_host else
+                                         ("each frame waited for (rt_sync: host polls the stream), "
+                                          "rt_set_latency_mode on, Python loop") if serial_frames and not use_group else
                                          ("each frame waited for on every rank (rt_group_sync), ranks start "
                                           "each frame after a barrier, rt_set_latency_mode on; rank 0's median")
                                          if serial_frames else None),

@@ -176,6 +176,11 @@ SCENE_SYMBOLS = {
     "rts_write_image": (_I, [C.c_char_p, _P, _I, _I, C.c_long, _I]),
 }
 
+# include/rt_host.h (librthost.so: the reference's render loop as a C++ host)
+HOST_SYMBOLS = {
+    "rth_render_loop": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P]),
+}
+
 RT_SYMBOLS = {
     "rt_create": (_I, [_P, _I]), "rt_destroy": (_I, [_P]), "rt_set_stream": (_I, [_P, _P]),
     "rt_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
@@ -262,6 +267,33 @@ def rt_lib():
     if _rt_lib is None:
         _rt_lib = _bind(_bind(_load("librtamd.so"), RT_SYMBOLS), GROUP_SYMBOLS)
     return _rt_lib
+
+
+_host_lib = None
+
+
+def host_lib():
+    """librthost.so: rth_render_loop, the reference's render loop (src/main.cpp:290-462)
+    as a C++ host over the C ABI (include/rt_host.h)."""
+    global _host_lib
+    if _host_lib is None:
+        rt_lib()  # librtamd.so first: librthost.so links it
+        _host_lib = _bind(_load("librthost.so"), HOST_SYMBOLS)
+    return _host_lib
+
+
+def render_loop(ctx, cams, light, width, height, dst_ptr, pitch, frames, wait_each=True):
+    """rth_render_loop on ComputeShader `ctx`: `frames` frames (camera cams[i % len]),
+    each waited for (wait_each) or back to back. Returns the host wall times in ms:
+    one per frame, or [total] when not waiting for each."""
+    cams = as_records(np.asarray(cams), CAMERA_DTYPE).reshape(-1)
+    light = as_records(np.asarray(light), LIGHT_DTYPE).reshape(1)
+    out = np.zeros(max(1, frames), np.float64)
+    rc = host_lib().rth_render_loop(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height),
+                                    C.c_void_p(dst_ptr), int(pitch), int(frames), int(bool(wait_each)), _ptr(out))
+    if rc != 0:
+        raise RTError("rth_render_loop", rc)
+    return out if wait_each else out[:1]
 
 
 def _f3(v):

@@ -577,3 +577,29 @@ def test_rccl_rank_group_frames_in_flight(ctx):
         assert ph["frames"] > 0 and ph["render_ms"] > 0 and ph["unstripe_ms"] == 0 and ph["fanin_ms"] == 0
     finally:
         g.close()
+
+
+def test_host_render_loop_frames(ctx):
+    """librthost.so rth_render_loop (the reference's render loop, src/main.cpp:290-462, as
+    a C++ host over the C ABI): waited and back-to-back frames, cameras cycling, leave
+    the last camera's frame; one time per waited frame."""
+    W, H = 640, 360
+    fs = rtamd.generate(3, 0, W, H)
+    cams = np.concatenate([_orbit_cameras(W, H, 3)[k] for k in (1, 2)])
+    refs = []
+    for c in cams:
+        ctx.upload(rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, c, fs.light))
+        ctx.set_params(W, H, 3)
+        refs.append(ctx.render(W, H))
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3)
+    out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ms = rtamd.render_loop(ctx, cams, fs.light, W, H, out.data_ptr(), W * 16, 5, True)
+    assert ms.shape == (5,) and (ms > 0).all()
+    assert np.array_equal(out.cpu().numpy(), refs[0])  # frame 4 took cams[4 % 2]
+    ms = rtamd.render_loop(ctx, cams, fs.light, W, H, out.data_ptr(), W * 16, 6, False)
+    assert ms.shape == (1,) and ms[0] > 0
+    assert np.array_equal(out.cpu().numpy(), refs[1])
+    with pytest.raises(rtamd.RTError):
+        rtamd.render_loop(ctx, cams, fs.light, W, H, out.data_ptr(), W * 12, 1, True)  # pitch < 16 W
