@@ -123,8 +123,6 @@ struct KParams {
     int tail_rx, tail_regions;               // 64x64-pixel regions: per row, total (one counter each)
     int tail_counters;                       // counters per set (>= tail_regions; all zeroed for the next)
     int tail_max_lanes;                      // a wave queues its rays only if at most this many are alive
-    unsigned char* __restrict__ tail_oct;    // RT_TAIL_SORT: per queue slot, the ray's direction octant
-    unsigned short* __restrict__ tail_perm;  // RT_TAIL_SORT: per region, its queued rays in octant order
     int rgb;                                 // output format (rt_dispatch_rows_fmt): 0 RGBA32F, 1 packed RGB32F
                                              // (12 B per pixel), 2 RGBA32F at the image row (RT_FORMAT_RGBA32F_IMAGE)
     float shadow_off;                        // k_accel's shadow-ray offset: 1e-3 (BVH branch, gpu_shader.comp:469);

@@ -1527,16 +1527,7 @@ constexpr size_t kTailAutoItems = 8192;  // RT_TAIL_AUTO threshold
 // k_accel_tail grid: one wave per possible chunk (64 per region), each taking one, or a
 // resident grid striding over the chunks.
 constexpr bool kTailOneShot = RT_TAIL_ONESHOT != 0;
-// k_accel_tail takes each region's rays in direction-octant order (k_tail_sort), so a
-// tail wave's 64 rays head into one octant (experiment builds)
-#ifndef RT_TAIL_SORT
-#define RT_TAIL_SORT 0
-#endif
-constexpr bool kTailSort = RT_TAIL_SORT != 0;
 
-__device__ __forceinline__ unsigned char dir_octant(const V& d) {
-    return static_cast<unsigned char>((d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0));
-}
 
 // Cost-ordered dispatch (rt_set_schedule, k_tile_order): 32 half-octave
 // buckets of a tile's work; the render kernel counts them per group of
@@ -1679,7 +1670,6 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
                     q[1] = make_float4(ray.d.x, ray.d.y, ray.d.z, acc.y);
                     q[2] = make_float4(att.x, att.y, att.z, acc.z);
                     q[3] = make_float4(__int_as_float(pc.r), __int_as_float(pc.x), 0.f, 0.f);
-                    if (kTailSort) kp.tail_oct[pos] = dir_octant(ray.d);
                 }
             }
             deferred = alive;
@@ -1821,7 +1811,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
         }
         const int k = (chunk - first) * 64 + lane;  // index within the region
         bool alive = k < n;
-        const int i = rid * kTailRegion + (kTailSort && alive ? kp.tail_perm[rid * kTailRegion + k] : k);
+        const int i = rid * kTailRegion + k;
         Ray ray{mk(0.f, 0.f, 0.f), mk(0.f, 0.f, 1.f)};
         V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
         int r = 0, x = 0;
@@ -1847,32 +1837,6 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
     }
     if (blockIdx.x == 0)
         for (int b = threadIdx.x; b < kp.tail_counters; b += blockDim.x) kp.tail_count_next[b] = 0;
-}
-
-// RT_TAIL_SORT: one workgroup per region, a counting sort of its queued rays by
-// direction octant into tail_perm (region-local indices). Any order gives the same
-// pixels: a ray's bounces do not depend on the other rays of its wave.
-__global__ __launch_bounds__(256) void k_tail_sort(KParams kp) {
-    __shared__ int cnt[8];
-    const int rid = blockIdx.x, t = threadIdx.x;
-    const int n = kp.tail_count[rid];
-    if (n == 0) return;
-    if (t < 8) cnt[t] = 0;
-    __syncthreads();
-    const unsigned char* oct = kp.tail_oct + static_cast<size_t>(rid) * kTailRegion;
-    for (int k = t; k < n; k += blockDim.x) atomicAdd(&cnt[oct[k]], 1);
-    __syncthreads();
-    if (t == 0) {
-        int acc = 0;
-        for (int o = 0; o < 8; ++o) {
-            const int c = cnt[o];
-            cnt[o] = acc;
-            acc += c;
-        }
-    }
-    __syncthreads();
-    unsigned short* perm = kp.tail_perm + static_cast<size_t>(rid) * kTailRegion;
-    for (int k = t; k < n; k += blockDim.x) perm[atomicAdd(&cnt[oct[k]], 1)] = static_cast<unsigned short>(k);
 }
 
 __global__ void k_pack_prims(const float4* __restrict__ geo_lin, const int* __restrict__ prim_shape,
@@ -2277,8 +2241,6 @@ struct rt_ctx {
     // compaction (rt_set_tail): bounces >= tail_from run in k_accel_tail (0: off)
     int tail_from = RT_TAIL_AUTO;
     float4* tail_queue = nullptr;
-    unsigned char* tail_oct = nullptr;    // RT_TAIL_SORT
-    unsigned short* tail_perm = nullptr;  // RT_TAIL_SORT
     size_t tail_cap = 0;     // queue entries
     int* tail_counts = nullptr;  // two sets of per-region counters, alternating by dispatch
     int tail_regions_cap = 0;
@@ -3208,9 +3170,12 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                    std::min(k2.lane_from_depth, k2.shadow_lane_from) >= k2.maxBounces;
                 hk = small ? std::max(16, k2.tiles / 256) : 0;
                 hp = small ? 8 : 1;
-                if (!small && c->latency_mode) {  // rt_set_latency_mode: the heaviest 1/512 as 2 waves
+                if (!small && c->latency_mode) {
+                    // rt_set_latency_mode: the heaviest 1/512 as 4 waves (car waited frame 0.2563 ms
+                    // with 2 waves, 0.2507 with 4; 1/256 as 2: 0.2518, 1/128 as 2: 0.2537, 1/1024 as
+                    // 4: 0.2559, 1/512 as 8: 0.2592; profiles/r04e_latency_sweep.json)
                     hk = std::max(16, k2.tiles / 512);
-                    hp = 2;
+                    hp = 4;
                 }
             }
             if (!c->persistent && !c->tile_times && hp > 1 && hk > 0) {
@@ -3239,16 +3204,9 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             const size_t need = static_cast<size_t>(regions) * kTailRegion;
             if (need > c->tail_cap) {
                 hipFree(c->tail_queue);
-                hipFree(c->tail_oct);
-                hipFree(c->tail_perm);
                 c->tail_queue = nullptr;
-                c->tail_oct = nullptr;
-                c->tail_perm = nullptr;
                 c->tail_cap = 0;
                 if (hipMalloc(&c->tail_queue, need * 4 * sizeof(float4)) != hipSuccess) return RT_ERR_NO_MEMORY;
-                if (kTailSort && (hipMalloc(&c->tail_oct, need) != hipSuccess ||
-                                  hipMalloc(&c->tail_perm, need * sizeof(unsigned short)) != hipSuccess))
-                    return RT_ERR_NO_MEMORY;
                 c->tail_cap = need;
             }
             if (regions > c->tail_regions_cap) {
@@ -3261,8 +3219,6 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 c->tail_regions_cap = regions;
             }
             k2.tail_queue = c->tail_queue;
-            k2.tail_oct = c->tail_oct;
-            k2.tail_perm = c->tail_perm;
             k2.tail_count = c->tail_counts + c->tail_parity * c->tail_regions_cap;
             k2.tail_count_next = c->tail_counts + (1 - c->tail_parity) * c->tail_regions_cap;
             k2.tail_from = tail_from;
@@ -3300,7 +3256,6 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         if (tail_on) {
             const size_t tlds = static_cast<size_t>(k2.lane_stack) * 64 * 6;
             const int tgrid = kTailOneShot ? regions * (kTailRegion / 64) : c->cu_count * 16;
-            if (kTailSort) hipLaunchKernelGGL(k_tail_sort, dim3(regions), dim3(256), 0, c->stream, k2);
             hipLaunchKernelGGL(spec ? k_accel_tail<true> : k_accel_tail<false>, dim3(tgrid), dim3(64), tlds,
                                c->stream, A, c->mat, k2);
             c->tail_parity = 1 - c->tail_parity;
@@ -3434,8 +3389,6 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->stats_dev);
     hipFree(c->tile_counter);
     hipFree(c->tail_queue);
-    hipFree(c->tail_oct);
-    hipFree(c->tail_perm);
     hipFree(c->tail_counts);
     hipFree(c->tile_times);
     hipFree(c->tile_order);
