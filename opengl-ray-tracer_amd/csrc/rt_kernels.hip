@@ -1973,9 +1973,12 @@ __device__ void reference_box(const FlatShape& s, float lo[3], float hi[3]) {
 //   wpos   : wide-record slots (4*w + s) of the local nodes above those prims
 // Per reference node j that lists an animated shape (node_ids[j]):
 //   node   : the animated shapes it lists (updateBVH's set, leaves + ancestors)
+//   wn     : the wnodes child slots (2 * parent + side) that hold its box
+//   item   : the scene-tree items (titems records) whose exact box is its box
 struct AnimMaps {
     const int *ids, *slot_off, *slot_list, *prim_off, *prim_list, *wpos_off, *wpos_list;
     const int *node_ids, *node_off, *node_list;
+    const int *wn_off, *wn_list, *item_off, *item_list;
     int count, nodes;
 };
 enum { AF_BOUNDED = 1, AF_CONE = 2 };  // per-frame flags: conservative box valid; normal moved
@@ -1984,8 +1987,10 @@ struct AnimOut {
     FlatShape* shapes;  // staging copy of the full shape array
     FlatNode* nodes;    // staging copy of the node array (authoritative boxes)
     float4 *geo_lin, *geo_leaf, *mat;
+    float4* packed;                   // the packed node copies (k_pack_nodes layout)
     float4 *anodes, *lnodes, *prims;  // accelerator (null when off)
-    float4* pbox;                     // conservative box per prim (lo, hi), for k_refit_local
+    float4 *wnodes, *titems;          // accelerator: per-parent child boxes, scene-tree items' exact boxes
+    float4* pbox;                     // conservative box per prim (lo, hi), for k_anim_refit
     const int* prim_seq;
     float4* sbox;                     // per animated shape: reference box, conservative box (4 float4)
     float origin_lim;
@@ -1994,7 +1999,9 @@ struct AnimOut {
 
 // One thread per animated shape: rewrites its records and derives its two
 // boxes (the reference's growToInclude box and the accelerator's conservative
-// one); k_grow_nodes then grows the nodes listing it.
+// one); k_anim_refit then grows the nodes listing it. `fresh` and `flags` are read
+// straight from the host's pinned (mapped, coherent) buffer: no copy engine
+// transfer and no wait for one ahead of the kernel.
 __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __restrict__ flags, AnimMaps m,
                           AnimOut o) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2031,7 +2038,7 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
     if (rta::classify(s, b, o.origin_lim) != rta::BOUNDED) return;  // the host checked the class
     sb[2] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
     sb[3] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
-    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {  // the prim's box for k_refit_local
+    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {  // the prim's box for k_anim_refit
         float4* pb = o.pbox + 2 * static_cast<size_t>(m.prim_list[q]);
         pb[0] = sb[2];
         pb[1] = sb[3];
@@ -2051,9 +2058,11 @@ __device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
 // node's box - updateBVH's growToInclude of each listed shape - and of its
 // content box. A single writer per node: no atomics, and the min/max result is
 // the same in any order (no stored value is NaN; a NaN coordinate adds nothing).
-__global__ __launch_bounds__(256) void k_grow_nodes(AnimMaps m, AnimOut o) {
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (j >= m.nodes) return;
+// The same lane then writes the grown box through to every copy the kernels
+// read: the packed node, the accelerator's exact box, its parent's child copy
+// (wnodes: exact + content box) and the scene-tree items gated by it. Nodes that
+// list no animated shape never change, so no other copy needs refreshing.
+__device__ void grow_node(const AnimMaps& m, const AnimOut& o, int j, int lane) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int q = m.node_off[j] + lane; q < m.node_off[j + 1]; q += 64) {
@@ -2068,17 +2077,38 @@ __global__ __launch_bounds__(256) void k_grow_nodes(AnimMaps m, AnimOut o) {
     wave_minmax(clo, chi);
     if (lane != 0) return;
     const int k = m.node_ids[j];
-    float* mn = &o.nodes[k].boundsMin.x;
-    float* mx = &o.nodes[k].boundsMax.x;
+    FlatNode& nd = o.nodes[k];
+    float* mn = &nd.boundsMin.x;
+    float* mx = &nd.boundsMax.x;
     for (int a = 0; a < 3; ++a) {  // glm::min(Min, p) = (p < Min) ? p : Min (BoundingBox.hpp:46)
         mn[a] = lo[a] < mn[a] ? lo[a] : mn[a];
         mx[a] = mx[a] < hi[a] ? hi[a] : mx[a];
     }
+    const bool leaf = nd.leftChild == -1;
+    const int ca = leaf ? -(nd.startShapeIdx + 1) : nd.leftChild, cb = leaf ? nd.numShapes : nd.rightChild;
+    o.packed[2 * static_cast<size_t>(k)] = make_float4(mn[0], mn[1], mn[2], __int_as_float(ca));
+    o.packed[2 * static_cast<size_t>(k) + 1] = make_float4(mx[0], mx[1], mx[2], __int_as_float(cb));
     if (!o.anodes) return;
-    float* c = reinterpret_cast<float*>(o.anodes + 4 * static_cast<size_t>(k) + 2);  // content box (accel.h)
-    for (int a = 0; a < 3; ++a) {
-        c[a] = fminf(c[a], clo[a]);
-        c[4 + a] = fmaxf(c[4 + a], chi[a]);
+    float4* an = o.anodes + 4 * static_cast<size_t>(k);
+    an[0] = make_float4(mn[0], mn[1], mn[2], an[0].w);
+    an[1] = make_float4(mx[0], mx[1], mx[2], an[1].w);
+    float4 c0 = an[2], c1 = an[3];  // content box (accel.h)
+    c0 = make_float4(fminf(c0.x, clo[0]), fminf(c0.y, clo[1]), fminf(c0.z, clo[2]), c0.w);
+    c1 = make_float4(fmaxf(c1.x, chi[0]), fmaxf(c1.y, chi[1]), fmaxf(c1.z, chi[2]), c1.w);
+    an[2] = c0;
+    an[3] = c1;
+    for (int qq = m.wn_off[j]; qq < m.wn_off[j + 1]; ++qq) {
+        const int ws = m.wn_list[qq];
+        float4* q = o.wnodes + 8 * static_cast<size_t>(ws >> 1) + 4 * (ws & 1);
+        q[0] = make_float4(mn[0], mn[1], mn[2], q[0].w);
+        q[1] = make_float4(mx[0], mx[1], mx[2], q[1].w);
+        q[2] = make_float4(c0.x, c0.y, c0.z, q[2].w);
+        q[3] = make_float4(c1.x, c1.y, c1.z, q[3].w);
+    }
+    for (int q = m.item_off[j]; q < m.item_off[j + 1]; ++q) {
+        float4* t = o.titems + 2 * static_cast<size_t>(m.item_list[q]);
+        t[0] = make_float4(mn[0], mn[1], mn[2], t[0].w);
+        t[1] = make_float4(mx[0], mx[1], mx[2], t[1].w);
     }
 }
 
@@ -2087,11 +2117,8 @@ __global__ __launch_bounds__(256) void k_grow_nodes(AnimMaps m, AnimOut o) {
 // per dirty wide-record slot, the union of pbox over the slot's prim range
 // (a local subtree's prims are contiguous, accel.cpp LocalBuilder).
 // dirty[j] = (4*w + s, first prim, end prim, 0).
-__global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ dirty, int n,
-                                                     const float4* __restrict__ pbox, float4* __restrict__ lnodes,
-                                                     int rec) {
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (j >= n) return;
+__device__ void refit_slot(const int4* __restrict__ dirty, int j, const float4* __restrict__ pbox,
+                           float4* __restrict__ lnodes, int rec, int lane) {
     const int4 d = dirty[j];
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int p = d.y + lane; p < d.z; p += 64) {
@@ -2107,6 +2134,21 @@ __global__ __launch_bounds__(256) void k_refit_local(const int4* __restrict__ di
     }
 }
 
+// rt_animate's second step, after k_animate: the grown reference nodes (waves
+// [0, m.nodes)) and the refit local / scene-tree slots (the next n_dirty waves)
+// in ONE launch: they read what k_animate wrote (sbox / pbox) and write disjoint
+// records. (Round 3 ran them as four launches, k_grow_nodes, k_refit_local,
+// k_refresh_nodes over all N nodes and k_refresh_items over all items.)
+__global__ __launch_bounds__(256) void k_anim_refit(AnimMaps m, AnimOut o, const int4* __restrict__ dirty,
+                                                    int n_dirty, int rec) {
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (w < m.nodes) {
+        grow_node(m, o, w, lane);
+    } else if (w - m.nodes < n_dirty) {
+        refit_slot(dirty, w - m.nodes, o.pbox, o.lnodes, rec, lane);
+    }
+}
+
 // Scene-tree wide slots of the unbounded subtree (kNoPrune): their boxes are the
 // reference leaves' padded boxes, which animation grows; while a set is animated
 // they are infinite (entered by every ray; the items' exact boxes still gate).
@@ -2116,48 +2158,6 @@ __global__ void k_inf_slots(const int* __restrict__ slots, int n, float4* __rest
     const int w = slots[i] >> 2, sl = slots[i] & 3;
     for (int r = 0; r < 6; ++r) *wide_box_f(lnodes, rec, w, sl, r) = r < 3 ? -INFINITY : INFINITY;
 }
-
-// The scene-tree items' exact boxes (titems) from the grown reference leaves.
-__global__ void k_refresh_items(const FlatNode* __restrict__ src, const int* __restrict__ ref, int n,
-                                float4* __restrict__ titems) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const FlatNode& nd = src[ref[i]];
-    float4* q = titems + 2 * static_cast<size_t>(i);
-    q[0] = make_float4(nd.boundsMin.x, nd.boundsMin.y, nd.boundsMin.z, q[0].w);
-    q[1] = make_float4(nd.boundsMax.x, nd.boundsMax.y, nd.boundsMax.z, q[1].w);
-}
-
-// Re-derives every copy of the node boxes from the staging nodes and the
-// content boxes: the packed nodes (k_packet, k_lane), and the accelerator's
-// exact boxes plus its per-parent child copies (anodes rows 0-1, wnodes).
-__global__ void k_refresh_nodes(const FlatNode* __restrict__ src, int N, float4* __restrict__ nodes,
-                                float4* __restrict__ anodes, float4* __restrict__ wnodes) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= N) return;
-    const FlatNode& n = src[k];
-    const bool leaf = n.leftChild == -1;
-    const int a = leaf ? -(n.startShapeIdx + 1) : n.leftChild, b = leaf ? n.numShapes : n.rightChild;
-    nodes[2 * k] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, __int_as_float(a));
-    nodes[2 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, __int_as_float(b));
-    if (!anodes) return;
-    float4* an = anodes + 4 * static_cast<size_t>(k);
-    an[0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, an[0].w);
-    an[1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, an[1].w);
-    if (leaf) return;
-    const int ch[2] = {n.leftChild, n.rightChild};
-    for (int s2 = 0; s2 < 2; ++s2) {
-        const FlatNode& cn = src[ch[s2]];
-        const float4* ca = anodes + 4 * static_cast<size_t>(ch[s2]);
-        float4* q = wnodes + 8 * static_cast<size_t>(k) + 4 * s2;
-        q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, q[0].w);
-        q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, q[1].w);
-        const float4 lo = ca[2], hi = ca[3];
-        q[2] = make_float4(lo.x, lo.y, lo.z, q[2].w);
-        q[3] = make_float4(hi.x, hi.y, hi.z, q[3].w);
-    }
-}
-
 
 }  // namespace
 
@@ -2192,7 +2192,8 @@ struct rt_ctx {
     float4 *anodes = nullptr, *lnodes = nullptr, *wnodes = nullptr, *prims = nullptr;
     int4* tleaf = nullptr;
     float4* titems = nullptr;  // scene-tree items (AccelPtrs::titems)
-    int* titem_ref = nullptr;  // per titems record: its reference leaf (k_refresh_items, animation)
+    int* titem_ref = nullptr;  // per titems record: its reference leaf (device copy)
+    std::vector<int> host_titem_ref;  // the same on the host (prepare_animation: items of a grown leaf)
     int n_titems = 0;
     int* anim_inf_slots = nullptr;  // wide slots whose boxes go infinite while animating (kNoPrune)
     int n_inf_slots = 0;
@@ -2258,20 +2259,19 @@ struct rt_ctx {
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
     size_t anim_maps_cap = 0;
     AnimMaps anim{};
-    // Per-frame upload, FlatShape[count] then int flags[count]: a ring of pinned host
-    // buffers, so rt_animate waits only for the copy kAnimRing frames back (not for the
-    // previous frame's render, which the previous copy is stream-ordered behind).
+    // Per-frame records, FlatShape[count] then int flags[count]: a ring of pinned, mapped
+    // host buffers that k_animate reads directly, so rt_animate waits only for the
+    // k_animate kAnimRing frames back (not for the previous frame's render).
     static constexpr int kAnimRing = 3;
     void* anim_pinned[kAnimRing] = {nullptr, nullptr, nullptr};
+    void* anim_pinned_dev[kAnimRing] = {nullptr, nullptr, nullptr};  // the same buffers as the device sees them
     size_t anim_pinned_cap[kAnimRing] = {0, 0, 0};
-    hipEvent_t anim_copied[kAnimRing] = {nullptr, nullptr, nullptr};  // that slot's upload has completed
+    hipEvent_t anim_copied[kAnimRing] = {nullptr, nullptr, nullptr};  // that slot's k_animate has read it
     int anim_slot = 0;
-    char* anim_frame = nullptr;         // the device copy (stream-ordered reuse)
-    size_t anim_frame_cap = 0;
     float4* anim_sbox = nullptr;        // per animated shape boxes (AnimOut::sbox)
     size_t anim_sbox_cap = 0;
     float4* pbox = nullptr;             // per prim conservative box (AnimOut::pbox)
-    int4* refit_dirty = nullptr;        // k_refit_local work list
+    int4* refit_dirty = nullptr;        // k_anim_refit's refit work list
     int n_dirty = 0;
     int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
@@ -2327,6 +2327,7 @@ void free_accel(rt_ctx* c) {
     hipFree(c->titem_ref);
     c->titem_ref = nullptr;
     c->n_titems = 0;
+    c->host_titem_ref.clear();
     hipFree(c->anim_inf_slots);
     c->anim_inf_slots = nullptr;
     c->n_inf_slots = 0;
@@ -2516,6 +2517,7 @@ int build_upload_accel(rt_ctx* c) {
         if (hipMalloc(&c->titem_ref, refs.size() * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
         HIP_TRY(hipMemcpyAsync(c->titem_ref, refs.data(), refs.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
         c->n_titems = static_cast<int>(refs.size());
+        c->host_titem_ref = refs;
     }
     // wnodes: per reference inner node both children's exact + content boxes;
     // tleaf: per reference leaf its plain range and local root code.
@@ -2693,7 +2695,7 @@ int prepare_animation(rt_ctx* c) {
         // nodes follow the local ones in lnodes (global slot 4*nw + q), a subtree's
         // prims are contiguous. Its unbounded part (kNoPrune: boxes are the padded
         // reference-leaf boxes, which grow) goes infinite while the set is animated;
-        // the items' exact boxes follow the grown leaves (k_refresh_items).
+        // the items' exact boxes follow the grown leaves (k_anim_refit).
         std::vector<int> inf_slots;
         const rta::SceneTree& T = A.st;
         if (T.wroot >= 0) {
@@ -2784,7 +2786,7 @@ int prepare_animation(rt_ctx* c) {
         list_at = buf.size();
         for (const auto& l : lists) buf.insert(buf.end(), l.begin(), l.end());
     };
-    // per reference node, the animated shapes it lists (k_grow_nodes)
+    // per reference node, the animated shapes it lists (k_anim_refit)
     std::vector<int> node_ids;
     std::vector<std::vector<int>> lists_of;
     {
@@ -2799,11 +2801,31 @@ int prepare_animation(rt_ctx* c) {
                 lists_of[slot[k]].push_back(i);
             }
     }
-    size_t o[8];
+    // per grown node, where its box is copied (k_anim_refit writes them through): the
+    // wnodes child slots of its parent(s) and the scene-tree items it gates
+    std::vector<std::vector<int>> wn_of(node_ids.size()), items_of(node_ids.size());
+    {
+        std::vector<int> slot(N, -1);
+        for (size_t j = 0; j < node_ids.size(); ++j) slot[node_ids[j]] = static_cast<int>(j);
+        for (int p = 0; p < N; ++p) {
+            const FlatNode& nd = c->host_nodes[p];
+            if (nd.leftChild == -1) continue;
+            if (slot[nd.leftChild] >= 0) wn_of[slot[nd.leftChild]].push_back(2 * p);
+            if (slot[nd.rightChild] >= 0) wn_of[slot[nd.rightChild]].push_back(2 * p + 1);
+        }
+        if (c->accel_ok && c->titems)
+            for (size_t i = 0; i < c->host_titem_ref.size(); ++i) {
+                const int k = c->host_titem_ref[i];
+                if (k >= 0 && k < N && slot[k] >= 0) items_of[slot[k]].push_back(static_cast<int>(i));
+            }
+    }
+    size_t o[12];
     append(slots_of, o[0], o[1]);
     append(prims_of, o[2], o[3]);
     append(wpos_of, o[4], o[5]);
     append(lists_of, o[6], o[7]);
+    append(wn_of, o[8], o[9]);
+    append(items_of, o[10], o[11]);
     const size_t o_ids = buf.size();
     buf.insert(buf.end(), node_ids.begin(), node_ids.end());
     int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
@@ -2811,8 +2833,9 @@ int prepare_animation(rt_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int* d = c->anim_maps;
-    c->anim = AnimMaps{d,         d + o[0], d + o[1], d + o[2], d + o[3], d + o[4],
-                       d + o[5],  d + o_ids, d + o[6], d + o[7], n,        static_cast<int>(node_ids.size())};
+    c->anim = AnimMaps{d,        d + o[0], d + o[1],  d + o[2],  d + o[3], d + o[4], d + o[5], d + o_ids,
+                       d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], n,
+                       static_cast<int>(node_ids.size())};
     return ensure_staging(c->anim_sbox, c->anim_sbox_cap, 4 * static_cast<size_t>(n));
 }
 
@@ -3396,7 +3419,6 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->sched_order);
     hipFree(c->sched_sets);
     hipFree(c->anim_maps);
-    hipFree(c->anim_frame);
     hipFree(c->anim_sbox);
     for (int k = 0; k < rt_ctx::kAnimRing; ++k) {
         if (c->anim_pinned[k]) hipHostFree(c->anim_pinned[k]);
@@ -3547,8 +3569,7 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
         const FlatShape &s = shapes[i], &b0 = c->anim_base[i];
         int cls = rta::UNBOUNDED;
         if (c->accel_ok) {
-            rta::Box3 b;
-            cls = rta::classify(s, b, c->accel.origin_lim);
+            cls = rta::classify_class(s, c->accel.origin_lim);  // classify's class, without the box
             if (cls != c->anim_cls[i]) rebuild = true;
         }
         const bool cone = s.type != b0.type || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
@@ -3561,48 +3582,45 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (!c->anim_copied[slot]) {
         HIP_TRY(hipEventCreateWithFlags(&c->anim_copied[slot], hipEventDisableTiming));
     } else {
-        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // this slot's last upload has left it
+        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // k_animate of this slot's last frame has read it
     }
     if (c->anim_pinned_cap[slot] < bytes) {
         if (c->anim_pinned[slot]) hipHostFree(c->anim_pinned[slot]);
         c->anim_pinned[slot] = nullptr;
+        c->anim_pinned_dev[slot] = nullptr;
         c->anim_pinned_cap[slot] = 0;
-        if (hipHostMalloc(&c->anim_pinned[slot], bytes) != hipSuccess) return RT_ERR_NO_MEMORY;
+        // mapped and coherent: k_animate reads it over the host link, never a stale cached copy
+        if (hipHostMalloc(&c->anim_pinned[slot], bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        if (hipHostGetDevicePointer(&c->anim_pinned_dev[slot], c->anim_pinned[slot], 0) != hipSuccess)
+            return RT_ERR_DEVICE;
         c->anim_pinned_cap[slot] = bytes;
     }
-    int rc = ensure_staging(c->anim_frame, c->anim_frame_cap, bytes);
-    if (rc != RT_OK) return rc;
     char* pin = static_cast<char*>(c->anim_pinned[slot]);
+    const char* pin_dev = static_cast<const char*>(c->anim_pinned_dev[slot]);
     std::memcpy(pin, shapes, n * sizeof(FlatShape));
     std::memcpy(pin + n * sizeof(FlatShape), flags.data(), n * sizeof(int));
-    HIP_TRY(hipMemcpyAsync(c->anim_frame, pin, bytes, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));
     const bool acc = c->accel_ok;
     const size_t P = c->accel.prim_shape.size();
-    const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat,
+    const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat, c->nodes,
                       acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
+                      acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
                       acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
                       c->accel.origin_lim, c->accel.mt ? 1 : 0};
+    // 1. the moved shapes' records and boxes, read from the pinned buffer
     hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
-                       reinterpret_cast<const FlatShape*>(c->anim_frame),
-                       reinterpret_cast<const int*>(c->anim_frame + n * sizeof(FlatShape)), c->anim, out);
-    if (c->anim.nodes > 0)
-        hipLaunchKernelGGL(k_grow_nodes, dim3((c->anim.nodes + 3) / 4), dim3(256), 0, c->stream, c->anim, out);
-    if (acc && c->n_dirty > 0)
-        hipLaunchKernelGGL(k_refit_local, dim3((c->n_dirty + 3) / 4), dim3(256), 0, c->stream, c->refit_dirty,
-                           c->n_dirty, c->pbox, c->lnodes, c->accel.mt ? kWideRecMt : kWideRec);
-    if (c->N > 0)
-        hipLaunchKernelGGL(k_refresh_nodes, dim3((c->N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, c->N,
-                           c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr);
+                       reinterpret_cast<const FlatShape*>(pin_dev),
+                       reinterpret_cast<const int*>(pin_dev + n * sizeof(FlatShape)), c->anim, out);
+    HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));  // the slot may be refilled after this
+    // 2. the grown reference nodes (written through to every copy) and the refit local boxes
+    const int nd = acc ? c->n_dirty : 0;
+    if (c->anim.nodes + nd > 0)
+        hipLaunchKernelGGL(k_anim_refit, dim3((c->anim.nodes + nd + 3) / 4), dim3(256), 0, c->stream, c->anim, out,
+                           c->refit_dirty, nd, c->accel.mt ? kWideRecMt : kWideRec);
     HIP_TRY(hipGetLastError());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
     c->brute_stale = c->mtc_stale = true;
     c->nodes_on_device_newer = true;
-    if (acc && c->titem_ref && c->n_titems > 0) {
-        hipLaunchKernelGGL(k_refresh_items, dim3((c->n_titems + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes,
-                           c->titem_ref, c->n_titems, c->titems);
-        HIP_TRY(hipGetLastError());
-    }
     if (!rebuild) return RT_OK;
     ++c->anim_rebuilds;
     return upload_accel(c);  // a bound changed kind: rebuild from the grown nodes

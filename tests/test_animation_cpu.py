@@ -6,11 +6,16 @@ properties: grow-only, idempotent on unmoved shapes, untouched elsewhere.
 The device refit (rt_animate) is checked against orc_update_bvh on the GPU
 (tests/test_gpu_parity.py, test_device_refit_*).
 """
+import os
+import subprocess
+
 import numpy as np
 import pytest
 
 import oracle
 import rtamd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _points(rec):
@@ -136,3 +141,15 @@ def test_update_bvh_rejects_bad_ids():
     fs = _scene(3, 4)
     with pytest.raises(RuntimeError):
         oracle.update_bvh(fs, np.array([len(fs.shapes)], np.int32))
+
+
+def test_class_check_equals_classify():
+    """rt_animate's per-frame class check (rta::classify_class: classify's class
+    without the box, squared forms of its square-root tests with a 1e-9 margin and
+    classify itself inside it) equals classify on 400k triangles, many placed at
+    its thresholds, and on degenerate / non-finite records (tests/native/class_check.cpp)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "native"), "build/class_check"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "tests", "native", "build", "class_check")], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "class_check ok" in r.stdout and " 0 mismatches" in r.stdout

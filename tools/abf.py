@@ -76,7 +76,8 @@ for _ in range(F):
              "persistent": lambda x: c.set_launch(1, bool(x)), "period": lambda x: c.debug_sched_period(x), "tail": lambda x: c.set_tail(x), "tlanes": lambda x: c.debug_tail_lanes(x), "shwalk": lambda x: c.debug_shadow_walk(x),
              "spec": lambda x: c.debug_spec(x), "stack": lambda x: c.debug_lane_stack(x),
              "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x),
-             "latency": lambda x: c.set_latency_mode(x)}[k](int(v))
+             "latency": lambda x: c.set_latency_mode(x), "cone": lambda x: c.debug_cone_cull(x),
+             "heavy": lambda x: c.debug_heavy(x // 100, x % 100)}[k](int(v))
     ctxs.append((c, s))
     bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
 
