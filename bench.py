@@ -681,12 +681,15 @@ def main():
     # Python loop's figure above is kept beside it.
     serial_frames_py = serial_frames
     serial_frames_host = []
-    if grp is None and anim is None and not strong:
+    if grp is None and not strong:
         for c_ in ctxs:
             c_.set_latency_mode(1)
-        rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, a.warmup, True)
-        serial_frames_host = list(rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, a.steps,
-                                                    True) * 1e-3)
+        frames_anim = anim[1] if anim is not None else None
+        for n_ in (a.warmup, a.steps):
+            ms_ = rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, n_, True, anim=frames_anim)
+            if anim is not None:  # the C++ loop animates ctx 0 with frames 0, 1, ... (oracle bookkeeping)
+                applied[0].extend(i % len(frames_anim) for i in range(n_))
+        serial_frames_host = list(ms_ * 1e-3)
         for c_ in ctxs:
             c_.set_latency_mode(0)
         serial_frames = serial_frames_host
@@ -758,6 +761,7 @@ def main():
             "serial_frame_ms_median": float(np.median(serial_frames)) * 1e3 if serial_frames else None,
             "serial_frame_ms_median_python": float(np.median(serial_frames_py)) * 1e3 if serial_frames_py else None,
             "serial_frame_median_mode": (("C++ host loop (librthost.so rth_render_loop: camera + light upload, "
+                                          + ("rt_animate, " if anim is not None else "") +
                                           "dispatch, rt_sync per frame), rt_set_latency_mode on"
                                           ) if serial_frames_host else
                                          ("each frame waited for (rt_sync: host polls the stream), "

@@ -30,6 +30,15 @@ extern "C" {
 int rth_render_loop(struct rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
                     int height, float* dst, size_t pitch, int frames, int wait_each, double* frame_ms);
 
+/* The same with the reference's animation (src/main.cpp:436-455, uploaded by
+ * updateScene + updateBVH at :336-346): before frame i's dispatch,
+ * rt_animate(ctx, anim + (i % anim_frames) * anim_count), i.e. anim holds
+ * anim_frames consecutive sets of anim_count records of the shapes marked with
+ * rt_set_animated. anim == NULL: rth_render_loop. */
+int rth_render_loop_anim(struct rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
+                         int height, float* dst, size_t pitch, int frames, int wait_each, const FlatShape* anim,
+                         int anim_count, int anim_frames, double* frame_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -179,6 +179,7 @@ SCENE_SYMBOLS = {
 # include/rt_host.h (librthost.so: the reference's render loop as a C++ host)
 HOST_SYMBOLS = {
     "rth_render_loop": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P]),
+    "rth_render_loop_anim": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _I, _P]),
 }
 
 RT_SYMBOLS = {
@@ -282,15 +283,24 @@ def host_lib():
     return _host_lib
 
 
-def render_loop(ctx, cams, light, width, height, dst_ptr, pitch, frames, wait_each=True):
-    """rth_render_loop on ComputeShader `ctx`: `frames` frames (camera cams[i % len]),
-    each waited for (wait_each) or back to back. Returns the host wall times in ms:
-    one per frame, or [total] when not waiting for each."""
+def render_loop(ctx, cams, light, width, height, dst_ptr, pitch, frames, wait_each=True, anim=None):
+    """rth_render_loop(_anim) on ComputeShader `ctx`: `frames` frames (camera cams[i % len]),
+    each waited for (wait_each) or back to back; anim: a list of per-frame record
+    arrays of the rt_set_animated shapes, frame i animated with anim[i % len] first.
+    Returns the host wall times in ms: one per frame, or [total] when not waiting."""
     cams = as_records(np.asarray(cams), CAMERA_DTYPE).reshape(-1)
     light = as_records(np.asarray(light), LIGHT_DTYPE).reshape(1)
     out = np.zeros(max(1, frames), np.float64)
-    rc = host_lib().rth_render_loop(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height),
-                                    C.c_void_p(dst_ptr), int(pitch), int(frames), int(bool(wait_each)), _ptr(out))
+    if anim is not None:
+        recs = as_records(np.concatenate([np.asarray(f).reshape(-1) for f in anim]), SHAPE_DTYPE)
+        per = len(np.asarray(anim[0]).reshape(-1))
+        rc = host_lib().rth_render_loop_anim(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height),
+                                             C.c_void_p(dst_ptr), int(pitch), int(frames), int(bool(wait_each)),
+                                             _ptr(recs), per, len(anim), _ptr(out))
+    else:
+        rc = host_lib().rth_render_loop(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height),
+                                        C.c_void_p(dst_ptr), int(pitch), int(frames), int(bool(wait_each)),
+                                        _ptr(out))
     if rc != 0:
         raise RTError("rth_render_loop", rc)
     return out if wait_each else out[:1]
