@@ -603,3 +603,36 @@ def test_host_render_loop_frames(ctx):
     assert np.array_equal(out.cpu().numpy(), refs[1])
     with pytest.raises(rtamd.RTError):
         rtamd.render_loop(ctx, cams, fs.light, W, H, out.data_ptr(), W * 12, 1, True)  # pitch < 16 W
+
+
+def test_host_render_loop_animated(ctx):
+    """rth_render_loop_anim: the C++ loop animating the car's wheels (rt_animate before
+    each dispatch) leaves the same frame and node boxes as the same animation frames
+    given one by one through the Python binding."""
+    import bench
+    W, H = 480, 270
+    fs = rtamd.generate(3, 0, W, H)
+    ids, frames = bench.wheel_frames(fs, 7)
+    out = torch.full((H, W, 4), -7.0, dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3)
+    ctx.set_animated(ids)
+    ms = rtamd.render_loop(ctx, fs.camera, fs.light, W, H, out.data_ptr(), W * 16, 10, True, anim=frames)
+    assert ms.shape == (10,) and (ms > 0).all()
+    got, got_nodes = out.cpu().numpy(), ctx.read_nodes(len(fs.nodes))
+    two = rtamd.ComputeShader(0)
+    try:
+        two.upload(fs)
+        two.set_params(W, H, 3)
+        two.set_animated(ids)
+        for i in range(10):
+            two.set_camera(fs.camera)
+            two.set_light(fs.light)
+            two.animate(frames[i % 7])
+        want = two.render(W, H)
+        assert np.array_equal(got, want)
+        assert np.array_equal(got_nodes, two.read_nodes(len(fs.nodes)))
+    finally:
+        two.close()
+        ctx.upload(fs)
