@@ -104,6 +104,17 @@ int rt_group_set_params(struct rt_group* g, const rt_params* params);
  * calls it for every frame, in the same order. */
 int rt_group_dispatch(struct rt_group* g, int width, int height, int stripe);
 
+/* Rows that can only be background stay off the links (default 1): a ray that
+ * misses the root node's box draws the background of its row
+ * (gpu_shader.comp:436-458), and every camera ray of an image row lies in one
+ * plane through the camera, so a row whose plane has every corner of the root
+ * box on one side (with a 1e-4 rad margin) is background. Each rank computes the
+ * same band of rows that may meet the box from the camera, parameters and tree
+ * it was given; the peers send only their rows inside it and rank 0 writes the
+ * others' background (1080p car: 283 of 1080 rows). Applies to the BVH branch
+ * with at least one bounce. The image does not depend on it. */
+int rt_group_set_sky_rows(struct rt_group* g, int on);
+
 /* Rank 0's stripes per period (1 <= share <= 64; default 1). Rank 0's rows
  * never cross a link, so when rank 0's ingress bounds the frame (7 peers' rows
  * into one GPU), a larger share moves fewer bytes: of a frame's B bytes, rank 0

@@ -36,6 +36,7 @@
 #include "../../include/rt_api.h"
 #include "../../include/rt_group.h"
 #include "group_wait.h"
+#include "sky_rows.h"
 #include "rt_internal.h"
 
 namespace {
@@ -94,19 +95,36 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 // rows (rt_dispatch_rows_ex RGB32F), one per rank r >= 1 in rank order; compact
 // row cr of rank r is image row (k - 1 + r) * s + (cr / s) * (k + P - 1) * s + cr % s
 // (rank_rows). Rows past a rank's count map to y >= height and are skipped. One
-// coalesced read and one streaming RGBA store (alpha 1) per pixel.
+// coalesced read and one streaming RGBA store (alpha 1) per pixel. Rows outside
+// [yb0, yb1) were not sent (sky_rows.h): they are the background of their row,
+// written here with the shader's own float operations (gpu_shader.comp:436,
+// mix = x + a (y - x); rt_kernels.hip background()).
 __global__ __launch_bounds__(256) void k_unstripe(const float* __restrict__ staging, int rows1, int width, int height,
-                                                   int s, int k, int P, f4v* __restrict__ img, size_t pitch_f4) {
+                                                   int s, int k, int P, f4v* __restrict__ img, size_t pitch_f4,
+                                                   int yb0, int yb1, float resY) {
     const int x = blockIdx.x * blockDim.x + threadIdx.x;
     const int by = blockIdx.y;  // (rank - 1) * rows1 + compact row
     if (x >= width) return;
     const int rank = 1 + by / rows1, cr = by - (rank - 1) * rows1;
     const int y = (k - 1 + rank) * s + (cr / s) * (k + P - 1) * s + cr % s;
     if (y >= height) return;
-    const float* p = staging + 3 * (static_cast<size_t>(by) * width + x);
-    const f4v v = {__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2),
-                   1.0f};
+    f4v v;
+    if (y >= yb0 && y < yb1) {
+        const float* p = staging + 3 * (static_cast<size_t>(by) * width + x);
+        v = f4v{__builtin_nontemporal_load(p), __builtin_nontemporal_load(p + 1), __builtin_nontemporal_load(p + 2),
+                1.0f};
+    } else {
+        const float a = static_cast<float>(y) / resY;
+        v = f4v{0.05f + a * (0.5f - 0.05f), 0.07f + a * (0.7f - 0.07f), 0.1f + a * (1.0f - 0.1f), 1.0f};
+    }
     __builtin_nontemporal_store(v, &img[static_cast<size_t>(y) * pitch_f4 + x]);
+}
+
+// The rank's rows (rank_rows) that lie above image row y: its compact rows below y.
+int rows_below(int y0, int stripe, int period, int rows, int y) {
+    if (y <= y0) return 0;
+    const int t = y - y0;
+    return std::min(rows, (t / period) * stripe + std::min(t % period, stripe));
 }
 
 }  // namespace
@@ -122,6 +140,12 @@ struct rt_group {
     int last_slot = -1;  // slot of the last dispatched frame
     bool have_scene = false;
     bool broken = false;        // an RCCL group after an abort: every call fails
+    // sky rows (sky_rows.h): the frame's camera, parameters and root box as set on every rank
+    FlatCamera cam{};
+    rt_params params{};
+    float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
+    bool have_cam = false, have_params = false, have_root = false;
+    bool sky_rows = true;       // rt_group_set_sky_rows
     double timeout_ms = 60000;  // rt_group_set_timeout
     bool phase_timing = true;   // rt_group_set_phase_timing
     // phase times of member `tm` (rank 0 when local, else the first member)
@@ -438,12 +462,26 @@ int rt_group_member_slot(rt_group* g, int k, int slot, rt_ctx** ctx) {
 int rt_group_upload_scene(rt_group* g, const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx,
                           int I) {
     const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_upload_scene(c, shapes, S, nodes, N, idx, I); });
-    if (rc == RT_OK) g->have_scene = true;
+    if (rc == RT_OK) {
+        g->have_scene = true;
+        g->have_root = N > 0 && nodes;  // the root the shader starts from (gpu_shader.comp:386)
+        if (g->have_root) {
+            const FlatNode& r = nodes[N - 1];
+            const float lo[3] = {r.boundsMin.x, r.boundsMin.y, r.boundsMin.z}, hi[3] = {r.boundsMax.x, r.boundsMax.y, r.boundsMax.z};
+            std::memcpy(g->root_lo, lo, sizeof lo);
+            std::memcpy(g->root_hi, hi, sizeof hi);
+        }
+    }
     return rc;
 }
 
 int rt_group_set_camera(rt_group* g, const FlatCamera* cam) {
-    return each_ctx(g, [&](rt_ctx* c) { return rt_set_camera(c, cam); });
+    const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_set_camera(c, cam); });
+    if (rc == RT_OK) {
+        g->cam = *cam;
+        g->have_cam = true;
+    }
+    return rc;
 }
 
 int rt_group_set_light(rt_group* g, const FlatLight* l) {
@@ -451,7 +489,18 @@ int rt_group_set_light(rt_group* g, const FlatLight* l) {
 }
 
 int rt_group_set_params(rt_group* g, const rt_params* p) {
-    return each_ctx(g, [&](rt_ctx* c) { return rt_set_params(c, p); });
+    const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_set_params(c, p); });
+    if (rc == RT_OK) {
+        g->params = *p;
+        g->have_params = true;
+    }
+    return rc;
+}
+
+int rt_group_set_sky_rows(rt_group* g, int on) {
+    if (!g) return RT_ERR_INVALID;
+    g->sky_rows = on != 0;
+    return RT_OK;
 }
 
 int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
@@ -509,6 +558,21 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             }
         }
     }
+    // Rows that can only be background (sky_rows.h) stay off the links: every rank
+    // computes the same band [yb0, yb1) from the same camera, box and parameters; a
+    // peer sends its compact rows inside it, rank 0 writes the rest as background.
+    // Only where the reference draws the background for a ray missing the root:
+    // the BVH branch with at least one bounce and a root box.
+    int yb0 = 0, yb1 = height;
+    if (g->sky_rows && P > 1 && g->have_cam && g->have_params && g->have_root && g->params.useBVH &&
+        g->params.maxBounces >= 1 && g->params.resY > 0)
+        rtg::sky_band(g->cam, g->root_lo, g->root_hi, height, g->params.resY, &yb0, &yb1);
+    // the peers' compact row range inside the band (one contiguous run each)
+    auto band_of = [&](int rank, int& c0, int& c1) {
+        const Rows w = rank_rows(height, P, stripe, k, rank);
+        c0 = rows_below(w.y0, w.stripe, w.period, w.rows, yb0);
+        c1 = rows_below(w.y0, w.stripe, w.period, w.rows, yb1);
+    };
     PhaseRec& ph = g->ring[g->ring_pos];
     if (ph.pending) {
         // kPhaseRing frames ago. Nothing makes the host wait between dispatches, so that
@@ -577,12 +641,16 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             ncclResult_t res = ncclSuccess;
             if (b.rank == 0) {
                 for (int r = 1; r < P && res == ncclSuccess; ++r) {
-                    const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, r).rows) * width * 3;
-                    if (n) res = ncclRecv(slot_ptr(r), n, ncclFloat32, r, b.comm, b.cstream);
+                    int c0, c1;
+                    band_of(r, c0, c1);
+                    const size_t n = static_cast<size_t>(c1 - c0) * width * 3;
+                    if (n) res = ncclRecv(slot_ptr(r) + c0 * row_b, n, ncclFloat32, r, b.comm, b.cstream);
                 }
             } else {
-                const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, b.rank).rows) * width * 3;
-                if (n) res = ncclSend(s.buf, n, ncclFloat32, 0, b.comm, b.cstream);
+                int c0, c1;
+                band_of(b.rank, c0, c1);
+                const size_t n = static_cast<size_t>(c1 - c0) * width * 3;
+                if (n) res = ncclSend(reinterpret_cast<char*>(s.buf) + c0 * row_b, n, ncclFloat32, 0, b.comm, b.cstream);
             }
             if (res != ncclSuccess) {
                 ncclGroupEnd();
@@ -612,9 +680,13 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         if (g->phase_timing && g->tm == g->root) F_HIP(hipEventRecord(ph.ev[2], r.cstream));
         for (Member& b : g->m) {
             if (b.rank == 0) continue;
-            const size_t n = static_cast<size_t>(rank_rows(height, P, stripe, k, b.rank).rows) * row_b;
+            int c0, c1;
+            band_of(b.rank, c0, c1);
+            const size_t n = static_cast<size_t>(c1 - c0) * row_b;
             F_HIP(hipStreamWaitEvent(r.cstream, b.slot[j].rendered, 0));
-            if (n) F_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank), r.device, b.slot[j].buf, b.device, n, r.cstream));
+            if (n)
+                F_HIP(hipMemcpyPeerAsync(slot_ptr(b.rank) + c0 * row_b, r.device,
+                                         reinterpret_cast<char*>(b.slot[j].buf) + c0 * row_b, b.device, n, r.cstream));
             b.slot[j].used = true;  // its next render waits for rs.fanned
         }
         if (g->phase_timing && g->tm == g->root) {
@@ -634,7 +706,7 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             if (g->phase_timing && g->tm == g->root) F_HIP(hipEventRecord(ph.ev[4], rs.stream));
             hipLaunchKernelGGL(k_unstripe, dim3((width + 255) / 256, (P - 1) * rows1), dim3(256), 0, rs.stream,
                                rs.staging, rows1, width, height, stripe, k, P, reinterpret_cast<f4v*>(rs.img),
-                               rs.img_pitch / 16);
+                               rs.img_pitch / 16, yb0, yb1, g->params.resY);
             F_HIP(hipGetLastError());
             if (g->phase_timing && g->tm == g->root) {
                 F_HIP(hipEventRecord(ph.ev[5], rs.stream));

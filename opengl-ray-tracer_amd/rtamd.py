@@ -228,6 +228,7 @@ GROUP_SYMBOLS = {
     "rt_group_frames": (_I, [_P]),
     "rt_group_set_timeout": (_I, [_P, C.c_double]),
     "rt_group_set_phase_timing": (_I, [_P, _I]),
+    "rt_group_set_sky_rows": (_I, [_P, _I]),
     "rt_group_check": (_I, [_P]),
     "rt_group_phase_times": (_I, [_P, _P]),
     "rt_group_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
@@ -866,6 +867,10 @@ class Group:
     def check(self):
         """Non-blocking RCCL asynchronous-error poll (rt_group_check)."""
         self._chk(self._lib.rt_group_check(self._h), "rt_group_check")
+
+    def set_sky_rows(self, on):
+        """rt_group_set_sky_rows: keep background-only rows off the links (default on)."""
+        self._chk(self._lib.rt_group_set_sky_rows(self._h, int(bool(on))), "rt_group_set_sky_rows")
 
     def set_phase_timing(self, on):
         """rt_group_set_phase_timing: record the render / fan-in / unstripe events (default on)."""

@@ -67,3 +67,15 @@ def test_group_wait_is_bounded():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "wait_check ok" in r.stdout
+
+
+def test_sky_rows_band_is_conservative():
+    """rt_group's sky-row band (csrc/sky_rows.h): over 3,000 random cameras and root
+    boxes, every pixel of every row it calls background has a camera ray (getRay in
+    float, as the kernels) that misses the box under the GLSL slab test
+    (tests/native/sky_check.cpp)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "native"), "build/sky_check"], check=True)
+    r = subprocess.run([os.path.join(ROOT, "tests", "native", "build", "sky_check")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sky_check ok" in r.stdout and " 0 violations" in r.stdout

@@ -636,3 +636,37 @@ def test_host_render_loop_animated(ctx):
     finally:
         two.close()
         ctx.upload(fs)
+
+
+@pytest.mark.parametrize("ranks,share", [(2, 1), (3, 2), (8, 1)])
+def test_group_sky_rows_identical(ctx, ranks, share):
+    """rt_group_set_sky_rows: the peers keep the background-only rows (every corner of
+    the root box on one side of the row's camera-ray plane) off the fan-in and rank 0
+    writes their background. Frames with the car camera (its top ~26 % of rows is
+    sky), a camera tilted up into the sky, one looking down at the road, and the
+    brute branch (where the root box does not gate) equal the single dispatch, with
+    the shortcut on and off."""
+    W, H = 480, 270
+    base = rtamd.generate(3, 0, W, H)
+    cams = [base.camera]
+    for tgt in ((0.0, -60.0, 0.0), (0.0, 30.0, 0.0)):
+        sc = rtamd.Scene().generate(3, 0, W / H)
+        sc.LookAt(tgt)
+        cams.append(sc.serializeScene().camera)
+    g = rtamd.Group([0] * ranks, rtamd.GATHER_COPY, frames=2)
+    try:
+        g.upload(base)
+        g.set_root_share(share)
+        for bvh in (True, False):
+            g.set_params(W, H, 3, bvh)
+            for cam in cams:
+                fs = rtamd.FlatScene(base.shapes, base.nodes, base.indices, cam, base.light)
+                ctx.upload(fs)
+                ctx.set_params(W, H, 3, bvh)
+                ref = ctx.render(W, H)
+                for on in (True, False):
+                    g.set_sky_rows(on)
+                    g.set_camera(cam)
+                    assert np.array_equal(g.render(W, H, 8), ref), f"bvh={bvh} sky_rows={on}"
+    finally:
+        g.close()
