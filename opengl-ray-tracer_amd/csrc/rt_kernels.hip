@@ -1747,12 +1747,26 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 o[5] = mt;
             }
         }
-        if (COST && kp.tile_cost && part <= 1) {
-            // a split tile's cost: its first band's, times the bands (one record per tile)
-            const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests) *
-                                            static_cast<unsigned long long>(part ? kp.heavy_parts : 1);
-            const unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
-            if (lane == 0) {
+        if (COST && kp.tile_cost) {
+            const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
+            unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
+            bool rec = part == 0;
+            if (part > 0 && lane == 0) {
+                // a split tile's cost is the sum of its parts' (one record per tile, by the
+                // part that finishes last). Round 3 took the first band's times the bands: a
+                // heavy tile whose first band is sky then ranked low, ran whole and late,
+                // ranked high again, and so on (the latency-mode car waited frame 0.25 or
+                // 0.287 ms by the phase of that cycle, r04l)
+                const int hk = slot / kp.heavy_parts;
+                atomicAdd(&kp.heavy_acc[hk], wk);
+                __threadfence();
+                if (atomicAdd(&kp.heavy_acc[kp.heavy_k + hk], 1u) == static_cast<unsigned>(kp.heavy_parts - 1)) {
+                    __threadfence();
+                    wk = atomicAdd(&kp.heavy_acc[hk], 0u);
+                    rec = true;
+                }
+            }
+            if (lane == 0 && rec) {
                 kp.tile_cost[tile] = wk;
                 atomicAdd(&kp.sched_hist[(tile / kOrderThreads) * kOrderBuckets + work_bucket(wk)], 1u);
             }
@@ -2232,6 +2246,8 @@ struct rt_ctx {
     // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
     int schedule = RT_SCHED_COST;
     unsigned* sched_cost = nullptr;
+    unsigned* heavy_acc = nullptr;  // split heavy tiles' part sums + counts (cost-recording dispatches)
+    size_t heavy_acc_cap = 0;
     int* sched_order = nullptr;
     unsigned* sched_sets = nullptr;      // 2 sets of per-group bucket histograms, alternating by frame
     int sched_parity = 0;
@@ -3206,6 +3222,19 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 k2.heavy_parts = hp;
             }
         }
+        k2.heavy_acc = nullptr;
+        if (k2.tile_cost && k2.heavy_k > 0) {  // the split tiles' part sums and counts (kernel comment)
+            const size_t need = 2 * static_cast<size_t>(k2.heavy_k);
+            if (c->heavy_acc_cap < need) {
+                hipFree(c->heavy_acc);
+                c->heavy_acc = nullptr;
+                c->heavy_acc_cap = 0;
+                if (hipMalloc(&c->heavy_acc, need * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                c->heavy_acc_cap = need;
+            }
+            HIP_TRY(hipMemsetAsync(c->heavy_acc, 0, need * sizeof(unsigned), c->stream));
+            k2.heavy_acc = c->heavy_acc;
+        }
         // Animated scenes keep the scene tree: rt_animate refits its boxes and items (prepare_animation).
         const int troot = c->tree_mode == RT_TREE_SCENE ? c->st_root : kNoChild;
         // production shape on a dispatch that records no tile work: the counter-free kernel
@@ -3416,6 +3445,7 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->tile_times);
     hipFree(c->tile_order);
     hipFree(c->sched_cost);
+    hipFree(c->heavy_acc);
     hipFree(c->sched_order);
     hipFree(c->sched_sets);
     hipFree(c->anim_maps);

@@ -27,26 +27,15 @@ import rtamd  # noqa: E402
 
 SETTINGS = {
     "default": {},
-    "split16x16": {"split": (16, 16)},
-    "split32x8": {"split": (32, 8)},
-    "split8x8": {"split": (8, 8)},
-    "split16x32": {"split": (16, 32)},
-    "split32x16": {"split": (32, 16)},
-    "heavy127x2": {"heavy": (127, 2)},
-    "heavy255x2": {"heavy": (255, 2)},
-    "heavy63x4": {"heavy": (63, 4)},
-    "heavy31x4": {"heavy": (31, 4)},
-    "heavy63x8": {"heavy": (63, 8)},
-    "heavy31x8": {"heavy": (31, 8)},
-    "heavy127x4": {"heavy": (127, 4)},
-    "no_heavy": {"heavy": (0, 1)},
-    "h63x4_s16x16": {"heavy": (63, 4), "split": (16, 16)},
-    "h255x2_s16x16": {"heavy": (255, 2), "split": (16, 16)},
-    "h63x4_s32x16": {"heavy": (63, 4), "split": (32, 16)},
-    "h31x8_s16x16": {"heavy": (31, 8), "split": (16, 16)},
-    "lanek506": {"lane_k": (506, 2)},
-    "lanek126": {"lane_k": (126, 2)},
+    # round 4 sweep 1 (latency mode's heavy tiles then 1/512 x 2 waves): profiles/r04e_latency_sweep.json
+    "heavy63x2": {"heavy": (63, 2)},
     "lanek0": {"lane_k": (0, 0)},
+    "lanek0_h127x4": {"lane_k": (0, 0), "heavy": (127, 4)},
+    "lanek0_h31x4": {"lane_k": (0, 0), "heavy": (31, 4)},
+    "lanek0_s16x16": {"lane_k": (0, 0), "split": (16, 16)},
+    "lanek64m2": {"lane_k": (64, 2)},
+    "lanek1024m2": {"lane_k": (1024, 2)},
+    "lanek253m3": {"lane_k": (253, 3)},
 }
 
 
