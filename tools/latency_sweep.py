@@ -68,7 +68,7 @@ def main():
         c.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
         c.sync()
 
-    ref, res, same = None, {n: [] for n in names}, {}
+    ref, res, same, pattern = None, {n: [] for n in names}, {}, {}
     for blk in range(a.blocks):
         for n in names:
             apply(SETTINGS[n])
@@ -80,13 +80,19 @@ def main():
                 frame()
                 w.append(time.perf_counter() - t0)
             res[n].append(float(np.median(w)) * 1e3)
+            wa = np.array(w) * 1e3
+            slow = wa > 0.5 * (np.percentile(wa, 10) + np.percentile(wa, 90))
+            pattern.setdefault(n, []).append({"slow_frac": float(slow.mean()),
+                                              "slow_by_phase8": [int(slow[k::8].sum()) for k in range(8)],
+                                              "p10": float(np.percentile(wa, 10)), "p90": float(np.percentile(wa, 90)),
+                                              "first40": "".join("x" if v else "." for v in slow[:40])})
             img = out.cpu().numpy()
             if ref is None:
                 ref = img
             same[n] = same.get(n, True) and bool(np.array_equal(img, ref))
     print(json.dumps({"config": a.config, "frames": a.frames, "blocks": a.blocks,
                       "waited_ms": {n: float(np.median(v)) for n, v in res.items()},
-                      "per_block": res, "image_equal": same}))
+                      "per_block": res, "pattern": pattern, "image_equal": same}))
     c.close()
 
 
