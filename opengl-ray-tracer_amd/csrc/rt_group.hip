@@ -57,6 +57,7 @@ struct Slot {
     hipEvent_t rendered = nullptr;  // this member's stripes are written
     hipEvent_t fanned = nullptr;    // the fan-in of the slot's frame is done (sent / received / copied)
     hipEvent_t released = nullptr;  // the slot's buffers may be written again
+    hipEvent_t sync_ev = nullptr;   // recorded behind the stream's work by each bounded wait
     bool used = false;              // `released` / `fanned` have been recorded
 };
 
@@ -64,6 +65,7 @@ struct Member {
     int rank = 0, device = 0;
     std::vector<Slot> slot;
     hipStream_t cstream = nullptr;  // fan-in stream: every frame's send/recv (or copies) in frame order
+    hipEvent_t csync_ev = nullptr;  // recorded behind cstream's work by each bounded wait
     ncclComm_t comm = nullptr;
 };
 
@@ -180,6 +182,7 @@ int add_slot(Member& b) {
     G_HIP(hipEventCreateWithFlags(&s.rendered, hipEventDisableTiming));
     G_HIP(hipEventCreateWithFlags(&s.fanned, hipEventDisableTiming));
     G_HIP(hipEventCreateWithFlags(&s.released, hipEventDisableTiming));
+    G_HIP(hipEventCreateWithFlags(&s.sync_ev, hipEventDisableTiming));
     return rtx::create_ctx(&s.ctx, b.device, s.stream);  // straight on the slot's stream (rt_internal.h)
 }
 
@@ -191,6 +194,7 @@ int add_member(rt_group* g, int rank, int device) {
     Member& b = g->m.back();
     G_HIP(hipSetDevice(device));
     G_HIP(rtx::make_stream(&b.cstream, true));
+    G_HIP(hipEventCreateWithFlags(&b.csync_ev, hipEventDisableTiming));
     return add_slot(b);
 }
 
@@ -235,27 +239,39 @@ int fail(rt_group* g, int rc) {
 }
 
 // Outstanding work on any of the group's streams: 1 yes, 0 none, -1 device error.
-// The last dispatched frame's slot first: while it runs (the usual case in a wait)
-// one query answers.
+// Polls the events mark_streams recorded behind each stream's work (an event query
+// sees a kernel end ~1.5 us sooner than hipStreamQuery, tools/native/wait_probe.hip);
+// the last dispatched frame's slot first: while it runs one query answers.
 int pending(rt_group* g) {
-    auto q = [](hipStream_t s) {
-        if (!s) return 0;
-        const hipError_t e = hipStreamQuery(s);
-        return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+    auto q = [](hipEvent_t e) {
+        if (!e) return 0;
+        const hipError_t r = hipEventQuery(e);
+        return r == hipSuccess ? 0 : (r == hipErrorNotReady ? 1 : -1);
     };
     if (g->last_slot >= 0)
         for (Member& b : g->m)
             if (g->last_slot < static_cast<int>(b.slot.size())) {
-                const int r = q(b.slot[g->last_slot].stream);
+                const int r = q(b.slot[g->last_slot].sync_ev);
                 if (r) return r;
             }
     for (Member& b : g->m) {
-        int r = q(b.cstream);
+        int r = q(b.csync_ev);
         if (r) return r;
         for (Slot& s : b.slot)
-            if ((r = q(s.stream))) return r;
+            if ((r = q(s.sync_ev))) return r;
     }
     return 0;
+}
+
+// Records every stream's sync event behind its current work (before a bounded wait).
+int mark_streams(rt_group* g) {
+    for (Member& b : g->m) {
+        if (hipSetDevice(b.device) != hipSuccess) return RT_ERR_DEVICE;
+        if (b.cstream && b.csync_ev && hipEventRecord(b.csync_ev, b.cstream) != hipSuccess) return RT_ERR_DEVICE;
+        for (Slot& s : b.slot)
+            if (s.stream && s.sync_ev && hipEventRecord(s.sync_ev, s.stream) != hipSuccess) return RT_ERR_DEVICE;
+    }
+    return RT_OK;
 }
 
 bool comm_error(rt_group* g) {
@@ -271,6 +287,7 @@ bool comm_error(rt_group* g) {
 // The bounded wait (group_wait.h); on a timeout or an RCCL error the communicators
 // are aborted.
 int wait_all(rt_group* g) {
+    if (mark_streams(g) != RT_OK) return fail(g, RT_ERR_DEVICE);
     const rtg::WaitResult w = rtg::wait_bounded([g] { return pending(g); }, [g] { return comm_error(g); },
                                                  g->timeout_ms);
     if (w == rtg::kWaitDone) return RT_OK;
@@ -401,8 +418,10 @@ int rt_group_destroy(rt_group* g) {
             if (s.rendered) hipEventDestroy(s.rendered);
             if (s.fanned) hipEventDestroy(s.fanned);
             if (s.released) hipEventDestroy(s.released);
+            if (s.sync_ev) hipEventDestroy(s.sync_ev);
             if (s.stream) hipStreamDestroy(s.stream);
         }
+        if (b.csync_ev) hipEventDestroy(b.csync_ev);
         if (b.cstream) hipStreamDestroy(b.cstream);
     }
     if (!g->m.empty()) {
@@ -440,6 +459,7 @@ int rt_group_set_frames(rt_group* g, int frames) {
             if (s.rendered) hipEventDestroy(s.rendered);
             if (s.fanned) hipEventDestroy(s.fanned);
             if (s.released) hipEventDestroy(s.released);
+            if (s.sync_ev) hipEventDestroy(s.sync_ev);
             if (s.stream) hipStreamDestroy(s.stream);
             b.slot.pop_back();
         }

@@ -2183,6 +2183,7 @@ struct rt_ctx {
     hipStream_t stream = nullptr;
     bool own_stream = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;      // used once the ring is full
+    hipEvent_t sync_ev = nullptr;                  // rt_sync's poll target
     hipEvent_t last0 = nullptr, last1 = nullptr;  // events of the latest dispatch
     bool timed = false;
     // per-dispatch event pairs since the last rt_kernel_times call
@@ -3456,6 +3457,7 @@ int rt_destroy(rt_ctx* c) {
     }
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
+    if (c->sync_ev) hipEventDestroy(c->sync_ev);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -3791,13 +3793,18 @@ int rt_sync(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     // A host that waits for every frame (the reference's loop, src/main.cpp:290-462)
-    // waits ~0.25 ms per frame: poll the stream back to back (yielding the core) for
-    // the first rtg::kSpinMs, so the frame's end is seen within a poll, instead of
-    // the runtime's interrupt-driven wake-up; past that, nap between polls
-    // (csrc/group_wait.h). No deadline: a single context has no peer to wait on.
+    // waits ~0.25 ms per frame: poll back to back (yielding the core) for the first
+    // rtg::kSpinMs, then nap between polls (csrc/group_wait.h). The poll is on an event
+    // recorded behind the stream's work, not on the stream: hipStreamQuery saw an empty
+    // kernel end 15.2 us after its launch, the event 10.7 us (and 247.3 against 245.8 us
+    // for a 235-us kernel; tools/native/wait_probe.hip, profiles/r04_wait_probe.txt). No
+    // deadline: a single context has no peer to wait on.
+    if (!c->sync_ev && hipEventCreateWithFlags(&c->sync_ev, hipEventDisableTiming) != hipSuccess) return RT_ERR_DEVICE;
+    HIP_TRY(hipEventRecord(c->sync_ev, c->stream));
+    const hipEvent_t ev = c->sync_ev;
     const rtg::WaitResult w = rtg::wait_bounded(
-        [c] {
-            const hipError_t e = hipStreamQuery(c->stream);
+        [ev] {
+            const hipError_t e = hipEventQuery(ev);
             return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
         },
         [] { return false; }, 0.0);
