@@ -57,7 +57,8 @@ struct Slot {
     hipEvent_t rendered = nullptr;  // this member's stripes are written
     hipEvent_t fanned = nullptr;    // the fan-in of the slot's frame is done (sent / received / copied)
     hipEvent_t released = nullptr;  // the slot's buffers may be written again
-    hipEvent_t sync_ev = nullptr;   // recorded behind the stream's work by each bounded wait
+    hipEvent_t sync_ev = nullptr;   // recorded behind the stream's work by a bounded wait
+    bool dirty = false;             // work was queued on `stream` since sync_ev was last recorded
     bool used = false;              // `released` / `fanned` have been recorded
 };
 
@@ -65,7 +66,8 @@ struct Member {
     int rank = 0, device = 0;
     std::vector<Slot> slot;
     hipStream_t cstream = nullptr;  // fan-in stream: every frame's send/recv (or copies) in frame order
-    hipEvent_t csync_ev = nullptr;  // recorded behind cstream's work by each bounded wait
+    hipEvent_t csync_ev = nullptr;  // recorded behind cstream's work by a bounded wait
+    bool cdirty = false;            // work was queued on cstream since csync_ev was last recorded
     ncclComm_t comm = nullptr;
 };
 
@@ -263,15 +265,31 @@ int pending(rt_group* g) {
     return 0;
 }
 
-// Records every stream's sync event behind its current work (before a bounded wait).
+// Records the sync event of every stream that was given work since its last record,
+// behind that work (before a bounded wait). A waited frame marks one or two streams:
+// each record is a marker packet on the stream (every stream marked each time cost a
+// 1-rank group's waited frame 22 us, r04o).
 int mark_streams(rt_group* g) {
     for (Member& b : g->m) {
         if (hipSetDevice(b.device) != hipSuccess) return RT_ERR_DEVICE;
-        if (b.cstream && b.csync_ev && hipEventRecord(b.csync_ev, b.cstream) != hipSuccess) return RT_ERR_DEVICE;
+        if (b.cdirty && b.cstream && b.csync_ev) {
+            if (hipEventRecord(b.csync_ev, b.cstream) != hipSuccess) return RT_ERR_DEVICE;
+            b.cdirty = false;
+        }
         for (Slot& s : b.slot)
-            if (s.stream && s.sync_ev && hipEventRecord(s.sync_ev, s.stream) != hipSuccess) return RT_ERR_DEVICE;
+            if (s.dirty && s.stream && s.sync_ev) {
+                if (hipEventRecord(s.sync_ev, s.stream) != hipSuccess) return RT_ERR_DEVICE;
+                s.dirty = false;
+            }
     }
     return RT_OK;
+}
+
+void mark_all_dirty(rt_group* g) {
+    for (Member& b : g->m) {
+        b.cdirty = true;
+        for (Slot& s : b.slot) s.dirty = true;
+    }
 }
 
 bool comm_error(rt_group* g) {
@@ -482,6 +500,7 @@ int rt_group_member_slot(rt_group* g, int k, int slot, rt_ctx** ctx) {
 int rt_group_upload_scene(rt_group* g, const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx,
                           int I) {
     const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_upload_scene(c, shapes, S, nodes, N, idx, I); });
+    if (g) mark_all_dirty(g);
     if (rc == RT_OK) {
         g->have_scene = true;
         g->have_root = N > 0 && nodes;  // the root the shader starts from (gpu_shader.comp:386)
@@ -593,6 +612,10 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         c0 = rows_below(w.y0, w.stripe, w.period, w.rows, yb0);
         c1 = rows_below(w.y0, w.stripe, w.period, w.rows, yb1);
     };
+    for (Member& b : g->m) {  // the streams this frame queues work on (mark_streams), errors included
+        b.slot[j].dirty = true;
+        b.cdirty = b.cdirty || P > 1;
+    }
     PhaseRec& ph = g->ring[g->ring_pos];
     if (ph.pending) {
         // kPhaseRing frames ago. Nothing makes the host wait between dispatches, so that
