@@ -227,7 +227,8 @@ int rt_set_launch(struct rt_ctx* ctx, int waves_per_block, int persistent);
 int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 
 /* Tile dispatch order of the accelerated kernel. RT_SCHED_ROWS: row-major.
- * RT_SCHED_COST (default): every dispatch records each 8x8 tile's duration,
+ * RT_SCHED_COST (default): a dispatch records each 8x8 tile's duration (its
+ * wave's wall time, in 40 ns units; every 8th frame once the order exists),
  * and the next dispatch with the same tile count starts the tiles in
  * decreasing order of those durations (longest first), so the frame is not
  * left waiting on expensive tiles that started late. The order only changes
@@ -242,8 +243,8 @@ int rt_set_schedule(struct rt_ctx* ctx, int mode);
  * reference's own loop, src/main.cpp:290-462) rather than keeping frames in
  * flight. 1: the accelerated kernel's instance with split walks in sparse
  * waves (idle lanes help a tile's few live rays) and, on frames not already
- * split, the heaviest 1/512 of the tiles as four waves each. Shortens one frame
- * (car: -6 to -8 %) and costs throughput when frames overlap. 0 (default): off.
+ * split, the heaviest 1/512 of the tiles as two waves each. Shortens one frame
+ * (car: -15 %) and costs throughput when frames overlap. 0 (default): off.
  * Same image either way. */
 int rt_set_latency_mode(struct rt_ctx* ctx, int on);
 

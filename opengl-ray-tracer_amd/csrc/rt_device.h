@@ -108,6 +108,7 @@ struct KParams {
     int heavy_k, heavy_parts;                // the first heavy_k tiles of tile_order run as heavy_parts
                                              // waves each, one band of 64/heavy_parts pixels per wave
     unsigned* __restrict__ tile_cost;        // optional: each tile's work (rt_set_schedule)
+    int cost_time;                           // tile_cost in wave wall-clock ticks, not lane work
     unsigned* __restrict__ heavy_acc;        // with tile_cost and heavy_k: per split tile its parts' summed
                                              // work, then per split tile the parts done (zeroed per dispatch)
     unsigned* __restrict__ sched_hist;       // with tile_cost: work-bucket histogram copies of this frame

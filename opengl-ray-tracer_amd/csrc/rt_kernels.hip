@@ -1710,7 +1710,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
     const int hs = kp.heavy_k * kp.heavy_parts;
     while (tile < kp.tiles + hs - kp.heavy_k) {
         unsigned long long t0 = 0;
-        if (TIMED) t0 = wall_clock64();
+        if (TIMED || (COST && kp.cost_time)) t0 = wall_clock64();
         int part = 0;
         const int slot = tile;
         if (kp.tile_order) {  // dispatch order -> image tile (a permutation)
@@ -1722,7 +1722,9 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
             }
         }
         WalkCount wc{0u, 0u, 0u, 0u};
-        unsigned long long* rec = TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(tile) : nullptr;
+        // a split tile's parts stamp records tiles + slot (rt_debug_tile_times with room for them)
+        unsigned long long* rec =
+            TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(part > 0 ? kp.tiles + slot : tile) : nullptr;
         accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, part, stk, stt, kp.lane_stack, wc, rec,
                                                 slot < kp.lane_k);
         if (TIMED) {
@@ -1748,7 +1750,13 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
             }
         }
         if (COST && kp.tile_cost) {
-            const unsigned long long work = wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
+            // the tile's cost: its wave's wall time in 40 ns units (cost_time) -- the length
+            // of its dependent chain, which a packet walk's union of nodes stretches beyond
+            // what its lanes' own steps count -- or those lanes' node steps + tests. Ranking by
+            // time: car waited frame 0.2504 -> 0.2247 ms with the latency mode's split below,
+            // in flight -1 % (r04v, profiles/r04v_*)
+            const unsigned long long work = kp.cost_time ? (wall_clock64() - t0) >> 2
+                                                         : wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
             unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
             bool rec = part == 0;
             if (part > 0 && lane == 0) {
@@ -2241,6 +2249,7 @@ struct rt_ctx {
     int split_max = kSplitMax, split_g = kSplitGroup;  // split per-lane walks (rt_debug_split)
     int heavy_k = kHeavyTiles, heavy_parts = kHeavyParts;  // heaviest tiles as several waves (rt_debug_heavy)
     int lane_k = -1, lane_k_mode = 2;  // heaviest slots' walk modes (rt_debug_lane_k; -1: auto)
+    int cost_time = -1;                // tile cost: 0 lane work, else wave wall time (rt_debug_cost_time)
     int latency_mode = 0;              // rt_set_latency_mode
     int* tile_order = nullptr;  // diagnostics (rt_debug_tile_order): fixed dispatch order of the 8x8 tiles
     int tile_order_n = 0;
@@ -2920,6 +2929,7 @@ int fill_kparams(rt_ctx* c, int width, int height, int y0, int stripe, int perio
     kp.heavy_parts = 1;
     kp.lane_k = 0;
     kp.lane_k_mode = 0;
+    kp.cost_time = 0;
     return RT_OK;
 }
 
@@ -2957,6 +2967,7 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->heavy_parts = c->heavy_parts;
     b->lane_k = c->lane_k;
     b->lane_k_mode = c->lane_k_mode;
+    b->cost_time = c->cost_time;
     b->latency_mode = c->latency_mode;
     b->schedule = c->schedule;
     b->sched_period = c->sched_period;
@@ -3211,18 +3222,24 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 hk = small ? std::max(16, k2.tiles / 256) : 0;
                 hp = small ? 8 : 1;
                 if (!small && c->latency_mode) {
-                    // rt_set_latency_mode: the heaviest 1/512 as 4 waves (car waited frame 0.2563 ms
-                    // with 2 waves, 0.2507 with 4; 1/256 as 2: 0.2518, 1/128 as 2: 0.2537, 1/1024 as
-                    // 4: 0.2559, 1/512 as 8: 0.2592; profiles/r04e_latency_sweep.json)
+                    // rt_set_latency_mode: the heaviest 1/512 as 2 waves. Car waited frame with the
+                    // wall-time cost order: 0.2247 ms (1/256 or 1/1024 as 2: 0.2248 / 0.2249; as 4:
+                    // 0.2389 and bimodal; none: 0.2544; profiles/r04v_latency_sweep.json). With the
+                    // lanes' work as the cost, 1/512 as 4 was best (0.2507, r04e)
                     hk = std::max(16, k2.tiles / 512);
-                    hp = 4;
+                    hp = 2;
                 }
             }
-            if (!c->persistent && !c->tile_times && hp > 1 && hk > 0) {
+            const bool stamps_fit =  // timed frames split only with a record per part
+                !c->tile_times ||
+                c->tile_times_cap >= static_cast<size_t>(k2.tiles) + static_cast<size_t>(std::min(hk, k2.tiles)) * hp;
+            if (!c->persistent && stamps_fit && hp > 1 && hk > 0) {
                 k2.heavy_k = std::min(hk, k2.tiles);
                 k2.heavy_parts = hp;
             }
         }
+        // the cost measure: explicit (rt_debug_cost_time) or the waves' wall time
+        k2.cost_time = c->cost_time != 0 ? 1 : 0;
         k2.heavy_acc = nullptr;
         if (k2.tile_cost && k2.heavy_k > 0) {  // the split tiles' part sums and counts (kernel comment)
             const size_t need = 2 * static_cast<size_t>(k2.heavy_k);
@@ -4030,6 +4047,15 @@ extern "C" int rt_debug_heavy(rt_ctx* c, int k, int parts) {
 // Diagnostics: the first k dispatch slots of the cost order (the heaviest tiles) walk
 // their camera rays (mode bit 0) and / or the camera rays' shadow rays (bit 1) per lane;
 // k = -1: the default policy.
+// Diagnostics: a cost-recording dispatch ranks the tiles by their waves' wall time
+// (1) or by their lanes' node steps + tests (0); -1: the default policy.
+extern "C" int rt_debug_cost_time(rt_ctx* c, int mode) {
+    if (!c || mode < -1 || mode > 1) return RT_ERR_INVALID;
+    c->cost_time = mode;
+    c->sched_valid = 0;
+    return RT_OK;
+}
+
 extern "C" int rt_debug_lane_k(rt_ctx* c, int k, int mode) {
     if (!c || k < -1 || mode < 0 || mode > 3) return RT_ERR_INVALID;
     c->lane_k = k;

@@ -702,6 +702,12 @@ class ComputeShader:
         fn.argtypes = [_P, _I, _I]
         self._chk(fn(self._h, int(k), int(parts)), "rt_debug_heavy")
 
+    def debug_cost_time(self, mode):
+        """Cost-order measure: 1 the tiles' wave wall time, 0 their lanes' steps + tests, -1 default."""
+        fn = self._lib.rt_debug_cost_time
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(mode)), "rt_debug_cost_time")
+
     def debug_lane_k(self, k, mode):
         """The first k dispatch slots walk camera rays (bit 0) / their shadows (bit 1) per lane."""
         fn = self._lib.rt_debug_lane_k

@@ -518,6 +518,37 @@ def test_heaviest_slots_walk_per_lane_exact(ctx, cfg, W, H, mb):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cfg,W,H,mb", [(3, 320, 180, 3), (5, 320, 180, 3)])
+def test_cost_measures_exact(ctx, cfg, W, H, mb):
+    """rt_debug_cost_time: the cost order ranks tiles by their waves' wall time (the
+    default) or by their lanes' node steps + tests. Either order, with and without
+    latency mode (its split heavy tiles record the sum of their parts), frame after
+    frame writes every pixel with the row-major frame's value."""
+    fs = rtamd.generate(cfg, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True)
+    try:
+        ctx.set_schedule(rtamd.SCHED_ROWS)
+        ref = ctx.render(W, H)
+        ctx.set_schedule(rtamd.SCHED_COST)
+        full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        for cm in (0, 1, -1):
+            for lat in (0, 1):
+                ctx.debug_cost_time(cm)
+                ctx.set_latency_mode(lat)
+                for _ in range(12):
+                    full.fill_(float("nan"))
+                    torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
+                    ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
+                    ctx.sync()
+                    img = full.cpu().numpy()
+                    assert np.array_equal(img, ref), f"cost {cm} latency {lat}: {int((img != ref).any(axis=-1).sum())} px"
+    finally:
+        ctx.debug_cost_time(-1)
+        ctx.set_latency_mode(0)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 320, 180, 3), (5, 320, 180, 3)])
 def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
     """rt_debug_heavy: the heaviest tiles of the cost order run as 2/4/8 waves, one

@@ -27,15 +27,18 @@ import rtamd  # noqa: E402
 
 SETTINGS = {
     "default": {},
-    # round 4 sweep 1 (latency mode's heavy tiles then 1/512 x 2 waves): profiles/r04e_latency_sweep.json
-    "heavy63x2": {"heavy": (63, 2)},
-    "lanek0": {"lane_k": (0, 0)},
-    "lanek0_h127x4": {"lane_k": (0, 0), "heavy": (127, 4)},
-    "lanek0_h31x4": {"lane_k": (0, 0), "heavy": (31, 4)},
-    "lanek0_s16x16": {"lane_k": (0, 0), "split": (16, 16)},
-    "lanek64m2": {"lane_k": (64, 2)},
-    "lanek1024m2": {"lane_k": (1024, 2)},
-    "lanek253m3": {"lane_k": (253, 3)},
+    # round 4 sweep 1 (latency mode's heavy tiles then 1/512 x 2 waves): profiles/r04e_latency_sweep.json;
+    # sweep 3 (raised wave priority for the first k slots, s_setprio): no effect, dropped
+    # (profiles/r04r_latency_sweep_prio_negative.json). Sweep 4: the cost order by the
+    # tiles' wave wall time (rt_debug_cost_time) instead of their lanes' steps + tests
+    "costtime": {"cost_time": 1},
+    "costtime_h63x2": {"cost_time": 1, "heavy": (63, 2)},
+    "costtime_h127x2": {"cost_time": 1, "heavy": (127, 2)},
+    "costtime_h31x2": {"cost_time": 1, "heavy": (31, 2)},
+    "costtime_h63x2_lanek0": {"cost_time": 1, "heavy": (63, 2), "lane_k": (0, 0)},
+    "costtime_h63x2_lanek506": {"cost_time": 1, "heavy": (63, 2), "lane_k": (506, 2)},
+    "costtime_h63x2_s16x16": {"cost_time": 1, "heavy": (63, 2), "split": (16, 16)},
+    "costtime_noheavy": {"cost_time": 1, "heavy": (0, 1)},
 }
 
 
@@ -61,6 +64,7 @@ def main():
         c.debug_split(*s.get("split", (16, 8)))
         c.debug_heavy(*s.get("heavy", (-1, 2)))
         c.debug_lane_k(*s.get("lane_k", (-1, 2)))
+        c.debug_cost_time(s.get("cost_time", -1))
 
     def frame():
         c.set_camera(fs.camera)

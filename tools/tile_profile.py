@@ -26,12 +26,15 @@ WL = {2: (2, 800, 600, 1), 3: (3, 1920, 1080, 3), 4: (3, 3840, 2160, 3), 5: (5, 
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--out", default=None)
+ap.add_argument("--latency", action="store_true", help="rt_set_latency_mode on (the waited-frame dispatch)")
 a = ap.parse_args()
 cfg, W, H, mb = WL[a.config]
 fs = rtamd.generate(cfg, 0, W, H)
 ctx = rtamd.ComputeShader(0)
 ctx.upload(fs)
 ctx.set_params(W, H, mb, True)
+if a.latency:
+    ctx.set_latency_mode(True)
 out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
 torch.cuda.synchronize()
 tiles_x, tiles_y = (W + 7) // 8, (H + 7) // 8
@@ -40,21 +43,41 @@ for _ in range(10):
     ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
 ctx.sync()
 kt = ctx.kernel_times()
-ctx.debug_tile_times(n)
+# records: one per tile, then (latency mode's split heavy tiles) one per part slot
+cap = n + (4096 if a.latency else 0)
+ctx.debug_tile_times(cap)
 ctx.dispatch_rows(W, H, 0, 1, 1, H, out.data_ptr(), W * 16)
-rec = ctx.tile_times(n).astype(np.int64)
+rec_all = ctx.tile_times(cap).astype(np.int64)
 ctx.debug_tile_times(0)
-t0 = rec[:, 0].min()
+parts = rec_all[n:][rec_all[n:, 1] > 0]  # part slots that ran (end stamp set)
+rec = rec_all[:n].copy()
+if len(parts):
+    # a split tile's own record is unused (zero): duration 0 here, its parts reported below
+    rec[rec[:, 1] == 0, 0:2] = rec_all[:n][rec_all[:n, 1] > 0, 0].min()
+rec_ev = np.concatenate([rec_all[:n][rec_all[:n, 1] > 0], parts])
+t0 = rec_ev[:, 0].min()
 start = (rec[:, 0] - t0) / 100.0  # us (100 MHz)
 dur = (rec[:, 1] - rec[:, 0]) / 100.0
-frame_us = (rec[:, 1].max() - t0) / 100.0
+frame_us = (rec_ev[:, 1].max() - t0) / 100.0
 order = np.argsort(-dur)
-res = {"config": a.config, "frame_us_timed": frame_us, "kernel_ms_untimed_median": float(np.median(kt)),
+res = {"config": a.config, "latency_mode": a.latency, "frame_us_timed": frame_us, "kernel_ms_untimed_median": float(np.median(kt)),
        "tiles": n, "dur_us_pcts": {p: float(np.percentile(dur, p)) for p in (50, 90, 99, 99.9, 100)}}
 # concurrency over time: busy waves per 5 us bucket
 edges = np.arange(0, frame_us + 5, 5.0)
-busy = [int(((start <= e) & (start + dur > e)).sum()) for e in edges]
+ev_s, ev_e = (rec_ev[:, 0] - t0) / 100.0, (rec_ev[:, 1] - t0) / 100.0
+busy = [int(((ev_s <= e) & (ev_e > e)).sum()) for e in edges]
 res["busy_waves_every_5us"] = busy
+if len(parts):
+    ps, pd = (parts[:, 0] - t0) / 100.0, (parts[:, 1] - parts[:, 0]) / 100.0
+    po = np.argsort(-pd)
+    res["split_parts"] = {"n": int(len(parts)), "dur_us_pcts": {p: float(np.percentile(pd, p)) for p in (50, 90, 100)},
+                          "slowest": [{"start_us": float(ps[i]), "dur_us": float(pd[i]), "walk_ticks":
+                                       [int(x) for x in parts[i, 6:12]]} for i in po[:12]]}
+    # whole tiles (not split) that end last
+    we = (rec_all[:n, 1] - t0) / 100.0
+    last = np.argsort(-we)[:12]
+    res["last_whole_tiles"] = [{"tile": int(t), "start_us": float(start[t]), "end_us": float(we[t]),
+                                "walk_ticks": [int(x) for x in rec_all[t, 6:12]]} for t in last]
 slow = order[:64]
 res["slowest"] = []
 for t in slow[:16]:
