@@ -649,6 +649,9 @@ def main():
     # completion interrupt. Over rt_group every rank starts each frame after a barrier,
     # so rank 0's frame includes the slowest peer's stripes crossing its link.
     serial_frames = []
+    # at least three cost-order periods (rt_set_schedule: every 8th frame) before the waited
+    # frames are timed, so latency mode's order (its split tiles recorded) has settled
+    wait_warmup = max(a.warmup, 24)
     if not (strong and not use_group):  # the torch-gather rehearsal has no waited-frame figure
         for c_ in ctxs:
             c_.set_latency_mode(1)
@@ -659,7 +662,7 @@ def main():
             else:
                 ctx.sync()
 
-        for i in range(a.warmup):
+        for i in range(wait_warmup):
             frame(i, 1)
             wait_frame()
         for i in range(a.steps):
@@ -685,7 +688,7 @@ def main():
         for c_ in ctxs:
             c_.set_latency_mode(1)
         frames_anim = anim[1] if anim is not None else None
-        for n_ in (a.warmup, a.steps):
+        for n_ in (wait_warmup, a.steps):
             ms_ = rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, n_, True, anim=frames_anim)
             if anim is not None:  # the C++ loop animates ctx 0 with frames 0, 1, ... (oracle bookkeeping)
                 applied[0].extend(i % len(frames_anim) for i in range(n_))
