@@ -649,9 +649,9 @@ def main():
     # completion interrupt. Over rt_group every rank starts each frame after a barrier,
     # so rank 0's frame includes the slowest peer's stripes crossing its link.
     serial_frames = []
-    # at least three cost-order periods (rt_set_schedule: every 8th frame) before the waited
+    # at least three cost-order periods (rt_set_schedule: every 16th frame) before the waited
     # frames are timed, so latency mode's order (its split tiles recorded) has settled
-    wait_warmup = max(a.warmup, 24)
+    wait_warmup = max(a.warmup, 48)
     if not (strong and not use_group):  # the torch-gather rehearsal has no waited-frame figure
         for c_ in ctxs:
             c_.set_latency_mode(1)

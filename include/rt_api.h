@@ -228,7 +228,7 @@ int rt_set_walk(struct rt_ctx* ctx, int lane_from_depth);
 
 /* Tile dispatch order of the accelerated kernel. RT_SCHED_ROWS: row-major.
  * RT_SCHED_COST (default): a dispatch records each 8x8 tile's duration (its
- * wave's wall time, in 40 ns units; every 8th frame once the order exists),
+ * wave's wall time, in 40 ns units; every 16th frame once the order exists),
  * and the next dispatch with the same tile count starts the tiles in
  * decreasing order of those durations (longest first), so the frame is not
  * left waiting on expensive tiles that started late. The order only changes

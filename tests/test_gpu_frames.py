@@ -466,7 +466,7 @@ def car_full_ref():
 def test_bench_steady_state_frames_vs_oracle(car_full_ref):
     """What bench.py times: F contexts on their own streams (F = the bench's own
     plan, 3 at 1080p), frames dealt round-robin with nothing waited on between
-    them, the cost-ordered schedule (re-derived every 8th dispatch; the dispatches
+    them, the cost-ordered schedule (re-derived every 16th dispatch; the dispatches
     between run the counter-free instance with the auto lane_k slots), 1920x1080,
     depth 3, on 2F hardware queues (tests/conftest.py raises GPU_MAX_HW_QUEUES
     before the runtime starts, as bench.py does). Each of the 24 frames goes to its

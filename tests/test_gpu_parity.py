@@ -435,9 +435,9 @@ def test_cost_schedule_identical_images(ctx, sched):
     ref = ctx.render(320, 180)
     ctx.set_schedule(sched)
     full = torch.empty((180, 320, 4), dtype=torch.float32, device="cuda")
-    # dispatch 1 records tile work, 2-8 reuse its order with the counter-free kernel,
-    # 9 records again (the order is re-derived every 8th dispatch)
-    for i in range(10):
+    # dispatch 1 records tile work, 2-16 reuse its order with the counter-free kernel,
+    # 17 records again (the order is re-derived every 16th dispatch)
+    for i in range(18):
         full.fill_(float("nan"))
         torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
         ctx.dispatch_rows(320, 180, 0, 1, 1, 180, full.data_ptr(), 320 * 16)
