@@ -1688,10 +1688,12 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 #ifndef RT_ACCEL_ATTR
 #define RT_ACCEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
-// COST = false: a dispatch that records no tile work (rt_set_schedule reuses the
-// last order), without the walk counters' registers (12 -> 3 spilled VGPRs).
+// COST = false: no walk counters (their registers: 12 -> 3 spilled VGPRs). REC: the
+// dispatch records each tile's cost for the next order (rt_set_schedule); without COST
+// it can only record the wall-time cost (kp.cost_time), which needs no counters.
 // TAIL: queue the rays alive after bounce tail_from - 1 for k_accel_tail (rt_set_tail).
-template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false>
+template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false,
+          bool REC = COST>
 __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
     // per-lane stacks, entry j of lane i at [j * blockDim.x + i]: codes, then bf16 entry parameters
@@ -1710,9 +1712,9 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
     const int hs = kp.heavy_k * kp.heavy_parts;
     while (tile < kp.tiles + hs - kp.heavy_k) {
         unsigned long long t0 = 0;
-        if (TIMED || (COST && kp.cost_time)) t0 = wall_clock64();
+        if (TIMED || (REC && kp.cost_time)) t0 = wall_clock64();
         int part = 0;
-        const int slot = tile;
+        const int slot = REC ? __builtin_amdgcn_readfirstlane(tile) : tile;
         if (kp.tile_order) {  // dispatch order -> image tile (a permutation)
             if (tile < hs) {
                 part = tile % kp.heavy_parts + 1;
@@ -1720,6 +1722,10 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
             } else {
                 tile = kp.tile_order[tile - hs + kp.heavy_k];
             }
+        }
+        if (REC) {  // wave-uniform: kept in SGPRs through the walks for the cost record
+            tile = __builtin_amdgcn_readfirstlane(tile);
+            part = __builtin_amdgcn_readfirstlane(part);
         }
         WalkCount wc{0u, 0u, 0u, 0u};
         // a split tile's parts stamp records tiles + slot (rt_debug_tile_times with room for them)
@@ -1749,14 +1755,15 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 o[5] = mt;
             }
         }
-        if (COST && kp.tile_cost) {
+        if (REC && kp.tile_cost) {
             // the tile's cost: its wave's wall time in 40 ns units (cost_time) -- the length
             // of its dependent chain, which a packet walk's union of nodes stretches beyond
             // what its lanes' own steps count -- or those lanes' node steps + tests. Ranking by
             // time: car waited frame 0.2504 -> 0.2247 ms with the latency mode's split below,
             // in flight -1 % (r04v, profiles/r04v_*)
-            const unsigned long long work = kp.cost_time ? (wall_clock64() - t0) >> 2
-                                                         : wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
+            const unsigned long long work = !COST || kp.cost_time
+                                                ? (wall_clock64() - t0) >> 2
+                                                : wave_sum(static_cast<unsigned long long>(wc.nodes) + wc.tests);
             unsigned wk = static_cast<unsigned>(work < 0xffffffffull ? work : 0xffffffffull);
             bool rec = part == 0;
             if (part > 0 && lane == 0) {
@@ -3301,10 +3308,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         if (c->accel.mt) {
             // Moller-Trumbore accelerator: its own instances; no compaction
             k2.tail_queue = nullptr;
-            kfn = spec ? (k2.tile_cost ? k_accel<false, false, true, true, false, true>
-                                       : k_accel<false, false, true, false, false, true>)
-                       : (k2.tile_cost ? k_accel<false, false, false, true, false, true>
-                                       : k_accel<false, false, false, false, false, true>);
+            // a dispatch recording wall-time costs: the counter-free instance that records
+            kfn = spec ? (!k2.tile_cost   ? k_accel<false, false, true, false, false, true>
+                          : k2.cost_time ? k_accel<false, false, true, false, false, true, true>
+                                         : k_accel<false, false, true, true, false, true>)
+                       : (!k2.tile_cost   ? k_accel<false, false, false, false, false, true>
+                          : k2.cost_time ? k_accel<false, false, false, false, false, true, true>
+                                         : k_accel<false, false, false, true, false, true>);
             blocks = (k2.tiles + wpb - 1) / wpb;
         } else if (kfn == k_accel<false, false, true>) {
             // production shape: the counter-free kernel on a dispatch that records no tile
@@ -3313,9 +3323,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 // the compacting instance; in latency mode without a queue (tail_from 0), for
                 // its split walks in sparse waves (lane_walk_any), which the production
                 // instance leaves out for its registers
-                kfn = k2.tile_cost ? k_accel<false, false, true, true, true> : k_accel<false, false, true, false, true>;
+                kfn = !k2.tile_cost  ? k_accel<false, false, true, false, true>
+                      : k2.cost_time ? k_accel<false, false, true, false, true, false, true>
+                                     : k_accel<false, false, true, true, true>;
             } else if (!k2.tile_cost) {
                 kfn = k_accel<false, false, true, false>;
+            } else if (k2.cost_time) {
+                kfn = k_accel<false, false, true, false, false, false, true>;  // records, no counters
             }
         } else if (tail) {
             k2.tail_queue = nullptr;
@@ -4033,6 +4047,18 @@ extern "C" int rt_debug_tile_order(rt_ctx* c, const int* order, int n) {
     HIP_TRY(hipMemcpy(c->tile_order, order, n * sizeof(int), hipMemcpyHostToDevice));
     c->tile_order_n = n;
     return RT_OK;
+}
+
+// Diagnostics: the current cost order (tile indices, longest first) into out[0, n);
+// returns the tiles copied (0 when no order exists yet).
+extern "C" int rt_debug_sched_order(rt_ctx* c, int* out, int n) {
+    if (!c || n < 0 || (n > 0 && !out)) return RT_ERR_INVALID;
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int k = std::min(n, c->sched_valid);
+    if (k > 0 && c->sched_order)
+        HIP_TRY(hipMemcpy(out, c->sched_order, static_cast<size_t>(k) * sizeof(int), hipMemcpyDeviceToHost));
+    return c->sched_order ? k : 0;
 }
 
 // Diagnostics: the first k tiles of the cost order (the heaviest) each run as `parts`

@@ -702,6 +702,16 @@ class ComputeShader:
         fn.argtypes = [_P, _I, _I]
         self._chk(fn(self._h, int(k), int(parts)), "rt_debug_heavy")
 
+    def debug_sched_order(self, n):
+        """The current cost order's first n tiles (longest first); empty before one exists."""
+        fn = self._lib.rt_debug_sched_order
+        fn.argtypes = [_P, _P, _I]
+        buf = np.zeros(max(n, 1), np.int32)
+        k = fn(self._h, _ptr(buf), int(n))
+        if k < 0:
+            raise RTError("rt_debug_sched_order", k)
+        return buf[:k].copy()
+
     def debug_cost_time(self, mode):
         """Cost-order measure: 1 the tiles' wave wall time, 0 their lanes' steps + tests, -1 default."""
         fn = self._lib.rt_debug_cost_time
