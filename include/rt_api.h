@@ -243,8 +243,8 @@ int rt_set_schedule(struct rt_ctx* ctx, int mode);
  * reference's own loop, src/main.cpp:290-462) rather than keeping frames in
  * flight. 1: the accelerated kernel's instance with split walks in sparse
  * waves (idle lanes help a tile's few live rays) and, on frames not already
- * split, the heaviest 1/512 of the tiles as two waves each. Shortens one frame
- * (car: -15 %) and costs throughput when frames overlap. 0 (default): off.
+ * split, the heaviest 1/200 of the tiles as four waves each. Shortens one frame
+ * (car: -19 %) and costs throughput when frames overlap. 0 (default): off.
  * Same image either way. */
 int rt_set_latency_mode(struct rt_ctx* ctx, int on);
 

@@ -3230,18 +3230,28 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 hk = small ? std::max(16, k2.tiles / 256) : 0;
                 hp = small ? 8 : 1;
                 if (!small && c->latency_mode) {
-                    // rt_set_latency_mode: the heaviest 1/512 as 2 waves. Car waited frame with the
-                    // wall-time cost order: 0.2247 ms (1/256 or 1/1024 as 2: 0.2248 / 0.2249; as 4:
-                    // 0.2389 and bimodal; none: 0.2544; profiles/r04v_latency_sweep.json). With the
-                    // lanes' work as the cost, 1/512 as 4 was best (0.2507, r04e)
-                    hk = std::max(16, k2.tiles / 512);
-                    hp = 2;
+                    // rt_set_latency_mode: the heaviest 1/200 as 4 waves. Car waited frame with the
+                    // wall-time cost order and whole-tile cost frames (Python loop,
+                    // profiles/r04z7_latency_sweep.json, r04z8_latency_sweep.json), heaviest k as
+                    // 4 waves: k = 95 0.2362 ms, 126 0.2161, 159 0.2184, 191 0.2203, 255 0.2260;
+                    // as 2 waves: 63 0.2371, 127-511 0.224, 1023 0.229; 126 as 8: 0.2275. Some
+                    // tiles ranked ~96-126 by whole time gain most from the split, so k sits
+                    // well above that edge (162 of the car's 32,400 tiles)
+                    hk = std::max(16, k2.tiles / 200);
+                    hp = 4;
                 }
             }
             const bool stamps_fit =  // timed frames split only with a record per part
                 !c->tile_times ||
                 c->tile_times_cap >= static_cast<size_t>(k2.tiles) + static_cast<size_t>(std::min(hk, k2.tiles)) * hp;
-            if (!c->persistent && stamps_fit && hp > 1 && hk > 0) {
+            // A dispatch that records wall-time costs runs every tile whole: a split tile's
+            // parts run side by side, so no sum or maximum of theirs stands for the whole
+            // tile's time, and a split set ranked by such an estimate locks in whatever
+            // tiles were split first (the latency-mode car waited frame settled at 0.222 or
+            // 0.237 ms by the split set it started from, r04z5). Recording whole tiles every
+            // 16th frame keeps the split set the 1/512 longest whole tiles.
+            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times;
+            if (!c->persistent && stamps_fit && hp > 1 && hk > 0 && !whole) {
                 k2.heavy_k = std::min(hk, k2.tiles);
                 k2.heavy_parts = hp;
             }

@@ -31,14 +31,16 @@ SETTINGS = {
     # sweep 3 (raised wave priority for the first k slots, s_setprio): no effect, dropped
     # (profiles/r04r_latency_sweep_prio_negative.json). Sweep 4: the cost order by the
     # tiles' wave wall time (rt_debug_cost_time) instead of their lanes' steps + tests
-    "costtime": {"cost_time": 1},
-    "costtime_h63x2": {"cost_time": 1, "heavy": (63, 2)},
-    "costtime_h127x2": {"cost_time": 1, "heavy": (127, 2)},
-    "costtime_h31x2": {"cost_time": 1, "heavy": (31, 2)},
-    "costtime_h63x2_lanek0": {"cost_time": 1, "heavy": (63, 2), "lane_k": (0, 0)},
-    "costtime_h63x2_lanek506": {"cost_time": 1, "heavy": (63, 2), "lane_k": (506, 2)},
-    "costtime_h63x2_s16x16": {"cost_time": 1, "heavy": (63, 2), "split": (16, 16)},
-    "costtime_noheavy": {"cost_time": 1, "heavy": (0, 1)},
+    # sweep 5 (r04z7): cost frames record whole tiles, so the order no longer depends on
+    # the split set it started from; split-set sizes again (profiles/r04z7_latency_sweep.json).
+    # Sweep 6 (r04z8): around the new default, 1/256 x 4
+    "h63x2": {"heavy": (63, 2)},
+    "h95x4": {"heavy": (95, 4)},
+    "h159x4": {"heavy": (159, 4)},
+    "h191x4": {"heavy": (191, 4)},
+    "h127x8": {"heavy": (127, 8)},
+    "h63x8": {"heavy": (63, 8)},
+    "h255x2": {"heavy": (255, 2)},
 }
 
 
