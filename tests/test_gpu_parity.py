@@ -518,6 +518,36 @@ def test_heaviest_slots_walk_per_lane_exact(ctx, cfg, W, H, mb):
 
 
 @pytest.mark.gpu
+def test_cost_order_ranks_by_wall_time(ctx):
+    """The cost order (rt_debug_sched_order) is a permutation of the frame's tiles, and
+    with the wall-time measure its head is the tiles that took longest: a tile whose
+    camera rays all miss the root box (sky) costs next to nothing, so the first 16 are
+    all tiles through the scene."""
+    W, H = 320, 180
+    fs = rtamd.generate(3, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3, True)
+    ctx.set_schedule(rtamd.SCHED_COST)
+    ctx.debug_cost_time(1)
+    try:
+        img = None
+        for _ in range(20):
+            img = ctx.render(W, H)
+        tx, ty = (W + 7) // 8, (H + 7) // 8
+        order = ctx.debug_sched_order(tx * ty)
+        assert sorted(order.tolist()) == list(range(tx * ty))
+        # a background-only tile is constant along each of its rows (the gradient runs in y)
+        sky_like = []
+        for t in order[:16].tolist():
+            y0, x0 = (t // tx) * 8, (t % tx) * 8
+            blk = img[y0:y0 + 8, x0:x0 + 8, :3]
+            sky_like.append(bool(np.all(blk == blk[:, :1, :])))  # constant along each row
+        assert not any(sky_like), f"head tiles {order[:16].tolist()} include background-only tiles"
+    finally:
+        ctx.debug_cost_time(-1)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfg,W,H,mb", [(3, 320, 180, 3), (5, 320, 180, 3)])
 def test_cost_measures_exact(ctx, cfg, W, H, mb):
     """rt_debug_cost_time: the cost order ranks tiles by their waves' wall time (the

@@ -77,7 +77,8 @@ for _ in range(F):
              "spec": lambda x: c.debug_spec(x), "stack": lambda x: c.debug_lane_stack(x),
              "walk": lambda x: c.set_walk(x), "tree": lambda x: c.set_tree(x),
              "latency": lambda x: c.set_latency_mode(x), "cone": lambda x: c.debug_cone_cull(x),
-             "heavy": lambda x: c.debug_heavy(x // 100, x % 100), "costtime": lambda x: c.debug_cost_time(x)}[k](int(v))
+             "heavy": lambda x: c.debug_heavy(x // 100, x % 100), "costtime": lambda x: c.debug_cost_time(x),
+             "lanek": lambda x: c.debug_lane_k(x // 10, x % 10)}[k](int(v))
     ctxs.append((c, s))
     bufs.append(torch.empty((H, W, 4), dtype=torch.float32, device="cuda"))
 

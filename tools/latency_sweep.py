@@ -33,14 +33,13 @@ SETTINGS = {
     # tiles' wave wall time (rt_debug_cost_time) instead of their lanes' steps + tests
     # sweep 5 (r04z7): cost frames record whole tiles, so the order no longer depends on
     # the split set it started from; split-set sizes again (profiles/r04z7_latency_sweep.json).
-    # Sweep 6 (r04z8): around the new default, 1/256 x 4
-    "h63x2": {"heavy": (63, 2)},
-    "h95x4": {"heavy": (95, 4)},
-    "h159x4": {"heavy": (159, 4)},
-    "h191x4": {"heavy": (191, 4)},
-    "h127x8": {"heavy": (127, 8)},
-    "h63x8": {"heavy": (63, 8)},
-    "h255x2": {"heavy": (255, 2)},
+    # Sweep 6 (r04z8): around the new default, 1/256 x 4 (profiles/r04z8_latency_sweep.json).
+    # Sweep 7 (r04z12): the heaviest slots' camera rays per lane under the wall-time order
+    "lanek128m3": {"lane_k": (128, 3)},
+    "lanek648m3": {"lane_k": (648, 3)},
+    "lanek648m1": {"lane_k": (648, 1)},
+    "lanek2048m3": {"lane_k": (2048, 3)},
+    "lanek0": {"lane_k": (0, 0)},
 }
 
 
