@@ -1615,7 +1615,7 @@ __device__ __forceinline__ void bounce_step(const AccelPtrs& A, const float4* __
 
 // Walk counts (node steps, tests) are kept when COST: they are the cost that
 // orders a later dispatch (rt_set_schedule). COUNT adds the per-walk records.
-template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false>
+template <bool COUNT, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false, bool QUEUE = TAIL>
 __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, const KParams& kp, int tile,
                            int part, int* stk, unsigned short* stt, int cap, WalkCount& wc,
                            unsigned long long* rec, bool heavy) {
@@ -1652,7 +1652,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         bounce_step<COUNT, SPEC, COST, MT, TAIL || RT_SPLIT_ALL>(A, mat, kp, depth, ray, alive, acc, att,
                                        [&]() { return tile_pixel(kp, tile).y; }, stk, stt, cap, wc, rec, lane_from,
                                        shadow_from);
-        if (TAIL && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
+        if (TAIL && QUEUE && depth + 1 == kp.tail_from && __popcll(__ballot(alive)) <= kp.tail_max_lanes) {
             // Compaction: the rays still alive go to the tail queue (one atomic per wave)
             // per 64x64-pixel region (8x8 tiles), so a tail wave's rays come from one area
             const unsigned long long m = __ballot(alive);
@@ -1693,7 +1693,7 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 // it can only record the wall-time cost (kp.cost_time), which needs no counters.
 // TAIL: queue the rays alive after bounce tail_from - 1 for k_accel_tail (rt_set_tail).
 template <bool PERSISTENT, bool TIMED, bool SPEC, bool COST = true, bool TAIL = false, bool MT = false,
-          bool REC = COST>
+          bool REC = COST, bool QUEUE = TAIL>
 __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, const float4* __restrict__ mat, KParams kp) {
     extern __shared__ int lds_stack[];
     // per-lane stacks, entry j of lane i at [j * blockDim.x + i]: codes, then bf16 entry parameters
@@ -1731,7 +1731,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         // a split tile's parts stamp records tiles + slot (rt_debug_tile_times with room for them)
         unsigned long long* rec =
             TIMED ? kp.tile_times + kTileRec * static_cast<size_t>(part > 0 ? kp.tiles + slot : tile) : nullptr;
-        accel_tile<TIMED, SPEC, COST, TAIL, MT>(A, mat, kp, tile, part, stk, stt, kp.lane_stack, wc, rec,
+        accel_tile<TIMED, SPEC, COST, TAIL, MT, QUEUE>(A, mat, kp, tile, part, stk, stt, kp.lane_stack, wc, rec,
                                                 slot < kp.lane_k);
         if (TIMED) {
             const unsigned long long t1 = wall_clock64();
@@ -3333,9 +3333,15 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 // the compacting instance; in latency mode without a queue (tail_from 0), for
                 // its split walks in sparse waves (lane_walk_any), which the production
                 // instance leaves out for its registers
-                kfn = !k2.tile_cost  ? k_accel<false, false, true, false, true>
-                      : k2.cost_time ? k_accel<false, false, true, false, true, false, true>
-                                     : k_accel<false, false, true, true, true>;
+                // (latency mode without compaction: the instance without the queue's code)
+                if (tail)
+                    kfn = !k2.tile_cost  ? k_accel<false, false, true, false, true>
+                          : k2.cost_time ? k_accel<false, false, true, false, true, false, true>
+                                         : k_accel<false, false, true, true, true>;
+                else
+                    kfn = !k2.tile_cost  ? k_accel<false, false, true, false, true, false, false, false>
+                          : k2.cost_time ? k_accel<false, false, true, false, true, false, true, false>
+                                         : k_accel<false, false, true, true, true, false, true, false>;
             } else if (!k2.tile_cost) {
                 kfn = k_accel<false, false, true, false>;
             } else if (k2.cost_time) {
