@@ -8,6 +8,7 @@
 #include <cstring>
 #include <functional>
 #include <numeric>
+#include <thread>
 
 namespace rta {
 namespace {
@@ -656,12 +657,62 @@ int log2_ceil(int n) {
 // for the few-leaf item codes).
 constexpr int kItemMax = RT_ITEM_MAX;
 
+// Host threads for the builds' independent halves (at most 16: the GPU box's CPU
+// share per GPU). 1 on a one-core host.
+int build_threads() {
+    const unsigned h = std::thread::hardware_concurrency();
+    return static_cast<int>(std::max(1u, std::min(16u, h)));
+}
+
+// fn(i0, i1) over [0, n) in contiguous chunks on up to build_threads() threads (the
+// calling one included); chunk c is [c n / T, (c + 1) n / T).
+template <class F>
+void parallel_chunks(int n, int min_per_thread, F fn) {
+    const int T = std::max(1, std::min(build_threads(), n / std::max(1, min_per_thread)));
+    if (T <= 1) {
+        fn(0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int c = 1; c < T; ++c)
+        th.emplace_back([&, c] {
+            fn(static_cast<int>(static_cast<long long>(c) * n / T),
+               static_cast<int>(static_cast<long long>(c + 1) * n / T), c);
+        });
+    fn(0, static_cast<int>(static_cast<long long>(n) / T), 0);
+    for (auto& t : th) t.join();
+}
+
 struct SceneBuilder {
     AccelHost& T;
-    std::vector<Atom> atoms;
-    std::vector<std::pair<int, int>> ap;  // (shape, seq)
-    std::vector<int> leaf_ref;            // per node: reference leaf of a leaf, -1 inner
+    std::vector<Atom>& atoms;                     // partitioned in place: sub-builders own disjoint ranges
+    const std::vector<std::pair<int, int>>& ap;  // (shape, seq)
+    std::vector<int> leaf_ref;                    // per node: reference leaf of a leaf, -1 inner
     int hmax = 0, height = 0;
+    int par = 0;  // levels below this one whose two halves may still be built on two threads
+
+    // Appends a sub-builder's tree (its nodes and prims numbered from 0, root first)
+    // after this one's, as the sequential build would have numbered it; returns the
+    // index of its root.
+    int splice(const SceneBuilder& o) {
+        const int off = static_cast<int>(T.lbox.size()), poff = static_cast<int>(T.prim_shape.size());
+        T.lbox.insert(T.lbox.end(), o.T.lbox.begin(), o.T.lbox.end());
+        for (size_t j = 0; j < o.T.la.size(); ++j) {
+            const int a = o.T.la[j], b = o.T.lb[j];
+            if (a >= 0) {  // inner: left, right | axis << 30
+                T.la.push_back(a + off);
+                T.lb.push_back(((b & 0x3fffffff) + off) | (b & ~0x3fffffff));
+            } else {  // leaf: -(start + 1), count
+                T.la.push_back(a - poff);
+                T.lb.push_back(b);
+            }
+        }
+        T.prim_shape.insert(T.prim_shape.end(), o.T.prim_shape.begin(), o.T.prim_shape.end());
+        T.prim_seq.insert(T.prim_seq.end(), o.T.prim_seq.begin(), o.T.prim_seq.end());
+        leaf_ref.insert(leaf_ref.end(), o.leaf_ref.begin(), o.leaf_ref.end());
+        height = std::max(height, o.height);
+        return off;
+    }
 
     int leaf(int b, int e) {
         const int k = static_cast<int>(T.lbox.size());
@@ -691,6 +742,8 @@ struct SceneBuilder {
         leaf_ref.push_back(-1);
         return k;
     }
+
+    static constexpr int kParAtoms = 8192;  // halves smaller than this stay on one thread
 
     // bounded = false: atoms with infinite boxes, split by count only.
     int build(int b, int e, int depth, bool bounded) {
@@ -826,8 +879,21 @@ struct SceneBuilder {
                                  [&](const Atom& x, const Atom& y) { return x.c[axis] < y.c[axis]; });
         }
         const int k = inner(box, 0, 0, axis);
-        const int l = build(b, mid, depth + 1, bounded);
-        const int r = build(mid, e, depth + 1, bounded);
+        int l, r;
+        if (par > 0 && n >= kParAtoms) {
+            // the halves on two threads, each into its own arrays, then appended in the
+            // sequential order: the same tree, node for node (tools/native/accel_time.cpp)
+            AccelHost tl, tr;
+            SceneBuilder L{tl, atoms, ap, {}, hmax, 0, par - 1}, R{tr, atoms, ap, {}, hmax, 0, par - 1};
+            std::thread th([&] { L.build(b, mid, depth + 1, bounded); });
+            R.build(mid, e, depth + 1, bounded);
+            th.join();
+            l = splice(L);
+            r = splice(R);
+        } else {
+            l = build(b, mid, depth + 1, bounded);
+            r = build(mid, e, depth + 1, bounded);
+        }
         T.la[k] = l;
         T.lb[k] = r | (axis << 30);
         return k;
@@ -866,7 +932,11 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
     st.nested = 1;
     AccelHost T;
     T.mt = out.mt;  // the scene tree's cones follow the accelerator's triangle test
-    SceneBuilder sb{T, {}, {}, {}, kSceneHeight, 0};
+    std::vector<Atom> atoms;
+    std::vector<std::pair<int, int>> ap;
+    int par = 0;  // thread levels: 2^par halves at most in flight
+    while ((2 << par) <= build_threads()) ++par;
+    SceneBuilder sb{T, atoms, ap, {}, kSceneHeight, 0, par};
     std::vector<Atom> unb;
     const Box3 inf_box{{-INFINITY, -INFINITY, -INFINITY}, {INFINITY, INFINITY, INFINITY}};
     // An unbounded shape is tested only when the ray passes its reference leaf's
@@ -894,9 +964,9 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
             else bnd.push_back(i);
         }
         auto add = [&](std::vector<Atom>& dst, const std::vector<std::pair<int, int>>& ps, const Box3& box) {
-            Atom at{k, static_cast<int>(sb.ap.size()), static_cast<int>(ps.size()), box, {0.f, 0.f, 0.f}};
+            Atom at{k, static_cast<int>(ap.size()), static_cast<int>(ps.size()), box, {0.f, 0.f, 0.f}};
             for (int a = 0; a < 3; ++a) at.c[a] = std::isfinite(box.lo[a]) ? 0.5f * (box.lo[a] + box.hi[a]) : 0.f;
-            sb.ap.insert(sb.ap.end(), ps.begin(), ps.end());
+            ap.insert(ap.end(), ps.begin(), ps.end());
             dst.push_back(at);
         };
         if (bnd.size() <= static_cast<size_t>(kItemMax)) {
@@ -1010,14 +1080,22 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 
     std::vector<Box3> sbox(S);
     std::vector<int> scls(S);
-    for (int i = 0; i < S; ++i) {
-        scls[i] = classify(shapes[i], sbox[i], 0.0, mt);
-        if (scls[i] == BOUNDED)
-            for (int a = 0; a < 3; ++a)
-                out.scene_mag = std::max({out.scene_mag, std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
-    }
+    // shapes classified independently, in chunks on the build threads (max is exact
+    // in any order)
+    std::vector<float> mag(build_threads(), 0.f);
+    parallel_chunks(S, 4096, [&](int i0, int i1, int c) {
+        for (int i = i0; i < i1; ++i) {
+            scls[i] = classify(shapes[i], sbox[i], 0.0, mt);
+            if (scls[i] == BOUNDED)
+                for (int a = 0; a < 3; ++a)
+                    mag[c] = std::max({mag[c], std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
+        }
+    });
+    for (float m : mag) out.scene_mag = std::max(out.scene_mag, m);
     out.origin_lim = static_cast<float>((mt ? kOriginRelMt : kOriginRel) * (out.scene_mag + 1.0));
-    for (int i = 0; i < S; ++i) scls[i] = classify(shapes[i], sbox[i], out.origin_lim, mt);
+    parallel_chunks(S, 4096, [&](int i0, int i1, int) {
+        for (int i = i0; i < i1; ++i) scls[i] = classify(shapes[i], sbox[i], out.origin_lim, mt);
+    });
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).
