@@ -8,6 +8,7 @@
 #include <cstring>
 #include <functional>
 #include <numeric>
+#include <exception>
 #include <thread>
 
 namespace rta {
@@ -674,13 +675,24 @@ void parallel_chunks(int n, int min_per_thread, F fn) {
         return;
     }
     std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(T);  // rethrown on the calling thread after every join
     for (int c = 1; c < T; ++c)
         th.emplace_back([&, c] {
-            fn(static_cast<int>(static_cast<long long>(c) * n / T),
-               static_cast<int>(static_cast<long long>(c + 1) * n / T), c);
+            try {
+                fn(static_cast<int>(static_cast<long long>(c) * n / T),
+                   static_cast<int>(static_cast<long long>(c + 1) * n / T), c);
+            } catch (...) {
+                err[c] = std::current_exception();
+            }
         });
-    fn(0, static_cast<int>(static_cast<long long>(n) / T), 0);
+    try {
+        fn(0, static_cast<int>(static_cast<long long>(n) / T), 0);
+    } catch (...) {
+        err[0] = std::current_exception();
+    }
     for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
 }
 
 struct SceneBuilder {
@@ -885,9 +897,22 @@ struct SceneBuilder {
             // sequential order: the same tree, node for node (tools/native/accel_time.cpp)
             AccelHost tl, tr;
             SceneBuilder L{tl, atoms, ap, {}, hmax, 0, par - 1}, R{tr, atoms, ap, {}, hmax, 0, par - 1};
-            std::thread th([&] { L.build(b, mid, depth + 1, bounded); });
-            R.build(mid, e, depth + 1, bounded);
+            std::exception_ptr err;  // an exception on the helper thread (bad_alloc) reaches the caller
+            std::thread th([&] {
+                try {
+                    L.build(b, mid, depth + 1, bounded);
+                } catch (...) {
+                    err = std::current_exception();
+                }
+            });
+            try {
+                R.build(mid, e, depth + 1, bounded);
+            } catch (...) {
+                th.join();
+                throw;
+            }
             th.join();
+            if (err) std::rethrow_exception(err);
             l = splice(L);
             r = splice(R);
         } else {
