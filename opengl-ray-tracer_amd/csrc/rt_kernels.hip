@@ -3244,13 +3244,15 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             const bool stamps_fit =  // timed frames split only with a record per part
                 !c->tile_times ||
                 c->tile_times_cap >= static_cast<size_t>(k2.tiles) + static_cast<size_t>(std::min(hk, k2.tiles)) * hp;
-            // A dispatch that records wall-time costs runs every tile whole: a split tile's
-            // parts run side by side, so no sum or maximum of theirs stands for the whole
-            // tile's time, and a split set ranked by such an estimate locks in whatever
-            // tiles were split first (the latency-mode car waited frame settled at 0.222 or
+            // In latency mode a dispatch that records wall-time costs runs every tile whole:
+            // a split tile's parts run side by side, so no sum or maximum of theirs stands for
+            // the whole tile's time, and a split set ranked by such an estimate locks in
+            // whatever tiles were split first (the car's waited frame settled at 0.222 or
             // 0.237 ms by the split set it started from, r04z5). Recording whole tiles every
-            // 16th frame keeps the split set the 1/512 longest whole tiles.
-            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times;
+            // 16th frame keeps the split set the longest whole tiles. The all-packet frames'
+            // own split (8 waves, above) stays on their cost frames: whole, those took 1.5x
+            // (config 2, the MT car; r04zz profiles), and in flight the ranking matters less.
+            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times && c->latency_mode;
             if (!c->persistent && stamps_fit && hp > 1 && hk > 0 && !whole) {
                 k2.heavy_k = std::min(hk, k2.tiles);
                 k2.heavy_parts = hp;
