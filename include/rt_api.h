@@ -244,7 +244,9 @@ int rt_set_schedule(struct rt_ctx* ctx, int mode);
  * flight. 1: the accelerated kernel's instance with split walks in sparse
  * waves (idle lanes help a tile's few live rays) and, on frames not already
  * split, the heaviest 1/200 of the tiles as four waves each. Shortens one frame
- * (car: -19 %) and costs throughput when frames overlap. 0 (default): off.
+ * (car: -19 %) and costs throughput when frames overlap. Frames of more than 16
+ * tiles per wave slot (65,536 8x8 tiles on 256 CUs: 3840x2160 has 129,600)
+ * render as in the default mode, which is faster for them. 0 (default): off.
  * Same image either way. */
 int rt_set_latency_mode(struct rt_ctx* ctx, int on);
 

@@ -1539,6 +1539,7 @@ constexpr int kMtWalkFrom = 1 << 16;      // auto walk policy of Moller-Trumbore
 constexpr int kMtPacketMaxNodes = 1024;  // ... over reference trees of fewer nodes (walk_from)
 // the heaviest tiles of the cost order as several waves (rt_debug_heavy)
 constexpr int kHeavyTiles = -1, kHeavyParts = 4, kHeavyAutoSlots = 2;  // -1: auto
+constexpr int kLatencyMaxSlots = 16;  // latency mode: frames of at most this many tiles per wave slot
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
 
 __device__ __forceinline__ int work_bucket(unsigned c) {
@@ -3216,6 +3217,12 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces || k2.lane_k > 0
                                ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
                                : 0;
+        // rt_set_latency_mode applies to frames of at most kLatencyMaxSlots tiles per wave
+        // slot: a bigger frame keeps the chip busy on its own, and the split-walk instance's
+        // throughput cost then outweighs the shorter chains (waited frame, latency mode on
+        // against off: car 1080p 0.216 against 0.262 ms; car 3840x2160 0.706 against 0.626;
+        // config 5 3.364 against 3.332; profiles/r04zz2_latency_sweep_*.json)
+        const bool latency = c->latency_mode && k2.tiles <= kLatencyMaxSlots * c->cu_count * 16;
         if (k2.tile_order && k2.tile_order == c->sched_order) {
             // heavy tiles: explicit (rt_debug_heavy) or auto. A frame of at most
             // kHeavyAutoSlots waves per wave slot whose walks are all packets (config 2:
@@ -3229,7 +3236,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                    std::min(k2.lane_from_depth, k2.shadow_lane_from) >= k2.maxBounces;
                 hk = small ? std::max(16, k2.tiles / 256) : 0;
                 hp = small ? 8 : 1;
-                if (!small && c->latency_mode) {
+                if (!small && latency) {
                     // rt_set_latency_mode: the heaviest 1/200 as 4 waves. Car waited frame with the
                     // wall-time cost order and whole-tile cost frames (Python loop,
                     // profiles/r04z7_latency_sweep.json, r04z8_latency_sweep.json), heaviest k as
@@ -3252,7 +3259,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             // 16th frame keeps the split set the longest whole tiles. The all-packet frames'
             // own split (8 waves, above) stays on their cost frames: whole, those took 1.5x
             // (config 2, the MT car; r04zz profiles), and in flight the ranking matters less.
-            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times && c->latency_mode;
+            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times && latency;
             if (!c->persistent && stamps_fit && hp > 1 && hk > 0 && !whole) {
                 k2.heavy_k = std::min(hk, k2.tiles);
                 k2.heavy_parts = hp;
@@ -3331,7 +3338,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         } else if (kfn == k_accel<false, false, true>) {
             // production shape: the counter-free kernel on a dispatch that records no tile
             // work; the queueing kernel when the tail runs (other shapes: no compaction)
-            if (tail || c->latency_mode) {
+            if (tail || latency) {
                 // the compacting instance; in latency mode without a queue (tail_from 0), for
                 // its split walks in sparse waves (lane_walk_any), which the production
                 // instance leaves out for its registers

@@ -35,11 +35,11 @@ SETTINGS = {
     # the split set it started from; split-set sizes again (profiles/r04z7_latency_sweep.json).
     # Sweep 6 (r04z8): around the new default, 1/256 x 4 (profiles/r04z8_latency_sweep.json).
     # Sweep 7 (r04z12): the heaviest slots' camera rays per lane under the wall-time order
-    "lanek128m3": {"lane_k": (128, 3)},
-    "lanek648m3": {"lane_k": (648, 3)},
-    "lanek648m1": {"lane_k": (648, 1)},
-    "lanek2048m3": {"lane_k": (2048, 3)},
-    "lanek0": {"lane_k": (0, 0)},
+    # (profiles/r04z12_latency_sweep_lanek.json: neutral). Sweep 8 (r04zz2): big frames (config
+    # 4 at 3840x2160, config 5), latency mode against the default mode
+    "latency_off": {"latency": 0},
+    "no_heavy": {"heavy": (0, 1)},
+    "h1_512x4": {"heavy": (253, 4)},
 }
 
 
@@ -66,6 +66,7 @@ def main():
         c.debug_heavy(*s.get("heavy", (-1, 2)))
         c.debug_lane_k(*s.get("lane_k", (-1, 2)))
         c.debug_cost_time(s.get("cost_time", -1))
+        c.set_latency_mode(s.get("latency", 1))
 
     def frame():
         c.set_camera(fs.camera)
