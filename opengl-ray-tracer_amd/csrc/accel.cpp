@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <numeric>
 #include <exception>
 #include <thread>
@@ -1147,57 +1148,107 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
         }
     }
 
-    // Leaves: always-tested prims and local BVHs.
-    int max_stack = 1;
-    for (int k = 0; k < N; ++k) {
-        const FlatNode& nd = nodes[k];
-        if (!reach[k] || nd.leftChild != -1) continue;
-        std::vector<Item> bounded;
+    // Leaves: always-tested prims and local BVHs. Each leaf is worked out on its own
+    // (build threads, chunks of leaves), then appended in node order exactly as one
+    // sequential pass would: plain prims first, then the local tree, its nodes and prims
+    // renumbered by where they land (the same accelerator: tools/native/accel_time.cpp).
+    struct LeafOut {
+        Box3 content;
+        int flags = 0, bounded = 0;
         std::vector<std::pair<int, int>> plain;  // (shape, seq)
-        Box3 content = empty_box();
-        bool unb = false;
-        for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
-            const int si = idx[nd.startShapeIdx + i];
-            const int seq = seq_base[k] + i;
-            if (scls[si] == NEVER) continue;
-            if (scls[si] == UNBOUNDED) {
-                plain.push_back({si, seq});
-                unb = true;
-                continue;
+        std::unique_ptr<AccelHost> loc;         // the local tree, numbered from 0 (root 0)
+    };
+    std::vector<int> leaves;
+    for (int k = 0; k < N; ++k)
+        if (reach[k] && nodes[k].leftChild == -1) leaves.push_back(k);
+    std::vector<LeafOut> lo(leaves.size());
+    std::vector<char> too_deep(build_threads(), 0);
+    parallel_chunks(static_cast<int>(leaves.size()), 256, [&](int q0, int q1, int c) {
+        for (int q = q0; q < q1; ++q) {
+            const int k = leaves[q];
+            const FlatNode& nd = nodes[k];
+            LeafOut& L = lo[q];
+            std::vector<Item> bounded;
+            Box3 content = empty_box();
+            bool unb = false;
+            for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
+                const int si = idx[nd.startShapeIdx + i];
+                const int seq = seq_base[k] + i;
+                if (scls[si] == NEVER) continue;
+                if (scls[si] == UNBOUNDED) {
+                    L.plain.push_back({si, seq});
+                    unb = true;
+                    continue;
+                }
+                grow(content, sbox[si]);
+                Item it{si, seq, sbox[si], {}};
+                for (int a = 0; a < 3; ++a) it.c[a] = 0.5f * (sbox[si].lo[a] + sbox[si].hi[a]);
+                double nn[3];
+                if (mt && mt_normal(shapes[si], nn)) {
+                    it.hn = true;
+                    for (int a = 0; a < 3; ++a) it.n[a] = static_cast<float>(nn[a]);
+                    MtTri mtt;
+                    Box3 tb;
+                    it.big = classify_mt_tight(shapes[si], tb, 0.0, mtt) == BOUNDED && mtt.X > kMtBigX;
+                }
+                bounded.push_back(it);
             }
-            grow(content, sbox[si]);
-            Item it{si, seq, sbox[si], {}};
-            for (int a = 0; a < 3; ++a) it.c[a] = 0.5f * (sbox[si].lo[a] + sbox[si].hi[a]);
-            double nn[3];
-            if (mt && mt_normal(shapes[si], nn)) {
-                it.hn = true;
-                for (int a = 0; a < 3; ++a) it.n[a] = static_cast<float>(nn[a]);
-                MtTri mtt;
-                Box3 tb;
-                it.big = classify_mt_tight(shapes[si], tb, 0.0, mtt) == BOUNDED && mtt.X > kMtBigX;
+            L.content = content;
+            L.flags = (unb || mt) ? 0 : 8;  // MT boxes hold for non-grazing rays only: no content culling
+            if (static_cast<int>(bounded.size()) <= leaf_threshold) {
+                for (const Item& it : bounded) L.plain.push_back({it.shape, it.seq});
+                std::sort(L.plain.begin(), L.plain.end(), [](auto& a, auto& b) { return a.second < b.second; });
+                bounded.clear();
             }
-            bounded.push_back(it);
+            if (!bounded.empty()) {
+                const int budget = stack_cap - depth[k] - 2;
+                if (budget < 1) {
+                    too_deep[c] = 1;
+                    continue;
+                }
+                L.loc = std::make_unique<AccelHost>();
+                L.loc->mt = mt;
+                LocalBuilder lb{*L.loc, std::move(bounded)};
+                lb.build(0, static_cast<int>(lb.items.size()), 0, budget);
+                L.bounded = static_cast<int>(lb.items.size());
+            }
         }
-        out.content[k] = content;
-        out.flags[k] = (unb || mt) ? 0 : 8;  // MT boxes hold for non-grazing rays only: no content culling
-        if (static_cast<int>(bounded.size()) <= leaf_threshold) {
-            for (const Item& it : bounded) plain.push_back({it.shape, it.seq});
-            std::sort(plain.begin(), plain.end(), [](auto& a, auto& b) { return a.second < b.second; });
-            bounded.clear();
-        }
+    });
+    for (char t : too_deep)
+        if (t) return false;
+    int max_stack = 1;
+    for (size_t q = 0; q < leaves.size(); ++q) {
+        const int k = leaves[q];
+        LeafOut& L = lo[q];
+        out.content[k] = L.content;
+        out.flags[k] = L.flags;
         out.plain_start[k] = static_cast<int>(out.prim_shape.size());
-        out.plain_count[k] = static_cast<int>(plain.size());
-        for (auto [si, seq] : plain) {
+        out.plain_count[k] = static_cast<int>(L.plain.size());
+        for (auto [si, seq] : L.plain) {
             out.prim_shape.push_back(si);
             out.prim_seq.push_back(seq);
         }
-        out.always_prims += static_cast<int>(plain.size());
-        if (!bounded.empty()) {
-            LocalBuilder lb{out, std::move(bounded)};
-            const int budget = stack_cap - depth[k] - 2;
-            if (budget < 1) return false;
-            out.local_root[k] = lb.build(0, static_cast<int>(lb.items.size()), 0, budget);
-            out.bounded_prims += static_cast<int>(lb.items.size());
+        out.always_prims += static_cast<int>(L.plain.size());
+        if (L.loc) {
+            const AccelHost& o = *L.loc;
+            const int off = static_cast<int>(out.lbox.size()), poff = static_cast<int>(out.prim_shape.size());
+            out.lbox.insert(out.lbox.end(), o.lbox.begin(), o.lbox.end());
+            for (size_t j2 = 0; j2 < o.la.size(); ++j2) {
+                const int a = o.la[j2], b = o.lb[j2];
+                if (a >= 0) {  // inner: left, right | axis << 30
+                    out.la.push_back(a + off);
+                    out.lb.push_back(((b & 0x3fffffff) + off) | (b & ~0x3fffffff));
+                } else {  // leaf: -(start + 1), count
+                    out.la.push_back(a - poff);
+                    out.lb.push_back(b);
+                }
+            }
+            out.prim_shape.insert(out.prim_shape.end(), o.prim_shape.begin(), o.prim_shape.end());
+            out.prim_seq.insert(out.prim_seq.end(), o.prim_seq.begin(), o.prim_seq.end());
+            out.local_leaves += o.local_leaves;
+            out.local_root[k] = off;  // the local root is its tree's first node
+            out.bounded_prims += L.bounded;
+            L.loc.reset();
         }
         max_stack = std::max(max_stack, depth[k] + 1);
     }
