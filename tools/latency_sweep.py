@@ -37,9 +37,13 @@ SETTINGS = {
     # Sweep 7 (r04z12): the heaviest slots' camera rays per lane under the wall-time order
     # (profiles/r04z12_latency_sweep_lanek.json: neutral). Sweep 8 (r04zz2): big frames (config
     # 4 at 3840x2160, config 5), latency mode against the default mode
-    "latency_off": {"latency": 0},
-    "no_heavy": {"heavy": (0, 1)},
-    "h1_512x4": {"heavy": (253, 4)},
+    # (profiles/r04zz2_latency_sweep_*.json). Sweep 9 (r04zz8): split walks under the new order
+    "split16x16": {"split": (16, 16)},
+    "split32x8": {"split": (32, 8)},
+    "split8x8": {"split": (8, 8)},
+    "split16x32": {"split": (16, 32)},
+    "split32x16": {"split": (32, 16)},
+    "split4x8": {"split": (4, 8)},
 }
 
 
