@@ -188,7 +188,7 @@ RTA_HD float rcp(float x) {
 // side and `lf` (>= 1) to multiply the distance limit by.
 constexpr int kMtPadF = 6;  // floats per local node in AccelHost::lmt
 RTA_HD bool mt_pad(const RayC& c, float so, const float* k, const float* m, float& pad, float& lf, float& q2,
-                   float& pt) {
+                   float& pt, float& ilf) {
     const float D = c.dlen;
     const float cn = std::fabs(std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz))) - k[3];
     const float A = std::fmax(1e-5f, D * std::fmax(cn, 0.0f) * m[0]) - 7.0f * D * m[1];
@@ -199,10 +199,18 @@ RTA_HD bool mt_pad(const RayC& c, float so, const float* k, const float* m, floa
     const float q = D * m[1] * std::fma(18.0f, so, m[3]) * ia;
     const float dl = 9.09f * m[1] * (so + m[2]) * ia;
     lf = 1.0001f * rcp(1.0f - r);
+    // 1 / lf from below without a second reciprocal: (1 - r) / 1.0001 times 0.99999
+    // (0.99989 * 1.0001 = 0.999990), against a rounding of rcp and the products of a few ulp
+    ilf = (1.0f - r) * 0.99989f;
     q2 = 2.0f * q;
     pt = 2.0f * D * dl * lf;
     pad = q2 + pt;
     return pad < 1e30f;
+}
+RTA_HD bool mt_pad(const RayC& c, float so, const float* k, const float* m, float& pad, float& lf, float& q2,
+                   float& pt) {
+    float ilf;
+    return mt_pad(c, so, k, m, pad, lf, q2, pt, ilf);
 }
 
 // The node's slab along its cone axis a: every triangle below lies within

@@ -897,6 +897,9 @@ constexpr int kWideRec = 8, kWideRecMt = 17;
 #define RT_MT_UNROLL 4  // MT wide_kids: children per unrolled step (r03j: 1 -> 4 car MT -15 %)
 #endif
 constexpr int kMtUnroll = RT_MT_UNROLL;
+#ifndef RT_MT_ILF
+#define RT_MT_ILF 1  // MT entry parameter scaled by mt_pad's 1/lf bound, not a reciprocal (car MT -2.0 %, r04zz9)
+#endif
 
 // Float `comp` of child `sl`'s box (0-2 lo.xyz, 3-5 hi.xyz) in wide record w:
 // row comp, lane sl of the SoA records; float comp of the child's 16-float
@@ -930,15 +933,19 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
             const float4 f0 = q[4 * s2], f1 = q[4 * s2 + 1], f2v = q[4 * s2 + 2], f3 = q[4 * s2 + 3];
             const float k[4] = {f1.z, f1.w, f2v.x, f2v.y};
             const float m[6] = {f2v.z, f2v.w, f3.x, f3.y, f3.z, f3.w};
-            float pad, lf, q2, pt, tt = 0.0f;
+            float pad, lf, q2, pt, ilf, tt = 0.0f;
             bool hh = true;
-            if (rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt)) {
+            if (rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt, ilf)) {
                 float tn, tf;
                 hh = rta::box_span(c, f0.x - pad, f0.y - pad, f0.z - pad, f0.w + pad, f1.x + pad, f1.y + pad,
                                    tl * lf, tn, tf);
                 if (hh && c.ix != 0.0f && m[5] < 3e38f)
                     hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
+#if RT_MT_ILF
+                tt = tn * ilf;  // the stack's prune compares with tl, not tl * lf (ilf <= 1 / lf)
+#else
                 tt = tn * rta::rcp(lf) * 0.99999f;  // the stack's prune compares with tl, not tl * lf
+#endif
             }
             // select-written (a lane-varying index would put t / h in scratch)
             t[0] = s2 == 0 ? tt : t[0], t[1] = s2 == 1 ? tt : t[1], t[2] = s2 == 2 ? tt : t[2];
