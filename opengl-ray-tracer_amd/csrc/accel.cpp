@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -660,8 +661,13 @@ int log2_ceil(int n) {
 constexpr int kItemMax = RT_ITEM_MAX;
 
 // Host threads for the builds' independent halves (at most 16: the GPU box's CPU
-// share per GPU). 1 on a one-core host.
+// share per GPU). 1 on a one-core host; RTA_BUILD_THREADS overrides it (1-64; the
+// accelerator is the same for every count, tests/test_accel_cpu.py).
 int build_threads() {
+    if (const char* e = std::getenv("RTA_BUILD_THREADS")) {
+        const int v = std::atoi(e);
+        if (v >= 1) return std::min(v, 64);
+    }
     const unsigned h = std::thread::hardware_concurrency();
     return static_cast<int>(std::max(1u, std::min(16u, h)));
 }

@@ -104,6 +104,33 @@ bool padded(const rta::RayC& c, const rta::Box3& b, float l) {
 
 extern "C" {
 
+// FNV-1a over every field of the accelerator built for the scene (0 if it cannot be
+// built): equal hashes mean the same accelerator.
+unsigned long long accel_hash(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
+                              int mt) {
+    rta::AccelHost A;
+    if (!rta::build_accel(shapes, S, nodes, N, idx, I, 8, 64, A, mt != 0)) return 0;
+    unsigned long long h = 1469598103934665603ull;
+    auto bytes = [&](const void* p, size_t n) {
+        const unsigned char* c = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; ++i) h = (h ^ c[i]) * 1099511628211ull;
+    };
+    auto v = [&](const auto& x) {
+        const size_t n = x.size();
+        bytes(&n, sizeof n);
+        if (n) bytes(x.data(), n * sizeof(x[0]));
+    };
+    auto sc = [&](const auto& x) { bytes(&x, sizeof x); };
+    v(A.prim_shape); v(A.prim_seq); v(A.content); v(A.flags); v(A.plain_start); v(A.plain_count);
+    v(A.local_root); v(A.lbox); v(A.la); v(A.lb); v(A.lcone); v(A.wchild); v(A.wsub); v(A.wroot);
+    sc(A.max_stack); sc(A.scene_mag); sc(A.origin_lim); sc(A.always_prims); sc(A.bounded_prims);
+    sc(A.local_leaves);
+    v(A.st.box); v(A.st.a); v(A.st.b); v(A.st.item_of); v(A.st.item_ref); v(A.st.item_start);
+    v(A.st.item_count); v(A.st.wchild); v(A.st.wsub); sc(A.st.wroot); sc(A.st.max_stack); sc(A.st.height);
+    sc(A.st.nested); v(A.st_cone); v(A.lmt); sc(A.mt_z);
+    return h;
+}
+
 // For each ray (o[i], d[i]): the accelerated closest hit (shape index or -1)
 // and the rays' shadow query against lim[i]. Returns -1 if the accelerator
 // cannot be built for this tree. out_info[8] (in): 1 = rays take the scene

@@ -43,6 +43,25 @@ def _p(a):
     return C.c_void_p(a.ctypes.data) if a.size else None
 
 
+@pytest.mark.parametrize("cfg", [2, 3, 5])
+def test_threaded_build_is_the_sequential_one(check_lib, cfg, monkeypatch):
+    """The host build runs the scene tree's SAH halves, the shape classification and the
+    per-leaf local builds on several threads, each into its own arrays appended in the
+    sequential order: every field of the accelerator (FNV hash) is the same with 1, 3 and
+    8 threads, for the barycentric and the Moller-Trumbore builds."""
+    fs = rtamd.generate(cfg, 0, 320, 180)
+    fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)
+    check_lib.accel_hash.restype = C.c_ulonglong
+    check_lib.accel_hash.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
+    for mt in (0, 1):
+        hashes = []
+        for t in ("1", "3", "8"):
+            monkeypatch.setenv("RTA_BUILD_THREADS", t)
+            hashes.append(check_lib.accel_hash(_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes),
+                                               _p(fs.indices), len(fs.indices), mt))
+        assert hashes[0] != 0 and len(set(hashes)) == 1, (cfg, mt, hashes)
+
+
 def compare(lib, fs, o, d, lim, tree=1, mt=0, mutate=False):
     fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)  # enforce record layout
     R = len(o)
