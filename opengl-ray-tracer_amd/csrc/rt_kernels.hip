@@ -1693,6 +1693,10 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
 // writes each tile's start/end wall clock and walk counts (diagnostics only).
 // At most 128 VGPRs: four waves per SIMD, which the LDS stacks also fit
 // (accel.h, kLaneStack).
+#ifndef RT_UNIFORM_TILE
+#define RT_UNIFORM_TILE 0  // tile / part / slot forced into SGPRs in every instance: car +-0, config 2 -1 %,
+                           // latency instance 4 -> 9 spilled VGPRs (r04zz14); off
+#endif
 #ifndef RT_ACCEL_ATTR
 #define RT_ACCEL_ATTR __attribute__((amdgpu_waves_per_eu(4)))
 #endif
@@ -1722,7 +1726,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
         unsigned long long t0 = 0;
         if (TIMED || (REC && kp.cost_time)) t0 = wall_clock64();
         int part = 0;
-        const int slot = REC ? __builtin_amdgcn_readfirstlane(tile) : tile;
+        const int slot = REC || RT_UNIFORM_TILE ? __builtin_amdgcn_readfirstlane(tile) : tile;
         if (kp.tile_order) {  // dispatch order -> image tile (a permutation)
             if (tile < hs) {
                 part = tile % kp.heavy_parts + 1;
@@ -1731,7 +1735,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 tile = kp.tile_order[tile - hs + kp.heavy_k];
             }
         }
-        if (REC) {  // wave-uniform: kept in SGPRs through the walks for the cost record
+        if (REC || RT_UNIFORM_TILE) {  // wave-uniform: kept in SGPRs through the walks
             tile = __builtin_amdgcn_readfirstlane(tile);
             part = __builtin_amdgcn_readfirstlane(part);
         }
