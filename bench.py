@@ -650,8 +650,10 @@ def main():
     # so rank 0's frame includes the slowest peer's stripes crossing its link.
     serial_frames = []
     # at least three cost-order periods (rt_set_schedule: every 16th frame) before the waited
-    # frames are timed, so latency mode's order (its split tiles recorded) has settled
-    wait_warmup = max(a.warmup, 48)
+    # frames are timed, so latency mode's order (its split tiles recorded) has settled; fewer
+    # where 48 frames would take over 0.1 s (config 5: 30; the brute-force 100k frames: none)
+    est_ms = serial / a.steps * 1e3 if serial else None
+    wait_warmup = max(a.warmup, 48 if est_ms is None else min(48, int(100.0 / max(est_ms, 1e-3))))
     if not (strong and not use_group):  # the torch-gather rehearsal has no waited-frame figure
         for c_ in ctxs:
             c_.set_latency_mode(1)
