@@ -460,11 +460,12 @@ def test_cost_schedule_identical_images(ctx, sched):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 640, 360, 3), (5, 320, 180, 3)])
+@pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 640, 360, 3), (5, 320, 180, 3), (3, 3840, 2160, 3)])
 def test_latency_mode_exact(ctx, cfg, W, H, mb):
     """rt_set_latency_mode: the split-walk instance without a queue and the heaviest tiles
-    as two waves (or, on config 5, compaction as usual): every pixel equals the default
-    mode's frame, frame after frame, and the oracle on a band."""
+    as four waves (or, on config 5, compaction as usual), and at 3840x2160 (129,600 tiles,
+    over latency mode's 16 tiles per wave slot) the default mode's dispatch: every pixel
+    equals the default mode's frame, frame after frame, and the oracle on a band."""
     fs = rtamd.generate(cfg, 0, W, H)
     ctx.upload(fs)
     ctx.set_params(W, H, mb, True)
