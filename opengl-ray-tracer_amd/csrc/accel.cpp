@@ -984,43 +984,47 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
             if (!(b.lo[a] <= b.hi[a])) return inf_box;  // NaN from infinite bounds: no bound at all
         return b;
     };
+    // per-leaf scratch, reused (no allocation per leaf or per atom)
+    std::vector<int> bnd;
+    std::vector<std::pair<int, int>> ub, ps;
     for (int k = 0; k < N; ++k) {
         const FlatNode& nd = nodes[k];
         if (!reach[k] || nd.leftChild != -1) continue;
-        std::vector<int> bnd;
-        std::vector<std::pair<int, int>> ub;
+        bnd.clear();
+        ub.clear();
         for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
             const int si = idx[nd.startShapeIdx + i];
             if (scls[si] == NEVER) continue;
             if (scls[si] == UNBOUNDED) ub.push_back({si, seq_base[k] + i});
             else bnd.push_back(i);
         }
-        auto add = [&](std::vector<Atom>& dst, const std::vector<std::pair<int, int>>& ps, const Box3& box) {
-            Atom at{k, static_cast<int>(ap.size()), static_cast<int>(ps.size()), box, {0.f, 0.f, 0.f}};
+        // an atom of n (shape, seq) pairs starting at p
+        auto add = [&](std::vector<Atom>& dst, const std::pair<int, int>* p, int n, const Box3& box) {
+            Atom at{k, static_cast<int>(ap.size()), n, box, {0.f, 0.f, 0.f}};
             for (int a = 0; a < 3; ++a) at.c[a] = std::isfinite(box.lo[a]) ? 0.5f * (box.lo[a] + box.hi[a]) : 0.f;
-            ap.insert(ap.end(), ps.begin(), ps.end());
+            ap.insert(ap.end(), p, p + n);
             dst.push_back(at);
         };
         if (bnd.size() <= static_cast<size_t>(kItemMax)) {
             if (!bnd.empty()) {
                 Box3 box = empty_box();
-                std::vector<std::pair<int, int>> ps;
+                ps.clear();
                 for (int i : bnd) {
                     const int si = idx[nd.startShapeIdx + i];
                     grow(box, sbox[si]);
                     ps.push_back({si, seq_base[k] + i});
                 }
-                add(sb.atoms, ps, box);
+                add(sb.atoms, ps.data(), static_cast<int>(ps.size()), box);
             }
         } else {
             for (int i : bnd) {
                 const int si = idx[nd.startShapeIdx + i];
-                add(sb.atoms, {{si, seq_base[k] + i}}, sbox[si]);
+                const std::pair<int, int> one{si, seq_base[k] + i};
+                add(sb.atoms, &one, 1, sbox[si]);
             }
         }
         for (size_t q = 0; q < ub.size(); q += 4)
-            add(unb, std::vector<std::pair<int, int>>(ub.begin() + q, ub.begin() + std::min(ub.size(), q + 4)),
-                leaf_pad(nd));
+            add(unb, ub.data() + q, static_cast<int>(std::min(ub.size(), q + 4) - q), leaf_pad(nd));
     }
     const int nb = static_cast<int>(sb.atoms.size()), nu = static_cast<int>(unb.size());
     if (nb + nu == 0) return;
