@@ -93,6 +93,11 @@ def parse(argv=None):
                     help="the reference's animations, refit on the device (rt_animate) inside the timed step: "
                          "config 2 = scene 1's three bouncing spheres (bounceSphere, src/main.cpp:438-445); "
                          "configs 3/4 = the car's four wheels turning (updateWheelAnimations, :1084-1109)")
+    ap.add_argument("--upload", default="device", choices=["device", "reference"],
+                    help="--animate's per-frame upload: device = rt_animate (the records, updateBVH on the device); "
+                         "reference = the reference's own calls (src/main.cpp:336-346): one rt_update_shapes per "
+                         "animated record, updateBVH on the host (rts_update_bvh), one rt_update_nodes "
+                         "(librthost.so rth_upload_animated), applied by the renderer as a device refit")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU; 0 = auto: 3 below 64k 8x8 tiles (1080p), 2 above (4K), up "
                          "to 4 while the GPU's share of a frame has fewer than 16k tiles; strong mode over "
@@ -516,8 +521,13 @@ def main():
         # (config 2), scene 2's turning wheels (configs 3/4)
         anim = sphere_frames(fs, 512) if a.config == 2 else wheel_frames(fs, 64)
         for c_ in ctxs:
-            c_.set_animated(anim[0])
+            if a.upload == "device":
+                c_.set_animated(anim[0])
     applied = [[] for _ in ctxs]  # per renderer: the animation frames it was given, in order
+    # --upload reference: each renderer's host keeps its own scene arrays, moved by the
+    # reference's own upload calls
+    ref_up = [rtamd.ReferenceUpload(fs, anim[0]) for _ in ctxs] if anim is not None and a.upload == "reference" \
+        else None
 
     def frame(i, inflight):
         if use_group:
@@ -530,7 +540,10 @@ def main():
         c_ = ctxs[i % inflight]
         c_.set_camera(cam)
         c_.set_light(light)
-        if anim is not None:
+        if ref_up is not None:  # updateScene + updateBVH + their uploads, as the reference makes them
+            ref_up[i % inflight].upload(c_, anim[1][i % len(anim[1])])
+            applied[i % inflight].append(i % len(anim[1]))
+        elif anim is not None:
             c_.animate(anim[1][i % len(anim[1])])  # updateScene + updateBVH on the device
             applied[i % inflight].append(i % len(anim[1]))
         buf = bufs[i % inflight]
@@ -691,7 +704,8 @@ def main():
             c_.set_latency_mode(1)
         frames_anim = anim[1] if anim is not None else None
         for n_ in (wait_warmup, a.steps):
-            ms_ = rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, n_, True, anim=frames_anim)
+            ms_ = rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, n_, True, anim=frames_anim,
+                                    ref=ref_up[0] if ref_up is not None else None)
             if anim is not None:  # the C++ loop animates ctx 0 with frames 0, 1, ... (oracle bookkeeping)
                 applied[0].extend(i % len(frames_anim) for i in range(n_))
         serial_frames_host = list(ms_ * 1e-3)
@@ -748,6 +762,7 @@ def main():
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
         suffix = "".join(f"_{n}" for n, on in (("brute", a.brute), ("mt", a.mt), ("fresnel", a.fresnel),
                                                   ("variant", a.variant), ("animate", a.animate)) if on)
+        refits = {"rebuilds": [c_.debug_anim_rebuilds() for c_ in ctxs], "refits": [c_.debug_refits() for c_ in ctxs]}
         # strong lines: the same kernel over this rank's rows; the single-GPU entry with its
         # issue floors scaled by the row share (roofline docstring)
         pmc = pmc_entry(f"config{a.config}_n{1 if strong else world}_{a.kernel}{suffix}")
@@ -766,7 +781,9 @@ def main():
             "serial_frame_ms_median": float(np.median(serial_frames)) * 1e3 if serial_frames else None,
             "serial_frame_ms_median_python": float(np.median(serial_frames_py)) * 1e3 if serial_frames_py else None,
             "serial_frame_median_mode": (("C++ host loop (librthost.so rth_render_loop: camera + light upload, "
-                                          + ("rt_animate, " if anim is not None else "") +
+                                          + ("rt_animate, " if anim is not None and ref_up is None else
+                                             "rth_upload_animated (rt_update_shapes per record, rts_update_bvh, "
+                                             "rt_update_nodes), " if ref_up is not None else "") +
                                           "dispatch, rt_sync per frame), rt_set_latency_mode on"
                                           ) if serial_frames_host else
                                          ("each frame waited for (rt_sync: host polls the stream), "
@@ -788,9 +805,12 @@ def main():
                        "width": W, "height": H, "maxBounces": mb, "useBVH": int(not a.brute),
                        "useFresnel": int(a.fresnel), "triangle_test": "moller-trumbore" if a.mt else "barycentric",
                        "animate": (None if not a.animate else
-                                   "scene 1's three spheres bounce (bounceSphere, src/main.cpp:438-445), "
-                                   "device refit per frame" if a.config == 2 else
-                                   "wheels turn (updateWheelAnimations), device refit per frame"), "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
+                                   ("scene 1's three spheres bounce (bounceSphere, src/main.cpp:438-445)" if a.config == 2
+                                    else "wheels turn (updateWheelAnimations)") +
+                                   (", uploaded as the reference does (one rt_update_shapes per record, updateBVH "
+                                    "on the host, rt_update_nodes; src/main.cpp:336-346), device refit per frame"
+                                    if ref_up is not None else ", rt_animate (device refit) per frame")),
+                       "shapes": len(fs.shapes), "bvh_nodes": len(fs.nodes),
                        "bvh_max_leaf": sc_stats["max_leaf"], "kernel": a.kernel, "walk": a.walk,
                        "parallelism": (f"row-stripes{a.stripe}x{world}+gather" if strong else
                                        f"frame-sharded x{world} (one frame per GPU per step, orbit 1 deg/rank)"
@@ -808,6 +828,7 @@ def main():
             "kernel_ms_mean_inflight": float(np.mean(kt_if)) if len(kt_if) else float("nan"),
             "roofline": roofline(info, kname, k_ms, rows * W, b_ref_rank, pmc, share=rows / H if strong else None),
             "accel": info,
+            "scene_updates": refits if anim is not None else None,
             "cpu_baseline": None,
             "parity": None,
         }
@@ -824,11 +845,15 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle  # noqa: E402  (checker only)
             torch.cuda.synchronize()
-            checks = []
+            checks, host_nodes_ok = [], True
             for k, b_ in enumerate(bufs):
                 if not applied[k]:
                     continue
                 fk = animated_oracle_scene(fs, anim[0], anim[1], applied[k])
+                if ref_up is not None:  # the host's own updateBVH (rts_update_bvh) grew the same boxes
+                    host_nodes_ok = host_nodes_ok and all(
+                        np.array_equal(ref_up[k].nodes[f].view(np.uint32), fk.nodes[f].view(np.uint32))
+                        for f in ("boundsMin", "boundsMax"))
                 ref, _ = oracle.render(fk, W, H, oracle.params(W, H, mb, not a.brute, a.fresnel, a.mt), threads=thr)
                 checks.append(parity_check([b_.cpu().numpy()], 0, ref, ""))
             out["parity"] = {"max_abs": max(c["max_abs"] for c in checks),
@@ -838,7 +863,8 @@ def main():
                                          "its last frame's records, node boxes grown by oracle.update_bvh "
                                          "(updateBVH restated) over every frame it was given"),
                              "animation_frames_applied": [len(x) for x in applied],
-                             "ok": all(c["ok"] for c in checks)}
+                             "host_nodes_equal_oracle": host_nodes_ok if ref_up is not None else None,
+                             "ok": all(c["ok"] for c in checks) and host_nodes_ok}
         if mode == "frames" and anim is None:
             # the timed frames themselves, against the oracle (outside the timed region)
             if out["cpu_baseline"] is not None:

@@ -39,6 +39,25 @@ int rth_render_loop_anim(struct rt_ctx* ctx, const FlatCamera* cams, int ncams, 
                          int height, float* dst, size_t pitch, int frames, int wait_each, const FlatShape* anim,
                          int anim_count, int anim_frames, double* frame_ms);
 
+/* The reference's own per-frame upload of an animated scene, call for call
+ * (src/main.cpp:336-346): for each j, shapes[ids[j]] = recs[j] and one
+ * rt_update_shapes of that record (updateScene's glBufferSubData per animated
+ * index, :981-992); then updateBVH on the host's node records (rts_update_bvh,
+ * librtscene.so; :1068-1077), grown in place, and one rt_update_nodes of them all
+ * (serializeBVH + glBufferSubData, :340-345). The renderer applies both at the
+ * next dispatch as a device refit (rt_api.h). */
+int rth_upload_animated(struct rt_ctx* ctx, FlatShape* shapes, int num_shapes, const int* ids,
+                        const FlatShape* recs, int count, FlatNode* nodes, int num_nodes, const int* indices,
+                        int num_indices);
+
+/* rth_render_loop with that upload before each dispatch: frame i moves shapes
+ * ids[0..count) to anim[(i % anim_frames) * count + j]. shapes / nodes are the
+ * host's whole scene arrays, updated in place as the reference's are. */
+int rth_render_loop_ref(struct rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
+                        int height, float* dst, size_t pitch, int frames, int wait_each, FlatShape* shapes,
+                        int num_shapes, const int* ids, int count, const FlatShape* anim, int anim_frames,
+                        FlatNode* nodes, int num_nodes, const int* indices, int num_indices, double* frame_ms);
+
 #ifdef __cplusplus
 }
 #endif

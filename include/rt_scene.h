@@ -84,6 +84,15 @@ int rts_set_light(struct rts_scene* s, const float* position, const float* color
 /* buildBVH(maxDepth) (src/main.cpp:1175-1193). Replaces any previous tree. */
 int rts_build_bvh(struct rts_scene* s, int max_depth);
 
+/* updateBVH (src/main.cpp:1068-1077) on serialised arrays, for a host that keeps
+ * the reference's own per-frame upload (rt_update_nodes): every node whose shape
+ * set lists one of the shapes ids[0..count) (a leaf listing it in bvhIndices, and
+ * every node above that leaf) grows to include that shape's current record
+ * (growToInclude, src/BoundingBox.hpp:44-95), in the order the reference grows
+ * them. Grow-only; nodes are updated in place. 0, or -1 on bad arguments. */
+int rts_update_bvh(const FlatShape* shapes, int num_shapes, FlatNode* nodes, int num_nodes, const int* indices,
+                   int num_indices, const int* ids, int count);
+
 /* Sizes of the serialised arrays: shapes, nodes, bvhIndices. */
 int rts_counts(const struct rts_scene* s, int* num_shapes, int* num_nodes, int* num_indices);
 

@@ -6,16 +6,52 @@
 // waits for it (glfwSwapBuffers; FPS = 1 / deltaTime, :290-300). This file is that
 // loop with the rt_* calls that replace the GL ones, so a waited
 // frame can be timed the way a C++ host would see it, without an interpreter
-// between the calls. It links librtamd.so through its headers only.
+// between the calls. It links librtamd.so and librtscene.so through their headers only.
 #include <chrono>
 #include <cstddef>
 
 #include "../../include/rt_api.h"
 #include "../../include/rt_host.h"
+#include "../../include/rt_scene.h"
 
-extern "C" int rth_render_loop_anim(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light,
-                                    int width, int height, float* dst, size_t pitch, int frames, int wait_each,
-                                    const FlatShape* anim, int anim_count, int anim_frames, double* frame_ms) {
+// The reference's own upload of an animated frame, call for call (:336-346):
+// updateScene's glBufferSubData of each animated record (:981-992), updateBVH on
+// the host's node objects (:1068-1077), then serializeBVH and one glBufferSubData
+// of every node record (:340-345).
+extern "C" int rth_upload_animated(rt_ctx* ctx, FlatShape* shapes, int num_shapes, const int* ids,
+                                   const FlatShape* recs, int count, FlatNode* nodes, int num_nodes, const int* indices,
+                                   int num_indices) {
+    if (!ctx || !shapes || num_shapes < 0 || count < 0 || (count > 0 && (!ids || !recs)) || !nodes || num_nodes < 0)
+        return RT_ERR_INVALID;
+    for (int j = 0; j < count; ++j) {
+        if (ids[j] < 0 || ids[j] >= num_shapes) return RT_ERR_INVALID;
+        shapes[ids[j]] = recs[j];                                       // flatScene.shapes[i] = serializeShape(...)
+        const int rc = rt_update_shapes(ctx, ids[j], 1, &shapes[ids[j]]);  // glBufferSubData of that one record
+        if (rc != RT_OK) return rc;
+    }
+    if (rts_update_bvh(shapes, num_shapes, nodes, num_nodes, indices, num_indices, ids, count) != 0)  // updateBVH
+        return RT_ERR_INVALID;
+    return rt_update_nodes(ctx, nodes, num_nodes);  // serializeBVH + glBufferSubData of the nodes
+}
+
+namespace {
+
+struct RefUpload {  // rth_render_loop_ref's scene, moved by the reference's upload
+    FlatShape* shapes;
+    int num_shapes;
+    const int* ids;
+    int count;
+    const FlatShape* anim;
+    int anim_frames;
+    FlatNode* nodes;
+    int num_nodes;
+    const int* indices;
+    int num_indices;
+};
+
+int render_loop(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width, int height,
+                float* dst, size_t pitch, int frames, int wait_each, const FlatShape* anim, int anim_count,
+                int anim_frames, const RefUpload* ref, double* frame_ms) {
     if (!ctx || !cams || ncams < 1 || !light || !dst || frames < 0 || !frame_ms) return RT_ERR_INVALID;
     if (anim && (anim_count < 1 || anim_frames < 1)) return RT_ERR_INVALID;
     using clk = std::chrono::steady_clock;
@@ -26,6 +62,10 @@ extern "C" int rth_render_loop_anim(rt_ctx* ctx, const FlatCamera* cams, int nca
         if (rc == RT_OK) rc = rt_set_light(ctx, light);                                        // SSBO 1
         if (rc == RT_OK && anim)  // updateScene + updateBVH + their uploads (:336-346), on the device
             rc = rt_animate(ctx, anim + static_cast<size_t>(i % anim_frames) * anim_count);
+        if (rc == RT_OK && ref)  // the same, as the reference uploads it
+            rc = rth_upload_animated(ctx, ref->shapes, ref->num_shapes, ref->ids,
+                                     ref->anim + static_cast<size_t>(i % ref->anim_frames) * ref->count, ref->count,
+                                     ref->nodes, ref->num_nodes, ref->indices, ref->num_indices);
         if (rc == RT_OK) rc = rt_dispatch_rows(ctx, width, height, 0, 1, 1, height, dst, pitch);  // dispatch
         if (rc == RT_OK && wait_each) rc = rt_sync(ctx);                                       // the frame's end
         if (rc != RT_OK) return rc;
@@ -39,8 +79,28 @@ extern "C" int rth_render_loop_anim(rt_ctx* ctx, const FlatCamera* cams, int nca
     return RT_OK;
 }
 
+}  // namespace
+
+extern "C" int rth_render_loop_anim(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light,
+                                    int width, int height, float* dst, size_t pitch, int frames, int wait_each,
+                                    const FlatShape* anim, int anim_count, int anim_frames, double* frame_ms) {
+    return render_loop(ctx, cams, ncams, light, width, height, dst, pitch, frames, wait_each, anim, anim_count,
+                       anim_frames, nullptr, frame_ms);
+}
+
 extern "C" int rth_render_loop(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
                                int height, float* dst, size_t pitch, int frames, int wait_each, double* frame_ms) {
-    return rth_render_loop_anim(ctx, cams, ncams, light, width, height, dst, pitch, frames, wait_each, nullptr, 0, 0,
-                                frame_ms);
+    return render_loop(ctx, cams, ncams, light, width, height, dst, pitch, frames, wait_each, nullptr, 0, 0, nullptr,
+                       frame_ms);
+}
+
+extern "C" int rth_render_loop_ref(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
+                                   int height, float* dst, size_t pitch, int frames, int wait_each, FlatShape* shapes,
+                                   int num_shapes, const int* ids, int count, const FlatShape* anim, int anim_frames,
+                                   FlatNode* nodes, int num_nodes, const int* indices, int num_indices,
+                                   double* frame_ms) {
+    if (!shapes || !ids || !anim || count < 1 || anim_frames < 1 || !nodes) return RT_ERR_INVALID;
+    const RefUpload ref{shapes, num_shapes, ids, count, anim, anim_frames, nodes, num_nodes, indices, num_indices};
+    return render_loop(ctx, cams, ncams, light, width, height, dst, pitch, frames, wait_each, nullptr, 0, 0, &ref,
+                       frame_ms);
 }

@@ -1647,9 +1647,15 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
         // The root's exact test (gpu_shader.comp:386-395) from the kernel arguments: a camera
         // ray that misses it hits nothing in any walk (every leaf box lies inside the root's
         // for the scene tree; the reference walk starts there), so it takes the background
-        // without the walk's dependent loads -- the sky tiles of a frame.
-        const bool in = ray_aabb(ray.o, inv_dir(ray.d), mk(kp.root_lo[0], kp.root_lo[1], kp.root_lo[2]),
-                                 mk(kp.root_hi[0], kp.root_hi[1], kp.root_hi[2]));
+        // without the walk's dependent loads -- the sky tiles of a frame. root_ok 2: the
+        // boxes were grown on the device (rt_animate), read the root's from anodes.
+        V rlo = mk(kp.root_lo[0], kp.root_lo[1], kp.root_lo[2]), rhi = mk(kp.root_hi[0], kp.root_hi[1], kp.root_hi[2]);
+        if (kp.root_ok == 2) {
+            const float4 a = A.anodes[4 * static_cast<size_t>(A.N - 1)], b = A.anodes[4 * static_cast<size_t>(A.N - 1) + 1];
+            rlo = mk(a.x, a.y, a.z);
+            rhi = mk(b.x, b.y, b.z);
+        }
+        const bool in = ray_aabb(ray.o, inv_dir(ray.d), rlo, rhi);
         if (alive && !in) {
             acc = background(kp, tile_pixel(kp, tile).y);
             alive = false;
@@ -2022,7 +2028,10 @@ struct AnimMaps {
     const int *wn_off, *wn_list, *item_off, *item_list;
     int count, nodes;
 };
-enum { AF_BOUNDED = 1, AF_CONE = 2 };  // per-frame flags: conservative box valid; normal moved
+// per-frame flags of a refit entry: conservative box valid; normal moved; the nodes
+// listing it grow to hold it (rt_animate: updateBVH on the device; rt_update_shapes
+// leaves the node boxes to rt_update_nodes, as glBufferSubData of the shapes does)
+enum { AF_BOUNDED = 1, AF_CONE = 2, AF_GROW = 4 };
 
 struct AnimOut {
     FlatShape* shapes;  // staging copy of the full shape array
@@ -2054,8 +2063,8 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
     store_geo(o.geo_lin + 5 * static_cast<size_t>(id), g);
     store_mat(o.mat, id, s.material);
     for (int q = m.slot_off[i]; q < m.slot_off[i + 1]; ++q) store_geo(o.geo_leaf + 5 * static_cast<size_t>(m.slot_list[q]), g);
-    float lo[3], hi[3];
-    reference_box(s, lo, hi);
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (fl & AF_GROW) reference_box(s, lo, hi);  // else the nodes keep their boxes
     float4* sb = o.sbox + 4 * static_cast<size_t>(i);
     sb[0] = make_float4(lo[0], lo[1], lo[2], 0.f);
     sb[1] = make_float4(hi[0], hi[1], hi[2], 0.f);
@@ -2121,18 +2130,26 @@ __device__ void grow_node(const AnimMaps& m, const AnimOut& o, int j, int lane) 
     FlatNode& nd = o.nodes[k];
     float* mn = &nd.boundsMin.x;
     float* mx = &nd.boundsMax.x;
+    // Only entries with AF_GROW contribute to lo/hi (k_animate); a node none of them
+    // moves keeps every copy of its exact box as it is.
+    bool grew = false;
     for (int a = 0; a < 3; ++a) {  // glm::min(Min, p) = (p < Min) ? p : Min (BoundingBox.hpp:46)
+        grew = grew || lo[a] < mn[a] || mx[a] < hi[a];
         mn[a] = lo[a] < mn[a] ? lo[a] : mn[a];
         mx[a] = mx[a] < hi[a] ? hi[a] : mx[a];
     }
-    const bool leaf = nd.leftChild == -1;
-    const int ca = leaf ? -(nd.startShapeIdx + 1) : nd.leftChild, cb = leaf ? nd.numShapes : nd.rightChild;
-    o.packed[2 * static_cast<size_t>(k)] = make_float4(mn[0], mn[1], mn[2], __int_as_float(ca));
-    o.packed[2 * static_cast<size_t>(k) + 1] = make_float4(mx[0], mx[1], mx[2], __int_as_float(cb));
+    if (grew) {
+        const bool leaf = nd.leftChild == -1;
+        const int ca = leaf ? -(nd.startShapeIdx + 1) : nd.leftChild, cb = leaf ? nd.numShapes : nd.rightChild;
+        o.packed[2 * static_cast<size_t>(k)] = make_float4(mn[0], mn[1], mn[2], __int_as_float(ca));
+        o.packed[2 * static_cast<size_t>(k) + 1] = make_float4(mx[0], mx[1], mx[2], __int_as_float(cb));
+    }
     if (!o.anodes) return;
     float4* an = o.anodes + 4 * static_cast<size_t>(k);
-    an[0] = make_float4(mn[0], mn[1], mn[2], an[0].w);
-    an[1] = make_float4(mx[0], mx[1], mx[2], an[1].w);
+    if (grew) {
+        an[0] = make_float4(mn[0], mn[1], mn[2], an[0].w);
+        an[1] = make_float4(mx[0], mx[1], mx[2], an[1].w);
+    }
     float4 c0 = an[2], c1 = an[3];  // content box (accel.h)
     c0 = make_float4(fminf(c0.x, clo[0]), fminf(c0.y, clo[1]), fminf(c0.z, clo[2]), c0.w);
     c1 = make_float4(fmaxf(c1.x, chi[0]), fmaxf(c1.y, chi[1]), fmaxf(c1.z, chi[2]), c1.w);
@@ -2141,15 +2158,57 @@ __device__ void grow_node(const AnimMaps& m, const AnimOut& o, int j, int lane) 
     for (int qq = m.wn_off[j]; qq < m.wn_off[j + 1]; ++qq) {
         const int ws = m.wn_list[qq];
         float4* q = o.wnodes + 8 * static_cast<size_t>(ws >> 1) + 4 * (ws & 1);
-        q[0] = make_float4(mn[0], mn[1], mn[2], q[0].w);
-        q[1] = make_float4(mx[0], mx[1], mx[2], q[1].w);
+        if (grew) {
+            q[0] = make_float4(mn[0], mn[1], mn[2], q[0].w);
+            q[1] = make_float4(mx[0], mx[1], mx[2], q[1].w);
+        }
         q[2] = make_float4(c0.x, c0.y, c0.z, q[2].w);
         q[3] = make_float4(c1.x, c1.y, c1.z, q[3].w);
     }
+    if (!grew) return;
     for (int q = m.item_off[j]; q < m.item_off[j + 1]; ++q) {
         float4* t = o.titems + 2 * static_cast<size_t>(m.item_list[q]);
         t[0] = make_float4(mn[0], mn[1], mn[2], t[0].w);
         t[1] = make_float4(mx[0], mx[1], mx[2], t[1].w);
+    }
+}
+
+// rt_update_nodes, applied at the next device operation (flush_updates): the host's
+// node records (same topology) written to every copy the kernels read, from the
+// pinned staging buffer. Threads [0, N): node k's record, packed copy and
+// accelerator exact box, and for an inner node its children's exact boxes in its
+// wnodes record; threads [N, N + n_items): one scene-tree item's gating box (its
+// reference leaf's). Content boxes, cones and codes are the shapes' and stay.
+__global__ void k_set_nodes(const FlatNode* __restrict__ src, int N, FlatNode* __restrict__ staging,
+                            float4* __restrict__ packed, float4* __restrict__ anodes, float4* __restrict__ wnodes,
+                            float4* __restrict__ titems, const int* __restrict__ titem_ref, int n_items) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < N) {
+        const FlatNode n = src[k];
+        staging[k] = n;
+        const bool leaf = n.leftChild == -1;
+        const int ca = leaf ? -(n.startShapeIdx + 1) : n.leftChild, cb = leaf ? n.numShapes : n.rightChild;
+        packed[2 * static_cast<size_t>(k)] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, __int_as_float(ca));
+        packed[2 * static_cast<size_t>(k) + 1] =
+            make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, __int_as_float(cb));
+        if (!anodes) return;
+        float* a = reinterpret_cast<float*>(anodes + 4 * static_cast<size_t>(k));
+        a[0] = n.boundsMin.x, a[1] = n.boundsMin.y, a[2] = n.boundsMin.z;
+        a[4] = n.boundsMax.x, a[5] = n.boundsMax.y, a[6] = n.boundsMax.z;
+        if (leaf) return;
+        const int ch[2] = {n.leftChild, n.rightChild};
+        for (int s = 0; s < 2; ++s) {
+            const FlatNode& cn = src[ch[s]];
+            float* q = reinterpret_cast<float*>(wnodes + 8 * static_cast<size_t>(k) + 4 * s);
+            q[0] = cn.boundsMin.x, q[1] = cn.boundsMin.y, q[2] = cn.boundsMin.z;
+            q[4] = cn.boundsMax.x, q[5] = cn.boundsMax.y, q[6] = cn.boundsMax.z;
+        }
+    } else if (k - N < n_items && titems) {
+        const int i = k - N;
+        const FlatNode& ln = src[titem_ref[i]];
+        float* t = reinterpret_cast<float*>(titems + 2 * static_cast<size_t>(i));
+        t[0] = ln.boundsMin.x, t[1] = ln.boundsMin.y, t[2] = ln.boundsMin.z;
+        t[4] = ln.boundsMax.x, t[5] = ln.boundsMax.y, t[6] = ln.boundsMax.z;
     }
 }
 
@@ -2239,6 +2298,7 @@ struct rt_ctx {
     int n_titems = 0;
     int* anim_inf_slots = nullptr;  // wide slots whose boxes go infinite while animating (kNoPrune)
     int n_inf_slots = 0;
+    bool inf_open = false;          // open_inf_slots ran since the accelerator was built
     int st_root = 0x7fffffff;  // scene-tree root code, kNoChild if none
     int tree_mode = 1;         // rt_set_tree
     int scene_stack = 0;       // rt_debug_scene_stack (0: the walk's own cap)
@@ -2298,10 +2358,25 @@ struct rt_ctx {
     int* tile_counter = nullptr;
     unsigned long long* tile_times = nullptr;  // diagnostics (rt_debug_tile_times)
     size_t tile_times_cap = 0;
-    // animation (rt_set_animated / rt_animate)
-    std::vector<int> anim_ids;
-    std::vector<int> anim_cls;          // accelerator class of each at the last build (accel_bound.h)
-    std::vector<FlatShape> anim_base;   // the record the accelerator's cones were built from
+    // animation (rt_set_animated / rt_animate) and the reference's own uploads
+    // (rt_update_shapes / rt_update_nodes), both applied by the device refit
+    std::vector<int> anim_ids;          // rt_set_animated's set, in rt_animate's record order
+    // The refit set: every shape moved since the accelerator was built (the animated
+    // set plus the shapes rt_update_shapes rewrote). One entry each; AnimMaps lists them.
+    std::vector<int> refit_ids;
+    std::vector<int> refit_of;          // per shape: its refit entry, -1 if none
+    std::vector<int> anim_cls;          // per refit entry: accelerator class at the last build (accel_bound.h)
+    std::vector<FlatShape> anim_base;   // per refit entry: the record the accelerator's cones were built from
+    std::vector<int> refit_flags;       // per refit entry: AF_BOUNDED / AF_CONE of its current record
+    // rt_update_shapes / rt_update_nodes only write the host copies; the next device
+    // operation (flush_updates) applies them in one refit, like glBufferSubData
+    // calls that take effect at the next dispatch.
+    std::vector<int> upd_ids;           // shapes written since the last flush
+    std::vector<char> upd_mark;         // per shape: listed in upd_ids
+    std::vector<std::pair<int, FlatShape>> upd_base;  // their build-time records (shapes new to the refit set)
+    bool nodes_dirty = false;           // host_nodes newer than every device copy
+    bool nodes_rebuild = false;         // host_nodes break a condition the accelerator was built on
+    int updates_flushed = 0;            // flushes that refit instead of rebuilding (diagnostics)
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
     size_t anim_maps_cap = 0;
     AnimMaps anim{};
@@ -2377,6 +2452,7 @@ void free_accel(rt_ctx* c) {
     hipFree(c->anim_inf_slots);
     c->anim_inf_slots = nullptr;
     c->n_inf_slots = 0;
+    c->inf_open = false;
     c->st_root = kNoChild;
     hipFree(c->prims);
     hipFree(c->prim_idx_dev);
@@ -2636,16 +2712,49 @@ int sync_host_nodes(rt_ctx* c) {
     return RT_OK;
 }
 
-// The device lists of rt_animate (AnimMaps) for the current scene and
-// accelerator. anim_base holds, per animated shape, the record the
-// accelerator's bounds and cones were built from.
+// The scene tree's unbounded part (kNoPrune) has boxes padded from the reference
+// leaves' exact boxes, which animation and rt_update_nodes change: once they may
+// differ from the build's, those wide slots go infinite (entered by every ray; the
+// items' exact boxes still gate). Idempotent; reset by every accelerator build.
+int open_inf_slots(rt_ctx* c) {
+    if (c->inf_open || !c->accel_ok) return RT_OK;
+    const rta::AccelHost& A = c->accel;
+    const rta::SceneTree& T = A.st;
+    c->inf_open = true;
+    if (T.wroot < 0) return RT_OK;
+    const size_t nw = A.wchild.size() / rta::kWide;
+    std::vector<int> slots;
+    for (size_t q = 0; q < T.wchild.size(); ++q) {
+        const int j = T.wchild[q];
+        if (j >= 0 && A.st_cone[4 * static_cast<size_t>(j) + 3] <= rta::kNoPrune)
+            slots.push_back(static_cast<int>(4 * nw + q));
+    }
+    hipFree(c->anim_inf_slots);
+    c->anim_inf_slots = nullptr;
+    c->n_inf_slots = static_cast<int>(slots.size());
+    if (slots.empty()) return RT_OK;
+    if (hipMalloc(&c->anim_inf_slots, slots.size() * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
+    HIP_TRY(hipMemcpyAsync(c->anim_inf_slots, slots.data(), slots.size() * sizeof(int), hipMemcpyHostToDevice,
+                           c->stream));
+    hipLaunchKernelGGL(k_inf_slots, dim3((c->n_inf_slots + 255) / 256), dim3(256), 0, c->stream, c->anim_inf_slots,
+                       c->n_inf_slots, c->lnodes, c->accel.mt ? kWideRecMt : kWideRec);
+    HIP_TRY(hipGetLastError());
+    return RT_OK;
+}
+
+// The device lists of the refit (AnimMaps) for the current scene, accelerator and
+// refit set (refit_ids: the animated shapes and those rt_update_shapes rewrote).
+// anim_base holds, per entry, the record the accelerator's bounds and cones were
+// built from.
 int prepare_animation(rt_ctx* c) {
-    const int n = static_cast<int>(c->anim_ids.size());
+    const int n = static_cast<int>(c->refit_ids.size());
     c->anim = AnimMaps{};
+    c->refit_of.assign(c->S, -1);
+    for (int i = 0; i < n; ++i) c->refit_of[c->refit_ids[i]] = i;
+    c->refit_flags.assign(n, -1);  // -1: derive at the next flush
     if (n == 0) return RT_OK;
     const int N = c->N;
-    std::vector<int> which(c->S, -1);  // shape -> animated index
-    for (int i = 0; i < n; ++i) which[c->anim_ids[i]] = i;
+    const std::vector<int>& which = c->refit_of;  // shape -> refit entry
     const rta::AccelHost& A = c->accel;
     c->anim_cls.assign(n, rta::UNBOUNDED);
     for (int i = 0; i < n; ++i) {
@@ -2742,7 +2851,6 @@ int prepare_animation(rt_ctx* c) {
         // prims are contiguous. Its unbounded part (kNoPrune: boxes are the padded
         // reference-leaf boxes, which grow) goes infinite while the set is animated;
         // the items' exact boxes follow the grown leaves (k_anim_refit).
-        std::vector<int> inf_slots;
         const rta::SceneTree& T = A.st;
         if (T.wroot >= 0) {
             const size_t nw = A.wchild.size() / rta::kWide, Ms = T.box.size();
@@ -2770,8 +2878,6 @@ int prepare_animation(rt_ctx* c) {
             for (size_t q = 0; q < T.wchild.size(); ++q)
                 if (T.wchild[q] >= 0) swpos[T.wchild[q]] = static_cast<int>(4 * nw + q);
             auto noprune = [&](int j) { return A.st_cone[4 * static_cast<size_t>(j) + 3] <= rta::kNoPrune; };
-            for (size_t j = 0; j < Ms; ++j)
-                if (swpos[j] >= 0 && noprune(static_cast<int>(j))) inf_slots.push_back(swpos[j]);
             std::vector<int> sstamp(Ms, -1);
             std::vector<char> sdirty(Ms, 0);
             for (size_t p = 0; p < P; ++p) {
@@ -2810,20 +2916,11 @@ int prepare_animation(rt_ctx* c) {
             HIP_TRY(hipMemcpyAsync(c->refit_dirty, work.data(), work.size() * sizeof(int4), hipMemcpyHostToDevice,
                                    c->stream));
         c->n_dirty = static_cast<int>(work.size());
-        hipFree(c->anim_inf_slots);
-        c->anim_inf_slots = nullptr;
-        c->n_inf_slots = static_cast<int>(inf_slots.size());
-        if (!inf_slots.empty()) {
-            if (hipMalloc(&c->anim_inf_slots, inf_slots.size() * sizeof(int)) != hipSuccess) return RT_ERR_NO_MEMORY;
-            HIP_TRY(hipMemcpyAsync(c->anim_inf_slots, inf_slots.data(), inf_slots.size() * sizeof(int),
-                                   hipMemcpyHostToDevice, c->stream));
-            hipLaunchKernelGGL(k_inf_slots, dim3((c->n_inf_slots + 255) / 256), dim3(256), 0, c->stream,
-                               c->anim_inf_slots, c->n_inf_slots, c->lnodes, c->accel.mt ? kWideRecMt : kWideRec);
-            HIP_TRY(hipGetLastError());
-        }
+        const int rc = open_inf_slots(c);
+        if (rc != RT_OK) return rc;
     }
     // one int allocation: ids, then (offsets, list) x 4
-    std::vector<int> buf(c->anim_ids);
+    std::vector<int> buf(c->refit_ids);
     auto append = [&](const std::vector<std::vector<int>>& lists, size_t& off_at, size_t& list_at) {
         off_at = buf.size();
         int run = 0;
@@ -2890,10 +2987,169 @@ int upload_accel(rt_ctx* c) {
     int rc = sync_host_nodes(c);
     if (rc != RT_OK) return rc;
     rc = build_upload_accel(c);
-    c->anim_base.resize(c->anim_ids.size());
-    for (size_t i = 0; i < c->anim_ids.size(); ++i) c->anim_base[i] = c->host_shapes[c->anim_ids[i]];
+    // the refit set stays (its shapes tend to move again), with the records just built from
+    c->anim_base.resize(c->refit_ids.size());
+    for (size_t i = 0; i < c->refit_ids.size(); ++i) c->anim_base[i] = c->host_shapes[c->refit_ids[i]];
+    c->nodes_rebuild = false;
     const int rc2 = prepare_animation(c);
     return rc != RT_OK ? rc : rc2;
+}
+
+// Whether every reachable inner node's children lie inside its box (accel.cpp
+// boxes_nest), the condition the scene tree was built on.
+bool host_nodes_nest(const rt_ctx* c) {
+    const int N = c->N;
+    if (N <= 0) return true;
+    auto in = [](const FlatNode& p, const FlatNode& q) {
+        const float* plo = &p.boundsMin.x;
+        const float* phi = &p.boundsMax.x;
+        const float* qlo = &q.boundsMin.x;
+        const float* qhi = &q.boundsMax.x;
+        for (int a = 0; a < 3; ++a)
+            if (!(plo[a] <= qlo[a] && qlo[a] <= phi[a] && plo[a] <= qhi[a] && qhi[a] <= phi[a])) return false;
+        return true;
+    };
+    std::vector<char> seen(N, 0);
+    std::vector<int> st{N - 1};
+    while (!st.empty()) {
+        const int k = st.back();
+        st.pop_back();
+        if (seen[k]) continue;
+        seen[k] = 1;
+        const FlatNode& nd = c->host_nodes[k];
+        if (nd.leftChild == -1) continue;
+        if (!in(nd, c->host_nodes[nd.leftChild]) || !in(nd, c->host_nodes[nd.rightChild])) return false;
+        st.push_back(nd.leftChild);
+        st.push_back(nd.rightChild);
+    }
+    return true;
+}
+
+// A slot of the pinned ring k_animate / k_set_nodes read from, at least `bytes`
+// large; waits for that slot's previous reader (kAnimRing flushes back).
+int pinned_slot(rt_ctx* c, size_t bytes, char** host, const char** dev) {
+    const int slot = c->anim_slot;
+    c->anim_slot = (slot + 1) % rt_ctx::kAnimRing;
+    if (!c->anim_copied[slot]) {
+        HIP_TRY(hipEventCreateWithFlags(&c->anim_copied[slot], hipEventDisableTiming));
+    } else {
+        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // this slot's last readers have run
+    }
+    if (c->anim_pinned_cap[slot] < bytes) {
+        if (c->anim_pinned[slot]) hipHostFree(c->anim_pinned[slot]);
+        c->anim_pinned[slot] = nullptr;
+        c->anim_pinned_dev[slot] = nullptr;
+        c->anim_pinned_cap[slot] = 0;
+        // mapped and coherent: the kernels read it over the host link, never a stale cached copy
+        if (hipHostMalloc(&c->anim_pinned[slot], bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+            return RT_ERR_NO_MEMORY;
+        if (hipHostGetDevicePointer(&c->anim_pinned_dev[slot], c->anim_pinned[slot], 0) != hipSuccess)
+            return RT_ERR_DEVICE;
+        c->anim_pinned_cap[slot] = bytes;
+    }
+    *host = static_cast<char*>(c->anim_pinned[slot]);
+    *dev = static_cast<const char*>(c->anim_pinned_dev[slot]);
+    return slot;
+}
+
+// Applies what rt_update_shapes / rt_update_nodes left on the host, and an
+// rt_animate frame (grow: the animated entries grow the nodes listing them, as
+// updateBVH does), to every device copy in one refit on the stream:
+//   k_animate    every refit entry's records, read from the pinned ring;
+//   k_anim_refit the nodes listing an entry (their content boxes; with grow their
+//                exact boxes) and the local / scene-tree boxes above its prims;
+//   k_set_nodes  the host's node records (rt_update_nodes), exact boxes only.
+// No host rebuild unless a moved shape changed its kind of bound or the new node
+// boxes break the nesting the scene tree was built on (then after the refit, as
+// rt_animate always did). Called by every operation that reads the device scene.
+int flush_updates(rt_ctx* c, bool grow = false) {
+    if (!c->have_scene || (c->upd_ids.empty() && !c->nodes_dirty && !grow)) return RT_OK;
+    int rc = RT_OK;
+    // shapes new to the refit set join it with their build-time records
+    bool added = false;
+    for (const auto& ub : c->upd_base)
+        if (c->refit_of[ub.first] < 0) {
+            c->refit_of[ub.first] = static_cast<int>(c->refit_ids.size());
+            c->refit_ids.push_back(ub.first);
+            c->anim_base.push_back(ub.second);
+            added = true;
+        }
+    if (added && (rc = prepare_animation(c)) != RT_OK) return rc;
+    const int n = static_cast<int>(c->refit_ids.size());
+    // per entry: class (a change rebuilds), cone (a moved normal drops its cones), grow
+    bool rebuild = c->nodes_rebuild;
+    std::vector<char> grows(n, 0);
+    if (grow)
+        for (int id : c->anim_ids)
+            if (c->refit_of[id] >= 0) grows[c->refit_of[id]] = 1;
+    std::vector<int> flags(n);
+    for (int i = 0; i < n; ++i) {
+        const int id = c->refit_ids[i];
+        if (c->refit_flags[i] < 0 || c->upd_mark[id] || grows[i]) {  // a record written since the last flush
+            const FlatShape &s = c->host_shapes[id], &b0 = c->anim_base[i];
+            int cls = rta::UNBOUNDED;
+            if (c->accel_ok) cls = rta::classify_class(s, c->accel.origin_lim);  // classify's class, without the box
+            const bool cone = s.type != b0.type || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
+                                                    std::memcmp(&s.planeNormal, &b0.planeNormal, sizeof(rt_vec3)) != 0);
+            c->refit_flags[i] = (cls == rta::BOUNDED ? AF_BOUNDED : 0) | (cone ? AF_CONE : 0) |
+                                (c->accel_ok && cls != c->anim_cls[i] ? 8 : 0);
+        }
+        if (c->refit_flags[i] & 8) rebuild = true;  // a bound changed kind since the build
+        flags[i] = (c->refit_flags[i] & (AF_BOUNDED | AF_CONE)) | (grows[i] ? AF_GROW : 0);
+    }
+    const bool nodes = c->nodes_dirty && c->N > 0;
+    const size_t rec_bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
+    const size_t bytes = rec_bytes + (nodes ? static_cast<size_t>(c->N) * sizeof(FlatNode) : 0);
+    if (bytes > 0) {
+        char* pin = nullptr;
+        const char* pin_dev = nullptr;
+        const int slot = pinned_slot(c, bytes, &pin, &pin_dev);
+        if (slot < 0) return slot;
+        for (int i = 0; i < n; ++i)
+            std::memcpy(pin + i * sizeof(FlatShape), &c->host_shapes[c->refit_ids[i]], sizeof(FlatShape));
+        std::memcpy(pin + n * sizeof(FlatShape), flags.data(), n * sizeof(int));
+        if (nodes) std::memcpy(pin + rec_bytes, c->host_nodes.data(), c->N * sizeof(FlatNode));
+        const bool acc = c->accel_ok;
+        const size_t P = c->accel.prim_shape.size();
+        if (n > 0) {
+            const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat, c->nodes,
+                              acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
+                              acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
+                              acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
+                              c->accel.origin_lim, c->accel.mt ? 1 : 0};
+            // 1. the entries' records and boxes, read from the pinned buffer
+            hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
+                               reinterpret_cast<const FlatShape*>(pin_dev),
+                               reinterpret_cast<const int*>(pin_dev + n * sizeof(FlatShape)), c->anim, out);
+            // 2. the nodes listing them (written through to every copy) and the refit local boxes
+            const int nd = acc ? c->n_dirty : 0;
+            if (c->anim.nodes + nd > 0)
+                hipLaunchKernelGGL(k_anim_refit, dim3((c->anim.nodes + nd + 3) / 4), dim3(256), 0, c->stream, c->anim,
+                                   out, c->refit_dirty, nd, c->accel.mt ? kWideRecMt : kWideRec);
+        }
+        if (nodes) {
+            // 3. rt_update_nodes: the host's records to every copy of the exact boxes
+            const int items = acc ? c->n_titems : 0;
+            hipLaunchKernelGGL(k_set_nodes, dim3((c->N + items + 255) / 256), dim3(256), 0, c->stream,
+                               reinterpret_cast<const FlatNode*>(pin_dev + rec_bytes), c->N, c->staging_nodes,
+                               c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr,
+                               acc ? c->titems : nullptr, c->titem_ref, items);
+        }
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));  // the slot may be refilled after this
+        if (nodes && (rc = open_inf_slots(c)) != RT_OK) return rc;
+    }
+    if (grow) c->nodes_on_device_newer = true;  // the device grew the nodes past host_nodes
+    c->nodes_dirty = false;
+    for (int id : c->upd_ids) c->upd_mark[id] = 0;
+    c->upd_ids.clear();
+    c->upd_base.clear();
+    if (!rebuild) {
+        ++c->updates_flushed;
+        return RT_OK;
+    }
+    ++c->anim_rebuilds;
+    return upload_accel(c);  // a bound changed kind, or the boxes stopped nesting: rebuild from the host copies
 }
 
 size_t sched_set_words(int tiles) {
@@ -3022,7 +3278,7 @@ bool sub_usable(const rt_ctx* b, const KParams& kp) {
 // leaf listing 0..S-1 with an infinite box, built on first use after the
 // shapes change. nullptr: render the branch literally (k_packet).
 rt_ctx* brute_ctx(rt_ctx* c, const KParams& kp) {
-    if (!c->brute_accel || kp.useBVH || !c->anim_ids.empty() || c->S <= 0 ||
+    if (!c->brute_accel || kp.useBVH || c->S <= 0 ||
         (c->kernel != RT_KERNEL_AUTO && c->kernel != RT_KERNEL_ACCEL))
         return nullptr;
     rt_ctx* b = sub_ctx(c, c->brute, c->brute_stale);
@@ -3113,6 +3369,7 @@ int render(rt_ctx* c, const KParams& kp) {
 }
 
 int launch(rt_ctx* c, const KParams& kp, bool stats) {
+    if (const int rc = flush_updates(c)) return rc;  // rt_update_shapes / rt_update_nodes since the last dispatch
     if (kp.out_rows == 0) return RT_OK;
     dim3 grid((kp.width + kTileW - 1) / kTileW, (kp.out_rows + kTileH - 1) / kTileH);
     if (grid.y > 65535u) return RT_ERR_INVALID;
@@ -3188,11 +3445,12 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             ++c->sched_frame;
         }
         k2.lane_from_depth = walk_from(c);
-        // the root's bounds as kernel arguments while the host copy is current (rt_animate
-        // grows boxes on the device)
+        // the root's bounds as kernel arguments while the host copy is current; once
+        // rt_animate grew the boxes on the device, from the accelerator's copy of the
+        // root record (which the refit keeps current)
         k2.root_ok = 0;
-        if (kp.N > 0 && kp.useBVH && c->anim_ids.empty() && !c->nodes_on_device_newer &&
-            static_cast<int>(c->host_nodes.size()) == kp.N) {
+        if (kp.N > 0 && kp.useBVH && c->nodes_on_device_newer) k2.root_ok = 2;
+        if (kp.N > 0 && kp.useBVH && !c->nodes_on_device_newer && static_cast<int>(c->host_nodes.size()) == kp.N) {
             const FlatNode& rn = c->host_nodes[kp.N - 1];
             k2.root_ok = 1;
             k2.root_lo[0] = rn.boundsMin.x;
@@ -3594,6 +3852,12 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->have_scene = true;
     c->nodes_on_device_newer = false;
     c->anim_ids.clear();  // ids refer to the previous scene
+    c->refit_ids.clear();
+    c->anim_base.clear();
+    c->upd_ids.clear();
+    c->upd_base.clear();
+    c->upd_mark.assign(S, 0);
+    c->nodes_dirty = c->nodes_rebuild = false;
     c->brute_stale = c->mtc_stale = true;
     return upload_accel(c);
 }
@@ -3602,18 +3866,26 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
     if (!c || !c->have_scene || first < 0 || count < 0 || first > c->S - count || (count > 0 && !shapes))
         return RT_ERR_INVALID;
     if (count == 0) return RT_OK;
-    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    // Rewrite the shape-order records of [first, first+count), then every
-    // leaf slot; the leaf copy is re-packed from the full staging array.
-    HIP_TRY(hipMemcpyAsync(c->staging_shapes + first, shapes, count * sizeof(FlatShape), hipMemcpyHostToDevice,
-                           c->stream));
-    hipLaunchKernelGGL(k_pack_shapes, dim3((c->S + c->I + 255) / 256), dim3(256), 0, c->stream, c->staging_shapes,
-                       c->S, c->staging_idx, c->I, c->geo_lin, c->geo_leaf, c->mat);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));  // glBufferSubData semantics: the host array may be reused
-    std::copy(shapes, shapes + count, c->host_shapes.begin() + first);
-    c->brute_stale = c->mtc_stale = true;
-    return upload_accel(c);  // moved shapes change the conservative bounds
+    // glBufferSubData of shape records (updateScene, src/main.cpp:981-992): the host copy
+    // now, the device copies at the next operation that reads them (flush_updates), as
+    // one refit with whatever else was written by then. The host array may be reused
+    // when this returns. Node boxes stay as they are until rt_update_nodes.
+    for (int j = 0; j < count; ++j) {
+        const int id = first + j;
+        if (!c->upd_mark[id]) {
+            if (c->refit_of[id] < 0) c->upd_base.emplace_back(id, c->host_shapes[id]);  // the build's record
+            c->upd_mark[id] = 1;
+            c->upd_ids.push_back(id);
+        }
+        c->host_shapes[id] = shapes[j];
+    }
+    // the brute-force context holds the same shapes in the same order: it refits too
+    if (c->brute && !c->brute_stale) {
+        const int rc = rt_update_shapes(c->brute, first, count, shapes);
+        if (rc != RT_OK) c->brute_stale = true;
+    }
+    c->mtc_stale = true;
+    return RT_OK;
 }
 
 int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
@@ -3625,15 +3897,20 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
             return RT_ERR_BVH;  // topology must not change: use rt_upload_scene
     }
     if (N == 0) return RT_OK;
-    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    HIP_TRY(hipMemcpyAsync(c->staging_nodes, nodes, N * sizeof(FlatNode), hipMemcpyHostToDevice, c->stream));
-    hipLaunchKernelGGL(k_pack_nodes, dim3((N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, N, c->nodes);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));  // the host array may be reused after return
+    // glBufferSubData of the node records (src/main.cpp:340-345): the host copy now,
+    // every device copy of the boxes at the next device operation (flush_updates).
     c->host_nodes.assign(nodes, nodes + N);
-    c->nodes_on_device_newer = false;
+    c->nodes_on_device_newer = false;  // these boxes replace any the device grew
+    c->nodes_dirty = true;
+    c->boxes_finite = 1;
+    for (int k = 0; k < N; ++k)
+        for (float v : {nodes[k].boundsMin.x, nodes[k].boundsMin.y, nodes[k].boundsMin.z, nodes[k].boundsMax.x,
+                        nodes[k].boundsMax.y, nodes[k].boundsMax.z})
+            if (std::isnan(v)) c->boxes_finite = 0;
+    // the scene tree holds only while the boxes nest (accel.h SceneTree)
+    if (c->accel_ok && c->accel.st.wroot >= 0 && !host_nodes_nest(c)) c->nodes_rebuild = true;
     c->mtc_stale = true;
-    return upload_accel(c);
+    return RT_OK;
 }
 
 int rt_set_animated(rt_ctx* c, const int* ids, int count) {
@@ -3644,91 +3921,47 @@ int rt_set_animated(rt_ctx* c, const int* ids, int count) {
         seen[ids[i]] = 1;
     }
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    int rc = sync_host_nodes(c);
-    if (rc != RT_OK) return rc;
-    // shapes that stay animated keep the base record the accelerator was built from
-    std::vector<FlatShape> base(count);
-    for (int i = 0; i < count; ++i) {
-        base[i] = c->host_shapes[ids[i]];
-        for (size_t j = 0; j < c->anim_ids.size(); ++j)
-            if (c->anim_ids[j] == ids[i] && j < c->anim_base.size()) base[i] = c->anim_base[j];
-    }
     c->anim_ids.assign(ids, ids + count);
-    c->anim_base = base;
-    return prepare_animation(c);
+    // The refit set takes the new ids with the records the accelerator was built from
+    // (a shape rewritten since: its record before the first rewrite); shapes already in
+    // it keep their base, and shapes that stop being animated stay in it.
+    bool added = false;
+    for (int i = 0; i < count; ++i) {
+        const int id = ids[i];
+        if (c->refit_of[id] >= 0) continue;
+        FlatShape base = c->host_shapes[id];
+        if (c->upd_mark[id])
+            for (const auto& ub : c->upd_base)
+                if (ub.first == id) base = ub.second;
+        c->refit_of[id] = static_cast<int>(c->refit_ids.size());
+        c->refit_ids.push_back(id);
+        c->anim_base.push_back(base);
+        added = true;
+    }
+    return added ? prepare_animation(c) : RT_OK;
 }
 
 int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (!c || !c->have_scene || c->anim_ids.empty() || !shapes) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    int rc = RT_OK;
+    // node records the host wrote before this frame apply first, then this frame's growth
+    if (c->nodes_dirty && (rc = flush_updates(c)) != RT_OK) return rc;
     const int n = static_cast<int>(c->anim_ids.size());
-    // host side: does each shape keep its kind of bound, did its normal move
-    bool rebuild = false;
-    std::vector<int> flags(n, 0);
-    for (int i = 0; i < n; ++i) {
-        const FlatShape &s = shapes[i], &b0 = c->anim_base[i];
-        int cls = rta::UNBOUNDED;
-        if (c->accel_ok) {
-            cls = rta::classify_class(s, c->accel.origin_lim);  // classify's class, without the box
-            if (cls != c->anim_cls[i]) rebuild = true;
-        }
-        const bool cone = s.type != b0.type || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
-                                                std::memcmp(&s.planeNormal, &b0.planeNormal, sizeof(rt_vec3)) != 0);
-        flags[i] = (cls == rta::BOUNDED ? AF_BOUNDED : 0) | (cone ? AF_CONE : 0);
-    }
-    const size_t bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
-    const int slot = c->anim_slot;
-    c->anim_slot = (slot + 1) % rt_ctx::kAnimRing;
-    if (!c->anim_copied[slot]) {
-        HIP_TRY(hipEventCreateWithFlags(&c->anim_copied[slot], hipEventDisableTiming));
-    } else {
-        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // k_animate of this slot's last frame has read it
-    }
-    if (c->anim_pinned_cap[slot] < bytes) {
-        if (c->anim_pinned[slot]) hipHostFree(c->anim_pinned[slot]);
-        c->anim_pinned[slot] = nullptr;
-        c->anim_pinned_dev[slot] = nullptr;
-        c->anim_pinned_cap[slot] = 0;
-        // mapped and coherent: k_animate reads it over the host link, never a stale cached copy
-        if (hipHostMalloc(&c->anim_pinned[slot], bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
-            return RT_ERR_NO_MEMORY;
-        if (hipHostGetDevicePointer(&c->anim_pinned_dev[slot], c->anim_pinned[slot], 0) != hipSuccess)
-            return RT_ERR_DEVICE;
-        c->anim_pinned_cap[slot] = bytes;
-    }
-    char* pin = static_cast<char*>(c->anim_pinned[slot]);
-    const char* pin_dev = static_cast<const char*>(c->anim_pinned_dev[slot]);
-    std::memcpy(pin, shapes, n * sizeof(FlatShape));
-    std::memcpy(pin + n * sizeof(FlatShape), flags.data(), n * sizeof(int));
-    const bool acc = c->accel_ok;
-    const size_t P = c->accel.prim_shape.size();
-    const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat, c->nodes,
-                      acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
-                      acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
-                      acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
-                      c->accel.origin_lim, c->accel.mt ? 1 : 0};
-    // 1. the moved shapes' records and boxes, read from the pinned buffer
-    hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
-                       reinterpret_cast<const FlatShape*>(pin_dev),
-                       reinterpret_cast<const int*>(pin_dev + n * sizeof(FlatShape)), c->anim, out);
-    HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));  // the slot may be refilled after this
-    // 2. the grown reference nodes (written through to every copy) and the refit local boxes
-    const int nd = acc ? c->n_dirty : 0;
-    if (c->anim.nodes + nd > 0)
-        hipLaunchKernelGGL(k_anim_refit, dim3((c->anim.nodes + nd + 3) / 4), dim3(256), 0, c->stream, c->anim, out,
-                           c->refit_dirty, nd, c->accel.mt ? kWideRecMt : kWideRec);
-    HIP_TRY(hipGetLastError());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
-    c->brute_stale = c->mtc_stale = true;
-    c->nodes_on_device_newer = true;
-    if (!rebuild) return RT_OK;
-    ++c->anim_rebuilds;
-    return upload_accel(c);  // a bound changed kind: rebuild from the grown nodes
+    if (c->brute && !c->brute_stale)  // the brute-force context: the same records, no nodes to grow
+        for (int i = 0; i < n && !c->brute_stale; ++i)
+            if (rt_update_shapes(c->brute, c->anim_ids[i], 1, &shapes[i]) != RT_OK) c->brute_stale = true;
+    c->mtc_stale = true;
+    // the records and the growth on the device (k_animate + k_anim_refit); a host
+    // rebuild only when a bound changed kind
+    return flush_updates(c, true);
 }
 
 int rt_build_lbvh(rt_ctx* c, float* device_ms) {
     if (!c || !c->have_scene) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    if (const int rc0 = flush_updates(c)) return rc0;  // staging_shapes current
     const int S = c->S;
     const int N = S > 0 ? 2 * S - 1 : 0;
     std::vector<FlatNode> nodes(static_cast<size_t>(N));
@@ -3777,6 +4010,7 @@ int rt_read_nodes(rt_ctx* c, FlatNode* nodes, int N) {
     if (!c || !c->have_scene || N != c->N || (N > 0 && !nodes)) return RT_ERR_INVALID;
     if (N == 0) return RT_OK;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    if (const int rc = flush_updates(c)) return rc;
     HIP_TRY(hipMemcpyAsync(nodes, c->staging_nodes, N * sizeof(FlatNode), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     return RT_OK;
@@ -3988,6 +4222,7 @@ extern "C" int rt_set_tree(rt_ctx* c, int mode) {
 }
 
 extern "C" int rt_debug_anim_rebuilds(rt_ctx* c) { return c ? c->anim_rebuilds : -1; }
+extern "C" int rt_debug_refits(rt_ctx* c) { return c ? c->updates_flushed : -1; }
 
 extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
     if (!c || lane_from_depth < -1) return RT_ERR_INVALID;

@@ -896,6 +896,75 @@ int rts_bvh_stats(const rts_scene* s, int* leaves, int* max_leaf, int* depth, in
     return 0;
 }
 
+// updateBVH (src/main.cpp:1068-1077) on the serialised arrays. A node's shape set
+// is the shapes of the leaves below it; split() hands every child its parent's
+// list filtered in order, so every list is in increasing shape index, and a node
+// grows by its animated shapes in that order (growToInclude keeps the first of
+// equal values, so the order can decide the sign of a zero).
+int rts_update_bvh(const FlatShape* shapes, int S, FlatNode* nodes, int N, const int* idx, int I, const int* ids,
+                   int count) {
+    if (S < 0 || N < 0 || I < 0 || count < 0 || (S > 0 && !shapes) || (N > 0 && !nodes) || (I > 0 && !idx) ||
+        (count > 0 && !ids))
+        return -1;
+    if (N == 0 || count == 0) return 0;
+    std::vector<char> animated(static_cast<size_t>(S), 0);
+    for (int j = 0; j < count; ++j) {
+        if (ids[j] < 0 || ids[j] >= S) return -1;
+        animated[ids[j]] = 1;
+    }
+    std::vector<std::vector<int>> parents(static_cast<size_t>(N));
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = nodes[k];
+        if (nd.leftChild == -1) continue;
+        if (nd.leftChild < 0 || nd.leftChild >= N || nd.rightChild < 0 || nd.rightChild >= N) return -1;
+        parents[nd.leftChild].push_back(k);
+        if (nd.rightChild != nd.leftChild) parents[nd.rightChild].push_back(k);
+    }
+    // per shape (ascending), the nodes listing it: its leaves and every node above them
+    std::vector<std::vector<int>> leaves_of(static_cast<size_t>(S));
+    for (int k = 0; k < N; ++k) {
+        const FlatNode& nd = nodes[k];
+        if (nd.leftChild != -1 || nd.numShapes <= 0) continue;
+        if (nd.startShapeIdx < 0 || nd.startShapeIdx > I - nd.numShapes) return -1;
+        for (int j = nd.startShapeIdx; j < nd.startShapeIdx + nd.numShapes; ++j) {
+            if (idx[j] < 0 || idx[j] >= S) return -1;
+            if (animated[idx[j]]) leaves_of[idx[j]].push_back(k);
+        }
+    }
+    std::vector<int> stamp(static_cast<size_t>(N), -1), todo;
+    for (int a = 0; a < S; ++a) {
+        if (!animated[a] || leaves_of[a].empty()) continue;
+        const FlatShape& f = shapes[a];
+        Prim p;
+        p.kind = f.type;
+        p.radius = f.sphereRadius;
+        p.normal = V3(&f.planeNormal.x);
+        p.width = f.wallWidth;
+        p.height = f.wallHeight;
+        p.p0 = f.type == RT_SPHERE ? V3(&f.sphereCenter.x) : f.type == RT_WALL ? V3(&f.wallStart.x) : V3(&f.triP1.x);
+        p.p1 = V3(&f.triP2.x);
+        p.p2 = V3(&f.triP3.x);
+        todo.assign(leaves_of[a].begin(), leaves_of[a].end());
+        for (int k : todo) stamp[k] = a;
+        while (!todo.empty()) {
+            const int k = todo.back();
+            todo.pop_back();
+            Box b;
+            b.lo = V3(&nodes[k].boundsMin.x);
+            b.hi = V3(&nodes[k].boundsMax.x);
+            b.grow(p);
+            nodes[k].boundsMin = flat(b.lo);
+            nodes[k].boundsMax = flat(b.hi);
+            for (int q : parents[k])
+                if (stamp[q] != a) {
+                    stamp[q] = a;
+                    todo.push_back(q);
+                }
+        }
+    }
+    return 0;
+}
+
 int rts_generate(rts_scene* s, int config, int variant, float aspect) {
     if (!s) return -1;
     *s = rts_scene();

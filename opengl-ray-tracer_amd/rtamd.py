@@ -174,12 +174,16 @@ SCENE_SYMBOLS = {
     "rts_load_obj": (_I, [_P, C.c_char_p, _P, _P, _I]),
     "rts_parse_obj": (_I, [_P, C.c_char_p, C.c_long, _P, _P, _I]),
     "rts_write_image": (_I, [C.c_char_p, _P, _I, _I, C.c_long, _I]),
+    "rts_update_bvh": (_I, [_P, _I, _P, _I, _P, _I, _P, _I]),
 }
 
 # include/rt_host.h (librthost.so: the reference's render loop as a C++ host)
 HOST_SYMBOLS = {
     "rth_render_loop": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P]),
     "rth_render_loop_anim": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _I, _P]),
+    "rth_upload_animated": (_I, [_P, _P, _I, _P, _P, _I, _P, _I, _P, _I]),
+    "rth_render_loop_ref": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _P, _I, _P, _I, _P, _I,
+                                 _P, _I, _P]),
 }
 
 RT_SYMBOLS = {
@@ -284,15 +288,60 @@ def host_lib():
     return _host_lib
 
 
-def render_loop(ctx, cams, light, width, height, dst_ptr, pitch, frames, wait_each=True, anim=None):
-    """rth_render_loop(_anim) on ComputeShader `ctx`: `frames` frames (camera cams[i % len]),
+def update_bvh(fs, ids):
+    """updateBVH (src/main.cpp:1068-1077) on the scene's arrays in place (librtscene.so
+    rts_update_bvh): every node listing one of the shapes `ids` grows to hold its
+    current record in fs.shapes."""
+    ids = np.ascontiguousarray(ids, np.int32)
+    rc = scene_lib().rts_update_bvh(_ptr(fs.shapes), len(fs.shapes), _ptr(fs.nodes), len(fs.nodes),
+                                    _ptr(fs.indices), len(fs.indices), _ptr(ids), len(ids))
+    if rc != 0:
+        raise RTError("rts_update_bvh", rc)
+
+
+class ReferenceUpload:
+    """A host that keeps the reference's own per-frame upload of an animated scene
+    (src/main.cpp:336-346): its own copies of the shape and node arrays, moved
+    frame by frame; upload() is one rth_upload_animated (librthost.so): one
+    rt_update_shapes per animated index, updateBVH on the host's nodes, one
+    rt_update_nodes."""
+
+    def __init__(self, fs, ids):
+        self.shapes = as_records(fs.shapes, SHAPE_DTYPE).copy()
+        self.nodes = as_records(fs.nodes, NODE_DTYPE).copy()
+        self.indices = np.ascontiguousarray(fs.indices, np.int32)
+        self.ids = np.ascontiguousarray(ids, np.int32)
+
+    def upload(self, ctx, recs):
+        recs = as_records(np.asarray(recs).reshape(-1), SHAPE_DTYPE)
+        rc = host_lib().rth_upload_animated(ctx._h, _ptr(self.shapes), len(self.shapes), _ptr(self.ids), _ptr(recs),
+                                            len(self.ids), _ptr(self.nodes), len(self.nodes), _ptr(self.indices),
+                                            len(self.indices))
+        if rc != 0:
+            raise RTError("rth_upload_animated", rc)
+
+    def scene(self, fs):
+        """The scene this host has uploaded (for the oracle)."""
+        return FlatScene(self.shapes.copy(), self.nodes.copy(), self.indices, fs.camera, fs.light)
+
+
+def render_loop(ctx, cams, light, width, height, dst_ptr, pitch, frames, wait_each=True, anim=None, ref=None):
+    """rth_render_loop(_anim / _ref) on ComputeShader `ctx`: `frames` frames (camera cams[i % len]),
     each waited for (wait_each) or back to back; anim: a list of per-frame record
-    arrays of the rt_set_animated shapes, frame i animated with anim[i % len] first.
+    arrays of the animated shapes, frame i animated with anim[i % len] first -- by
+    rt_animate, or with `ref` (a ReferenceUpload) by the reference's own upload.
     Returns the host wall times in ms: one per frame, or [total] when not waiting."""
     cams = as_records(np.asarray(cams), CAMERA_DTYPE).reshape(-1)
     light = as_records(np.asarray(light), LIGHT_DTYPE).reshape(1)
     out = np.zeros(max(1, frames), np.float64)
-    if anim is not None:
+    if ref is not None:
+        recs = as_records(np.concatenate([np.asarray(f).reshape(-1) for f in anim]), SHAPE_DTYPE)
+        rc = host_lib().rth_render_loop_ref(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height),
+                                            C.c_void_p(dst_ptr), int(pitch), int(frames), int(bool(wait_each)),
+                                            _ptr(ref.shapes), len(ref.shapes), _ptr(ref.ids), len(ref.ids), _ptr(recs),
+                                            len(anim), _ptr(ref.nodes), len(ref.nodes), _ptr(ref.indices),
+                                            len(ref.indices), _ptr(out))
+    elif anim is not None:
         recs = as_records(np.concatenate([np.asarray(f).reshape(-1) for f in anim]), SHAPE_DTYPE)
         per = len(np.asarray(anim[0]).reshape(-1))
         rc = host_lib().rth_render_loop_anim(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height),
@@ -681,6 +730,14 @@ class ComputeShader:
     def debug_anim_rebuilds(self):
         """Host rebuilds rt_animate fell back to since the context was made."""
         fn = self._lib.rt_debug_anim_rebuilds
+        fn.argtypes = [_P]
+        fn.restype = _I
+        return int(fn(self._h))
+
+    def debug_refits(self):
+        """Device refits that applied rt_update_shapes / rt_update_nodes / rt_animate
+        without a host rebuild, since the context was made."""
+        fn = self._lib.rt_debug_refits
         fn.argtypes = [_P]
         fn.restype = _I
         return int(fn(self._h))

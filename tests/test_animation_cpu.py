@@ -153,3 +153,25 @@ def test_class_check_equals_classify():
                        text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "class_check ok" in r.stdout and " 0 mismatches" in r.stdout
+
+
+@pytest.mark.parametrize("depth", [0, 3, 15])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_host_update_bvh_equals_oracle(depth, seed):
+    """rts_update_bvh (librtscene.so: the updateBVH a host keeping the reference's own
+    upload runs before rt_update_nodes) grows the same boxes, bit for bit, as the
+    oracle's restatement, over moving frames."""
+    fs = _scene(seed, depth)
+    rng = np.random.default_rng(100 + seed)
+    ids = np.sort(rng.choice(len(fs.shapes), 30, replace=False)).astype(np.int32)
+    mine = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    for step in range(4):
+        fs.shapes = _move(fs.shapes, ids, rng)
+        mine.shapes = fs.shapes.copy()
+        oracle.update_bvh(fs, ids)
+        rtamd.update_bvh(mine, ids)
+        for f in ("boundsMin", "boundsMax", "leftChild", "rightChild", "startShapeIdx", "numShapes"):
+            assert np.array_equal(mine.nodes[f].view(np.uint32 if mine.nodes[f].dtype.kind == "f" else np.int32),
+                                  fs.nodes[f].view(np.uint32 if fs.nodes[f].dtype.kind == "f" else np.int32)), (step, f)
+    with pytest.raises(rtamd.RTError):
+        rtamd.update_bvh(mine, np.array([len(fs.shapes)], np.int32))

@@ -1,0 +1,233 @@
+"""The reference's own per-frame upload through the drop-in ABI (-m gpu).
+
+The reference animates by uploading: updateScene issues one glBufferSubData per
+animated shape record (src/main.cpp:981-992), updateBVH grows the node objects on
+the host (:1068-1077) and serializeBVH + one glBufferSubData re-upload the nodes
+(:336-346). Its drop-ins are rt_update_shapes (per record) and rt_update_nodes.
+The renderer applies whatever was written by the next dispatch as one device
+refit (flush_updates in rt_kernels.hip): no accelerator rebuild unless a moved
+shape changes its kind of bound or the new node boxes stop nesting. These tests
+check that every frame is the oracle's frame of the host's own scene, that the
+refit path equals a fresh upload of the same arrays bit for bit (including the
+rebuild cases and the brute-force and Moller-Trumbore branches), and that no
+rebuild happens on the published animations.
+"""
+import numpy as np
+import pytest
+import torch
+
+import bench
+import oracle
+import rtamd
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = rtamd.ComputeShader(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def fresh():
+    """A second context: every scene uploaded whole (the accelerator built from scratch)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    c = rtamd.ComputeShader(0)
+    yield c
+    c.close()
+
+
+def check(img, ref, what):
+    diff = np.abs(img.astype(np.float64) - ref.astype(np.float64))
+    bad = int((diff > TOL).any(axis=-1).sum())
+    assert np.isfinite(img).all() == np.isfinite(ref).all(), what
+    assert bad == 0, f"{what}: {bad} pixels over {TOL}, max diff {np.nanmax(diff):.3g}"
+
+
+def same(a, b, what):
+    bad = int((a.view(np.uint32) != b.view(np.uint32)).any(axis=-1).sum())
+    assert bad == 0, f"{what}: {bad} pixels differ"
+
+
+@pytest.mark.parametrize("cfg", [3, 2])
+def test_reference_upload_loop_matches_oracle(ctx, cfg):
+    """64 frames of main.cpp's loop call for call from the C++ host (librthost.so
+    rth_render_loop_ref: camera, light, one rt_update_shapes per animated record,
+    rts_update_bvh, one rt_update_nodes, dispatch, wait): config 3's four wheels turn
+    (updateWheelAnimations), config 2's three spheres bounce (bounceSphere). Every
+    frame equals the oracle's frame of the host's own scene (its records and its
+    updateBVH-grown nodes); every frame is one device refit and none a rebuild; the
+    last frame equals the same animation through rt_animate (the device's updateBVH)."""
+    W, H = (192, 108) if cfg == 3 else (160, 120)
+    mb = 3 if cfg == 3 else 1
+    fs = rtamd.generate(cfg, 0, W, H)
+    ids, frames = bench.wheel_frames(fs, 64) if cfg == 3 else bench.sphere_frames(fs, 64)
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    ru = rtamd.ReferenceUpload(fs, ids)
+    out = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+    r0, f0 = ctx.debug_anim_rebuilds(), ctx.debug_refits()
+    p = oracle.params(W, H, mb)
+    for k in range(64):
+        rtamd.render_loop(ctx, fs.camera, fs.light, W, H, out.data_ptr(), W * 16, 1, True, anim=[frames[k]], ref=ru)
+        want, _ = oracle.render(ru.scene(fs), W, H, p)
+        check(out.cpu().numpy(), want, f"config {cfg} frame {k}")
+    assert ctx.debug_anim_rebuilds() == r0, "the published animation rebuilt the accelerator"
+    assert ctx.debug_refits() - f0 == 64
+    assert ctx.accel_info()["scene_tree"] == 1
+    last = out.cpu().numpy()
+    # the same frames through rt_animate (the node growth on the device)
+    ctx.upload(fs)
+    ctx.set_animated(ids)
+    for k in range(64):
+        ctx.animate(frames[k])
+    got = ctx.read_nodes(len(fs.nodes))
+    for f in ("boundsMin", "boundsMax"):
+        assert np.array_equal(got[f].view(np.uint32), ru.nodes[f].view(np.uint32)), f
+    same(ctx.render(W, H), last, "rt_animate against the reference's upload")
+
+
+def _soup(seed, n_tri=1500):
+    rng = np.random.default_rng(seed)
+    sc = rtamd.Scene()
+    for i in range(n_tri):
+        c = rng.uniform(-20, 20, 3)
+        c[1] = rng.uniform(-4, 4)
+        v = c + rng.normal(size=(3, 3)) * rng.uniform(0.3, 2.0)
+        sc.add_triangle(v[0], v[1], v[2], invert=bool(i % 2),
+                        mat=rtamd.material(color=rng.uniform(0, 1, 3), specular=0.3 if i % 5 == 0 else 0.0))
+    for _ in range(30):
+        sc.add_sphere(rng.uniform(-20, 20, 3), rng.uniform(0.3, 2.5), mat=rtamd.material(color=rng.uniform(0, 1, 3)))
+    sc.add_wall((-10, -10, -25), 20, 15, (0.1, 0.2, 1.0), mat=rtamd.material(specular=0.8))
+    sc.add_plane((0, 0, 1), (0, 0, -40), mat=rtamd.material(color=(0.2, 0.5, 0.2), specular=0.0))
+    sc.set_camera((5, -25, 45), 60, 4 / 3)
+    sc.LookAt((0, 0, 0))
+    sc.set_light((10, -30, 20), (1, 1, 1), 40)
+    sc.buildBVH(6)
+    return sc.serializeScene()
+
+
+def _moved(shapes, ids, rng, k):
+    s = shapes.copy()
+    for i in ids:
+        t = s["type"][i]
+        d = (rng.normal(size=3) * 0.8).astype(np.float32)
+        if t == 0:
+            s["sphereCenter"][i] += d
+        elif t == 2:
+            s["wallStart"][i] += d
+        elif t == 3:
+            c = (s["triP1"][i].astype(np.float64) + s["triP2"][i] + s["triP3"][i]) / 3
+            a = 0.2 * (k + 1)
+            for f in ("triP1", "triP2", "triP3"):
+                q = s[f][i].astype(np.float64) - c
+                q = np.array([q[0] * np.cos(a) - q[2] * np.sin(a), q[1], q[0] * np.sin(a) + q[2] * np.cos(a)])
+                s[f][i] = (q + c + d).astype(np.float32)
+    return s
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_update_path_equals_fresh_upload(ctx, fresh, seed):
+    """rt_update_shapes (single records and ranges) + rt_update_nodes, refit on the
+    device, against the same arrays uploaded whole, bit for bit, for the BVH branch
+    (barycentric and Moller-Trumbore) and the brute-force branch: moves the refit
+    absorbs, a triangle collapsing to a sliver and node boxes that stop nesting
+    (host rebuilds), node boxes alone, and shapes moved without a node update (the
+    reference's frame then keeps the old boxes)."""
+    W, H = 200, 150
+    fs = _soup(seed)
+    rng = np.random.default_rng(seed)
+    tri = np.where(fs.shapes["type"] == 3)[0]
+    ids = np.sort(np.concatenate([rng.choice(tri, 60, replace=False), np.where(fs.shapes["type"] == 0)[0][:6],
+                                  np.where(fs.shapes["type"] == 2)[0]])).astype(np.int32)
+    host = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    ctx.upload(fs)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    fresh.set_kernel(rtamd.KERNEL_AUTO)
+
+    def frames(what):
+        fresh.upload(host)
+        for bvh, mt in ((True, False), (True, True), (False, False)):
+            for c in (ctx, fresh):
+                c.set_params(W, H, 3, bvh, False, mt)
+            same(ctx.render(W, H), fresh.render(W, H), f"{what} bvh {bvh} mt {mt}")
+        ctx.set_params(W, H, 3, True)
+
+    frames("as uploaded")
+    r0 = ctx.debug_anim_rebuilds()
+    for k in range(3):  # the refit absorbs these
+        host.shapes = _moved(host.shapes, ids, rng, k)
+        lo = int(ids[0])
+        ctx.update_shapes(lo, host.shapes[lo:lo + 1])
+        for j in ids[1:]:
+            ctx.update_shapes(int(j), host.shapes[j:j + 1])
+        ctx.update_shapes(int(tri[5]), host.shapes[tri[5]:tri[5] + 3])  # a range, partly unmoved
+        rtamd.update_bvh(host, ids)
+        ctx.update_nodes(host.nodes)
+        frames(f"step {k}")
+    assert ctx.debug_anim_rebuilds() == r0
+    # a moved triangle collapses to a sliver: no conservative bound, a host rebuild
+    t = int(ids[np.isin(ids, tri)][0])
+    host.shapes["triP3"][t] = host.shapes["triP1"][t] + (host.shapes["triP2"][t] - host.shapes["triP1"][t]) * 0.5
+    ctx.update_shapes(t, host.shapes[t:t + 1])
+    rtamd.update_bvh(host, np.array([t], np.int32))
+    ctx.update_nodes(host.nodes)
+    frames("sliver")
+    assert ctx.debug_anim_rebuilds() == r0 + 1
+    # node boxes alone, grown (still nested): a refit
+    host.nodes["boundsMin"] -= np.float32(0.75)
+    host.nodes["boundsMax"] += np.float32(0.75)
+    ctx.update_nodes(host.nodes)
+    frames("nodes grown")
+    assert ctx.debug_anim_rebuilds() == r0 + 1
+    # a leaf box that no longer lies in its parent's: the scene tree cannot hold, a rebuild
+    leaf = int(np.where(host.nodes["leftChild"] == -1)[0][0])
+    host.nodes["boundsMax"][leaf] += np.float32(50.0)
+    ctx.update_nodes(host.nodes)
+    frames("not nested")
+    assert ctx.debug_anim_rebuilds() == r0 + 2
+    # shapes moved with no node update: the old boxes decide which leaves are tested
+    host.shapes = _moved(host.shapes, ids[:20], rng, 5)
+    for j in ids[:20]:
+        ctx.update_shapes(int(j), host.shapes[j:j + 1])
+    frames("shapes only")
+    p = oracle.params(W, H, 3)
+    want, _ = oracle.render(host, W, H, p)
+    check(ctx.render(W, H), want, "shapes only vs oracle")
+
+
+def test_update_then_animate_and_readback(ctx):
+    """rt_update_nodes followed by rt_animate in the same frame: the host's boxes
+    apply first, then the device grows them (rt_read_nodes = updateBVH over the
+    host's boxes); rt_update_shapes of shapes outside the animated set in between."""
+    W, H = 160, 120
+    fs = rtamd.generate(2, 0, W, H)
+    ids, frames = bench.sphere_frames(fs, 4)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 1, True)
+    ctx.set_animated(ids)
+    host = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    other = np.int32(len(fs.shapes) - 1)
+    for k in range(4):
+        host.nodes["boundsMax"][-1] += np.float32(0.5)
+        ctx.update_nodes(host.nodes)
+        moved = host.shapes[other:other + 1].copy()
+        moved["material"]["color"] = np.float32([0.1 * k, 0.5, 0.9])
+        host.shapes[other] = moved[0]
+        ctx.update_shapes(int(other), moved)
+        ctx.animate(frames[k])
+        host.shapes[ids] = frames[k]
+        rtamd.update_bvh(host, ids)
+        got = ctx.read_nodes(len(host.nodes))
+        for f in ("boundsMin", "boundsMax"):
+            assert np.array_equal(got[f].view(np.uint32), host.nodes[f].view(np.uint32)), (k, f)
+        want, _ = oracle.render(host, W, H, oracle.params(W, H, 1))
+        check(ctx.render(W, H), want, f"frame {k}")
