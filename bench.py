@@ -98,6 +98,11 @@ def parse(argv=None):
                          "reference = the reference's own calls (src/main.cpp:336-346): one rt_update_shapes per "
                          "animated record, updateBVH on the host (rts_update_bvh), one rt_update_nodes "
                          "(librthost.so rth_upload_animated), applied by the renderer as a device refit")
+    ap.add_argument("--camera-path", default="static", choices=["static", "orbit", "dolly"],
+                    help="the camera per frame: static (the config's camera); orbit = 0.5 deg per frame about "
+                         "the look-at point (Camera::LookAt after each step); dolly = Camera::ProcessKeyboard "
+                         "FORWARD at the reference's SPEED (15 units/s, 1/60 s per frame), 96 frames in, 96 back "
+                         "(src/camera.hpp:75-90, src/main.cpp:509-534)")
     ap.add_argument("--inflight", type=int, default=0,
                     help="frames in flight per GPU; 0 = auto: 3 below 64k 8x8 tiles (1080p), 2 above (4K), up "
                          "to 4 while the GPU's share of a frame has fewer than 16k tiles; strong mode over "
@@ -295,6 +300,27 @@ def sphere_frames(fs, n):
             rec["sphereCenter"][k][1] = base["sphereCenter"][k][1] + np.float32(amp) * np.sin(np.float32(fr) * t)
         frames.append(rec)
     return ids, frames
+
+
+def camera_path(rtamd, sc, fs, kind, target):
+    """The per-frame cameras of --camera-path (FlatCamera records, dealt as cams[i % n])."""
+    import numpy as np
+    if kind == "static":
+        return np.ascontiguousarray(fs.camera).reshape(1)
+    cams = []
+    if kind == "orbit":  # 720 frames, 0.5 degrees each: one full turn
+        for _ in range(720):
+            sc.orbit(target, 0.5)
+            cams.append(sc.camera().copy())
+        sc.orbit(target, -360.0)
+    else:  # Camera::ProcessKeyboard(FORWARD / BACKWARD, 1/60): Position +-= Front * (SPEED * dt), in float
+        c = np.ascontiguousarray(fs.camera).reshape(1).copy()
+        v = np.float32(15.0) * np.float32(1.0 / 60.0)
+        for k in range(192):
+            cams.append(c.copy())
+            step = c["Front"][0] * v
+            c["Position"][0] = c["Position"][0] + step if k < 96 else c["Position"][0] - step
+    return np.ascontiguousarray(np.concatenate(cams)).astype(rtamd.CAMERA_DTYPE)
 
 
 def animated_oracle_scene(fs, ids, frames, applied):
@@ -513,6 +539,8 @@ def main():
     rays_step, b_ref_rank, rows = count_work()
 
     cam, light = fs.camera, fs.light
+    cams = camera_path(rtamd, sc, fs, a.camera_path, target)  # cams[i % len(cams)] for frame i
+    last_cam = [None for _ in range(max(F, 1))]  # per renderer: the camera of its last frame
     anim = None
     if a.animate:
         if use_group or a.config not in (2, 3, 4):
@@ -531,14 +559,15 @@ def main():
 
     def frame(i, inflight):
         if use_group:
-            grp.set_camera(cam)    # SSBO 2 (src/main.cpp:328-330)
+            grp.set_camera(cams[i % len(cams)])    # SSBO 2 (src/main.cpp:328-330)
             grp.set_light(light)   # SSBO 1 (:332-334)
             grp.dispatch(W, H, a.stripe)  # this rank's stripes + send/recv to rank 0 + unstripe there
             if inflight == 1:
                 group_sync()  # one frame at a time: the frame slots would otherwise overlap
             return
         c_ = ctxs[i % inflight]
-        c_.set_camera(cam)
+        c_.set_camera(cams[i % len(cams)])
+        last_cam[i % inflight] = i % len(cams)
         c_.set_light(light)
         if ref_up is not None:  # updateScene + updateBVH + their uploads, as the reference makes them
             ref_up[i % inflight].upload(c_, anim[1][i % len(anim[1])])
@@ -704,7 +733,8 @@ def main():
             c_.set_latency_mode(1)
         frames_anim = anim[1] if anim is not None else None
         for n_ in (wait_warmup, a.steps):
-            ms_ = rtamd.render_loop(ctx, cam, light, W, H, bufs[0].data_ptr(), W * 16, n_, True, anim=frames_anim,
+            last_cam[0] = (n_ - 1) % len(cams)
+            ms_ = rtamd.render_loop(ctx, cams, light, W, H, bufs[0].data_ptr(), W * 16, n_, True, anim=frames_anim,
                                     ref=ref_up[0] if ref_up is not None else None)
             if anim is not None:  # the C++ loop animates ctx 0 with frames 0, 1, ... (oracle bookkeeping)
                 applied[0].extend(i % len(frames_anim) for i in range(n_))
@@ -762,6 +792,8 @@ def main():
                       if use_group else f"torch.distributed.gather ({a.backend}) + index_copy_ unpermute")
         suffix = "".join(f"_{n}" for n, on in (("brute", a.brute), ("mt", a.mt), ("fresnel", a.fresnel),
                                                   ("variant", a.variant), ("animate", a.animate)) if on)
+        if a.camera_path != "static":
+            suffix += "_" + a.camera_path
         refits = {"rebuilds": [c_.debug_anim_rebuilds() for c_ in ctxs], "refits": [c_.debug_refits() for c_ in ctxs]}
         # strong lines: the same kernel over this rank's rows; the single-GPU entry with its
         # issue floors scaled by the row share (roofline docstring)
@@ -838,18 +870,27 @@ def main():
                                                (not a.brute, a.fresnel, a.mt))
             out["cpu_baseline"]["reference_cpu_path"] = cpu_reference_1core(rtamd, a.cpu_seconds / 2, cfg, a.variant,
                                                                             W, H)
-        if mode == "frames" and anim is not None:
+        moving = len(cams) > 1
+        if moving:
+            out["camera_path"] = {"kind": a.camera_path, "cameras": len(cams),
+                                  "last_camera_per_renderer": [x for x in last_cam if x is not None]}
+        if mode == "frames" and (anim is not None or moving):
             # every renderer's last timed frame against the oracle rendering that
-            # renderer's scene: the last animated records and the boxes grown by every
-            # frame it was given (outside the timed region; whole frames)
+            # renderer's scene: its last frame's camera, and when animated its last
+            # records and the boxes grown by every frame it was given (outside the timed
+            # region; whole frames)
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle  # noqa: E402  (checker only)
             torch.cuda.synchronize()
             checks, host_nodes_ok = [], True
             for k, b_ in enumerate(bufs):
-                if not applied[k]:
+                if anim is not None and not applied[k]:
                     continue
-                fk = animated_oracle_scene(fs, anim[0], anim[1], applied[k])
+                if last_cam[k] is None:
+                    continue
+                fk = (animated_oracle_scene(fs, anim[0], anim[1], applied[k]) if anim is not None else
+                      rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light))
+                fk.camera = cams[last_cam[k]:last_cam[k] + 1].copy()
                 if ref_up is not None:  # the host's own updateBVH (rts_update_bvh) grew the same boxes
                     host_nodes_ok = host_nodes_ok and all(
                         np.array_equal(ref_up[k].nodes[f].view(np.uint32), fk.nodes[f].view(np.uint32))
@@ -859,13 +900,14 @@ def main():
             out["parity"] = {"max_abs": max(c["max_abs"] for c in checks),
                              "bad_pixels": sum(c["bad_pixels"] for c in checks), "frames_checked": len(checks),
                              "tol": PARITY_TOL, "rows_checked": [0, H],
-                             "against": ("oracle/rt_oracle.c (GLSL restated) on each renderer's animated scene: "
-                                         "its last frame's records, node boxes grown by oracle.update_bvh "
-                                         "(updateBVH restated) over every frame it was given"),
-                             "animation_frames_applied": [len(x) for x in applied],
+                             "against": ("oracle/rt_oracle.c (GLSL restated) on each renderer's last frame: its "
+                                         "camera" + (", its last records, node boxes grown by oracle.update_bvh "
+                                                     "(updateBVH restated) over every frame it was given"
+                                                     if anim is not None else "")),
+                             "animation_frames_applied": [len(x) for x in applied] if anim is not None else None,
                              "host_nodes_equal_oracle": host_nodes_ok if ref_up is not None else None,
                              "ok": all(c["ok"] for c in checks) and host_nodes_ok}
-        if mode == "frames" and anim is None:
+        if mode == "frames" and anim is None and not moving:
             # the timed frames themselves, against the oracle (outside the timed region)
             if out["cpu_baseline"] is not None:
                 ry0, ref = cpu_baseline.last_image

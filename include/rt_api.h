@@ -104,10 +104,25 @@ int rt_set_stream(struct rt_ctx* ctx, void* hip_stream);
 int rt_upload_scene(struct rt_ctx* ctx, const FlatShape* shapes, int num_shapes,
                     const FlatNode* nodes, int num_nodes, const int* indices, int num_indices);
 
-/* Partial re-upload of shapes [first, first+count) (src/main.cpp:981-992, updateScene). */
+/* Partial re-upload of shapes [first, first+count) (glBufferSubData in updateScene,
+ * src/main.cpp:981-992). Node boxes are not touched (the reference's are not either,
+ * until it re-uploads them). The host array may be reused when the call returns. */
 int rt_update_shapes(struct rt_ctx* ctx, int first, int count, const FlatShape* shapes);
 
-/* Re-upload of all nodes with the same topology (src/main.cpp:340-345, updateBVH). */
+/* Re-upload of all nodes with the same topology (src/main.cpp:340-345, after
+ * updateBVH + serializeBVH); RT_ERR_BVH if the topology differs.
+ *
+ * Both calls only write the context's host copies and return; the next operation
+ * that reads the device scene (a dispatch, rt_collect_stats, rt_read_nodes,
+ * rt_build_lbvh, rt_animate) applies everything written since as ONE device refit
+ * on the context's stream: the moved shapes' records, the boxes of the accelerator
+ * above them, and every copy of the node boxes. So the reference's loop -- one
+ * rt_update_shapes per animated record, then one rt_update_nodes -- costs one small
+ * kernel per frame, not one rebuild per call. The accelerator is rebuilt on the host
+ * only when a moved shape's kind of bound changed (the frame is exact before that
+ * too: the refit enters every box above it) or the new node boxes no longer nest
+ * (the scene tree's condition, rt_set_tree). rt_debug_refits / rt_debug_anim_rebuilds
+ * count the two outcomes. */
 int rt_update_nodes(struct rt_ctx* ctx, const FlatNode* nodes, int num_nodes);
 
 /* Device-side animation. Replaces the reference's
@@ -123,12 +138,13 @@ int rt_update_nodes(struct rt_ctx* ctx, const FlatNode* nodes, int num_nodes);
  * device it then grows every node whose shape set lists an animated shape to
  * include the shape, exactly as updateBVH does. That means the leaf and every
  * node above it, growToInclude (src/BoundingBox.hpp:44-95), grow-only.
- * The accelerator's conservative boxes grow along with the node boxes.
- * A moved shape whose kind of bound changes triggers a host rebuild of the
- * accelerator. Examples: a triangle that becomes too thin to bound, or a
- * sphere whose radius becomes infinite. The frame is identical either way.
- * The host array may be reused when the call returns. RT_ERR_INVALID if no
- * set is marked.
+ * The accelerator's conservative boxes are refit along with the node boxes, in
+ * one kernel launch per call (with any rt_update_shapes / rt_update_nodes pending).
+ * A moved shape whose kind of bound changes (a triangle that becomes too thin to
+ * bound, a sphere whose radius becomes infinite) is entered through every box
+ * above it until the host rebuilds the accelerator, which the refit requests.
+ * The frame is identical either way. The host array may be reused when the call
+ * returns. RT_ERR_INVALID if no set is marked.
  *
  * rt_read_nodes copies the current node records to the host, including the
  * boxes rt_animate grew. num_nodes must match the scene's node count. */
@@ -279,9 +295,11 @@ int rt_read_indices(struct rt_ctx* ctx, int* indices, int num_indices);
  * reference tree's child boxes nest in their parents' boxes, rays whose slab
  * values cannot be NaN walk one SAH tree over all reference leaves' shapes,
  * testing each leaf's own exact box before its shapes (the nesting makes that
- * test equivalent to the reference's walk down to the leaf); other rays, and
- * animated scenes (rt_set_animated), walk the reference tree. RT_TREE_REFERENCE:
- * every ray walks the reference tree. Same image either way. */
+ * test equivalent to the reference's walk down to the leaf); other rays walk the
+ * reference tree. Animated and updated scenes keep the scene tree: the refit
+ * (rt_animate, rt_update_shapes / rt_update_nodes) refits its boxes and items,
+ * and node boxes that stop nesting rebuild the accelerator without it.
+ * RT_TREE_REFERENCE: every ray walks the reference tree. Same image either way. */
 enum rt_tree { RT_TREE_REFERENCE = 0, RT_TREE_SCENE = 1 };
 int rt_set_tree(struct rt_ctx* ctx, int mode);
 

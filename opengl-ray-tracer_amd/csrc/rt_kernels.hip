@@ -2026,12 +2026,15 @@ struct AnimMaps {
     const int *ids, *slot_off, *slot_list, *prim_off, *prim_list, *wpos_off, *wpos_list;
     const int *node_ids, *node_off, *node_list;
     const int *wn_off, *wn_list, *item_off, *item_list;
+    const int* ecls;       // per entry: its class when the accelerator was built (accel_bound.h)
+    const int* prim_entry; // per accelerator prim: its shape's refit entry, -1 if none
+    const float4* enorm;   // per entry: that record's stored normal (xyz) and type (w, int bits)
     int count, nodes;
 };
-// per-frame flags of a refit entry: conservative box valid; normal moved; the nodes
-// listing it grow to hold it (rt_animate: updateBVH on the device; rt_update_shapes
-// leaves the node boxes to rt_update_nodes, as glBufferSubData of the shapes does)
-enum { AF_BOUNDED = 1, AF_CONE = 2, AF_GROW = 4 };
+// the per-frame flag of a refit entry: the nodes listing it grow to hold it
+// (rt_animate: updateBVH on the device; rt_update_shapes leaves the node boxes to
+// rt_update_nodes, as a glBufferSubData of the shape records does)
+enum { AF_GROW = 4 };
 
 struct AnimOut {
     FlatShape* shapes;  // staging copy of the full shape array
@@ -2040,24 +2043,67 @@ struct AnimOut {
     float4* packed;                   // the packed node copies (k_pack_nodes layout)
     float4 *anodes, *lnodes, *prims;  // accelerator (null when off)
     float4 *wnodes, *titems;          // accelerator: per-parent child boxes, scene-tree items' exact boxes
-    float4* pbox;                     // conservative box per prim (lo, hi), for k_anim_refit
+    float4* pbox;                     // conservative box per prim (lo, hi), for the slot refit
     const int* prim_seq;
-    float4* sbox;                     // per animated shape: reference box, conservative box (4 float4)
+    float4* sbox;                     // per entry: reference box, conservative box (4 float4)
     float origin_lim;
     int mt;                           // the accelerator's wide nodes: kWideRecMt float cones, else kWideRec
 };
 
-// One thread per animated shape: rewrites its records and derives its two
-// boxes (the reference's growToInclude box and the accelerator's conservative
-// one); k_anim_refit then grows the nodes listing it. `fresh` and `flags` are read
-// straight from the host's pinned (mapped, coherent) buffer: no copy engine
-// transfer and no wait for one ahead of the kernel.
-__global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __restrict__ flags, AnimMaps m,
-                          AnimOut o) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One refit launch (k_refit) of flush_updates: what it reads from the pinned ring
+// and how its workgroups split the work.
+struct RefitArgs {
+    const FlatShape* fresh;    // per entry: its current record (pinned, mapped)
+    const int* flags;          // per entry: AF_GROW (pinned)
+    const FlatNode* nsrc;      // rt_update_nodes: the host's node records (pinned), or null
+    int* report;               // pinned: set to 1 when an entry's bound changed kind
+    unsigned* ctr;             // [0] workgroup tickets, [1] finished record workgroups
+    unsigned tbase, abase;     // their values before this launch
+    int na, nd, nb;            // workgroups of the record, node-set and node roles
+    const int4* dirty;         // slot refit work list (n_dirty entries after the nb node waves)
+    int n_dirty, rec;          // its length; the wide record size (kWideRec / kWideRecMt)
+    const int* titem_ref;      // per scene-tree item: its reference leaf
+    int n_items, N;
+    int wait;                  // node / slot roles wait for the record role (one launch, rt_debug_refit 0)
+    int direct;                // node / slot roles derive the entries' boxes from `fresh` themselves
+};
+
+__device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
+    for (int off = 32; off > 0; off >>= 1)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
+            hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
+        }
+}
+
+// Record role, one lane per refit entry: rewrites its records and derives its two
+// boxes (the reference's growToInclude box when it grows the nodes, and the
+// accelerator's conservative one) for the node and slot roles. The class of the
+// bound is decided here, on the device: a shape whose bound changed kind since the
+// build (a triangle collapsing to a sliver, a sphere going infinite) gets an
+// infinite conservative box, so every box above it is entered and it is tested like
+// an always-tested shape -- the frame stays exact -- and `report` asks the host to
+// rebuild the accelerator for speed. A moved stored normal drops the back-face
+// cones above the shape (they were built from the old normals).
+// The conservative box an entry's current record contributes to the boxes above it
+// (b): its classify() box; empty if it was always tested since the build (no box
+// above it); infinite if its bound changed kind since (every box above it then
+// entered). Returns whether the kind changed.
+__device__ bool entry_cbox(const AnimOut& o, const FlatShape& s, int was, rta::Box3& b) {
+    const int cls = rta::classify(s, b, o.origin_lim, o.mt != 0);
+    const bool changed = cls != was;
+    if (was != rta::BOUNDED || cls != rta::BOUNDED)
+        for (int a = 0; a < 3; ++a) {
+            b.lo[a] = was != rta::BOUNDED ? INFINITY : -INFINITY;
+            b.hi[a] = was != rta::BOUNDED ? -INFINITY : INFINITY;
+        }
+    return changed;
+}
+
+__device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int i) {
     if (i >= m.count) return;
-    const FlatShape s = fresh[i];
-    const int id = m.ids[i], fl = flags[i];
+    const FlatShape s = r.fresh[i];
+    const int id = m.ids[i], fl = r.flags[i];
     o.shapes[id] = s;
     const GeoRec g = pack_geo(s, id);
     store_geo(o.geo_lin + 5 * static_cast<size_t>(id), g);
@@ -2068,14 +2114,22 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
     float4* sb = o.sbox + 4 * static_cast<size_t>(i);
     sb[0] = make_float4(lo[0], lo[1], lo[2], 0.f);
     sb[1] = make_float4(hi[0], hi[1], hi[2], 0.f);
-    sb[2] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);  // no conservative box unless bounded
-    sb[3] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
-    if (!o.anodes) return;
+    if (!o.anodes) {
+        sb[2] = make_float4(INFINITY, INFINITY, INFINITY, 0.f);
+        sb[3] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
+        return;
+    }
     for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {
         const int p = m.prim_list[q];
         store_prim(o.prims, p, pack_prim(g, o.prim_seq[p]));  // rank in the reference walk (k_pack_prims)
     }
-    if (fl & AF_CONE)
+    const float4 bn = m.enorm[i];
+    const int btype = __float_as_int(bn.w);
+    const bool cone = s.type != btype || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
+                                          (__float_as_int(s.planeNormal.x) != __float_as_int(bn.x) ||
+                                           __float_as_int(s.planeNormal.y) != __float_as_int(bn.y) ||
+                                           __float_as_int(s.planeNormal.z) != __float_as_int(bn.z)));
+    if (cone)
         for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
             const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
             if (o.mt)
@@ -2083,41 +2137,47 @@ __global__ void k_animate(const FlatShape* __restrict__ fresh, const int* __rest
             else  // never cull
                 reinterpret_cast<int*>(o.lnodes + kWideRec * static_cast<size_t>(w) + 6)[sl] = rta::kConeNever;
         }
-    if (!(fl & AF_BOUNDED)) return;
     rta::Box3 b;
-    if (rta::classify(s, b, o.origin_lim) != rta::BOUNDED) return;  // the host checked the class
+    const int was = m.ecls[i];
+    if (entry_cbox(o, s, was, b)) *r.report = 1;  // the host rebuilds at its next flush
     sb[2] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
     sb[3] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
-    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {  // the prim's box for k_anim_refit
+    if (was != rta::BOUNDED) return;  // always tested since the build: no box above it
+    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {  // the prim's box for the slot refit
         float4* pb = o.pbox + 2 * static_cast<size_t>(m.prim_list[q]);
         pb[0] = sb[2];
         pb[1] = sb[3];
     }
 }
 
-__device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
-    for (int off = 32; off > 0; off >>= 1)
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
-            hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
-        }
-}
-
-// One wave per reference node listing an animated shape: the union of their
-// boxes (lanes stride the list, then a wave reduction), then one grow of the
-// node's box - updateBVH's growToInclude of each listed shape - and of its
-// content box. A single writer per node: no atomics, and the min/max result is
-// the same in any order (no stored value is NaN; a NaN coordinate adds nothing).
-// The same lane then writes the grown box through to every copy the kernels
-// read: the packed node, the accelerator's exact box, its parent's child copy
-// (wnodes: exact + content box) and the scene-tree items gated by it. Nodes that
-// list no animated shape never change, so no other copy needs refreshing.
-__device__ void grow_node(const AnimMaps& m, const AnimOut& o, int j, int lane) {
+// Node role, one wave per reference node listing a refit entry: the union of the
+// entries' boxes (lanes stride the list, then a wave reduction), then one grow of
+// the node's box - updateBVH's growToInclude of each listed shape, entries with
+// AF_GROW only - and of its content box. A single writer per node: no atomics,
+// and the min/max result is the same in any order (no stored value is NaN; a NaN
+// coordinate adds nothing). The same lane writes the grown box through to every
+// copy the kernels read: the packed node, the accelerator's exact box, its
+// parent's child copy (wnodes: exact + content box) and the scene-tree items gated
+// by it. Nodes listing no entry never change, so no other copy needs refreshing.
+__device__ void grow_node(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, int lane) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int q = m.node_off[j] + lane; q < m.node_off[j + 1]; q += 64) {
-        const float4* sb = o.sbox + 4 * static_cast<size_t>(m.node_list[q]);
-        const float4 a = sb[0], b = sb[1], c = sb[2], d = sb[3];
+        const int i = m.node_list[q];
+        float4 a, b, c, d;
+        if (r.direct) {  // from the record itself (no wait for the record role)
+            const FlatShape s = r.fresh[i];
+            float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+            if (r.flags[i] & AF_GROW) reference_box(s, rl, rh);
+            rta::Box3 cb;
+            if (o.anodes) entry_cbox(o, s, m.ecls[i], cb);
+            else cb = rta::Box3{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+            a = make_float4(rl[0], rl[1], rl[2], 0.f), b = make_float4(rh[0], rh[1], rh[2], 0.f);
+            c = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], 0.f), d = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
+        } else {
+            const float4* sb = o.sbox + 4 * static_cast<size_t>(i);
+            a = sb[0], b = sb[1], c = sb[2], d = sb[3];
+        }
         lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
         hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
         clo[0] = fminf(clo[0], c.x), clo[1] = fminf(clo[1], c.y), clo[2] = fminf(clo[2], c.z);
@@ -2128,17 +2188,17 @@ __device__ void grow_node(const AnimMaps& m, const AnimOut& o, int j, int lane) 
     if (lane != 0) return;
     const int k = m.node_ids[j];
     FlatNode& nd = o.nodes[k];
-    float* mn = &nd.boundsMin.x;
-    float* mx = &nd.boundsMax.x;
-    // Only entries with AF_GROW contribute to lo/hi (k_animate); a node none of them
-    // moves keeps every copy of its exact box as it is.
+    float mn[3] = {nd.boundsMin.x, nd.boundsMin.y, nd.boundsMin.z};
+    float mx[3] = {nd.boundsMax.x, nd.boundsMax.y, nd.boundsMax.z};
     bool grew = false;
     for (int a = 0; a < 3; ++a) {  // glm::min(Min, p) = (p < Min) ? p : Min (BoundingBox.hpp:46)
         grew = grew || lo[a] < mn[a] || mx[a] < hi[a];
         mn[a] = lo[a] < mn[a] ? lo[a] : mn[a];
         mx[a] = mx[a] < hi[a] ? hi[a] : mx[a];
     }
-    if (grew) {
+    if (grew) {  // only then: the node-set role may be writing this record in the same launch
+        nd.boundsMin = rt_vec3{mn[0], mn[1], mn[2]};
+        nd.boundsMax = rt_vec3{mx[0], mx[1], mx[2]};
         const bool leaf = nd.leftChild == -1;
         const int ca = leaf ? -(nd.startShapeIdx + 1) : nd.leftChild, cb = leaf ? nd.numShapes : nd.rightChild;
         o.packed[2 * static_cast<size_t>(k)] = make_float4(mn[0], mn[1], mn[2], __int_as_float(ca));
@@ -2173,56 +2233,62 @@ __device__ void grow_node(const AnimMaps& m, const AnimOut& o, int j, int lane) 
     }
 }
 
-// rt_update_nodes, applied at the next device operation (flush_updates): the host's
-// node records (same topology) written to every copy the kernels read, from the
-// pinned staging buffer. Threads [0, N): node k's record, packed copy and
-// accelerator exact box, and for an inner node its children's exact boxes in its
-// wnodes record; threads [N, N + n_items): one scene-tree item's gating box (its
+// Node-set role (rt_update_nodes), one lane per node or scene-tree item: the host's
+// node records (same topology) to every copy the kernels read. k < N: node k's
+// record, packed copy and accelerator exact box, and for an inner node its
+// children's exact boxes in its wnodes record; k >= N: item k - N's gating box (its
 // reference leaf's). Content boxes, cones and codes are the shapes' and stay.
-__global__ void k_set_nodes(const FlatNode* __restrict__ src, int N, FlatNode* __restrict__ staging,
-                            float4* __restrict__ packed, float4* __restrict__ anodes, float4* __restrict__ wnodes,
-                            float4* __restrict__ titems, const int* __restrict__ titem_ref, int n_items) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < N) {
+__device__ void set_node(const AnimOut& o, const RefitArgs& r, int k) {
+    const FlatNode* __restrict__ src = r.nsrc;
+    if (k < r.N) {
         const FlatNode n = src[k];
-        staging[k] = n;
+        o.nodes[k] = n;
         const bool leaf = n.leftChild == -1;
         const int ca = leaf ? -(n.startShapeIdx + 1) : n.leftChild, cb = leaf ? n.numShapes : n.rightChild;
-        packed[2 * static_cast<size_t>(k)] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, __int_as_float(ca));
-        packed[2 * static_cast<size_t>(k) + 1] =
+        o.packed[2 * static_cast<size_t>(k)] =
+            make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, __int_as_float(ca));
+        o.packed[2 * static_cast<size_t>(k) + 1] =
             make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, __int_as_float(cb));
-        if (!anodes) return;
-        float* a = reinterpret_cast<float*>(anodes + 4 * static_cast<size_t>(k));
+        if (!o.anodes) return;
+        float* a = reinterpret_cast<float*>(o.anodes + 4 * static_cast<size_t>(k));
         a[0] = n.boundsMin.x, a[1] = n.boundsMin.y, a[2] = n.boundsMin.z;
         a[4] = n.boundsMax.x, a[5] = n.boundsMax.y, a[6] = n.boundsMax.z;
         if (leaf) return;
         const int ch[2] = {n.leftChild, n.rightChild};
         for (int s = 0; s < 2; ++s) {
             const FlatNode& cn = src[ch[s]];
-            float* q = reinterpret_cast<float*>(wnodes + 8 * static_cast<size_t>(k) + 4 * s);
+            float* q = reinterpret_cast<float*>(o.wnodes + 8 * static_cast<size_t>(k) + 4 * s);
             q[0] = cn.boundsMin.x, q[1] = cn.boundsMin.y, q[2] = cn.boundsMin.z;
             q[4] = cn.boundsMax.x, q[5] = cn.boundsMax.y, q[6] = cn.boundsMax.z;
         }
-    } else if (k - N < n_items && titems) {
-        const int i = k - N;
-        const FlatNode& ln = src[titem_ref[i]];
-        float* t = reinterpret_cast<float*>(titems + 2 * static_cast<size_t>(i));
+    } else if (k - r.N < r.n_items && o.titems) {
+        const int i = k - r.N;
+        const FlatNode& ln = src[r.titem_ref[i]];
+        float* t = reinterpret_cast<float*>(o.titems + 2 * static_cast<size_t>(i));
         t[0] = ln.boundsMin.x, t[1] = ln.boundsMin.y, t[2] = ln.boundsMin.z;
         t[4] = ln.boundsMax.x, t[5] = ln.boundsMax.y, t[6] = ln.boundsMax.z;
     }
 }
 
-// Exact refit of the local boxes above moved prims (they are the
-// accelerator's own, so unlike the reference nodes they may shrink): one wave
-// per dirty wide-record slot, the union of pbox over the slot's prim range
-// (a local subtree's prims are contiguous, accel.cpp LocalBuilder).
-// dirty[j] = (4*w + s, first prim, end prim, 0).
-__device__ void refit_slot(const int4* __restrict__ dirty, int j, const float4* __restrict__ pbox,
-                           float4* __restrict__ lnodes, int rec, int lane) {
-    const int4 d = dirty[j];
+// Slot role: exact refit of the local / scene-tree boxes above moved prims (they
+// are the accelerator's own, so unlike the reference nodes they may shrink): one
+// wave per dirty wide-record slot, the union of pbox over the slot's prim range (a
+// subtree's prims are contiguous, accel.cpp LocalBuilder). dirty[j] = (4*w + s,
+// first prim, end prim, 0).
+__device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, int lane) {
+    const int4 d = r.dirty[j];
+    const float4* __restrict__ pbox = o.pbox;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (int p = d.y + lane; p < d.z; p += 64) {
-        const float4 a = pbox[2 * static_cast<size_t>(p)], b = pbox[2 * static_cast<size_t>(p) + 1];
+        const int e = r.direct ? m.prim_entry[p] : -1;
+        float4 a, b;
+        if (e >= 0 && m.ecls[e] == rta::BOUNDED) {  // a moved prim, from its record itself
+            rta::Box3 cb;
+            entry_cbox(o, r.fresh[e], rta::BOUNDED, cb);
+            a = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], 0.f), b = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
+        } else {
+            a = pbox[2 * static_cast<size_t>(p)], b = pbox[2 * static_cast<size_t>(p) + 1];
+        }
         lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
         hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
     }
@@ -2230,23 +2296,55 @@ __device__ void refit_slot(const int4* __restrict__ dirty, int j, const float4* 
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
         const int w = d.x >> 2, sl = d.x & 3;
         const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
-        *wide_box_f(lnodes, rec, w, sl, lane) = v;
+        *wide_box_f(o.lnodes, r.rec, w, sl, lane) = v;
     }
 }
 
-// rt_animate's second step, after k_animate: the grown reference nodes (waves
-// [0, m.nodes)) and the refit local / scene-tree slots (the next n_dirty waves)
-// in ONE launch: they read what k_animate wrote (sbox / pbox) and write disjoint
-// records. (Round 3 ran them as four launches, k_grow_nodes, k_refit_local,
-// k_refresh_nodes over all N nodes and k_refresh_items over all items.)
-__global__ __launch_bounds__(256) void k_anim_refit(AnimMaps m, AnimOut o, const int4* __restrict__ dirty,
-                                                    int n_dirty, int rec) {
-    const int w = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-    if (w < m.nodes) {
-        grow_node(m, o, w, lane);
-    } else if (w - m.nodes < n_dirty) {
-        refit_slot(dirty, w - m.nodes, o.pbox, o.lnodes, rec, lane);
+// The per-frame refit of flush_updates, in one-wave workgroups with four roles:
+//   [0, na)             record role (refit_record), 64 entries each;
+//   [na, na + nd)       node-set role (set_node), 64 nodes or items each;
+//   [na + nd, ...)      one wave each: node role (grow_node) for the first nb, then
+//                       slot role (refit_slot); both read what the record role wrote.
+// Default (rt_debug_refit 1): two launches, records and node sets, then nodes and
+// slots: the kernel boundary orders them (GPU time ~12 + ~12 us on the car's wheels,
+// no gap between the two). Mode 0 is ONE launch whose workgroups take tickets on
+// arrival (handed out in the order they start, so a later ticket waits only for work
+// already running) and whose node / slot waves spin until every record workgroup has
+// released its writes: measured slower (35 us), the single ticket counter serialising
+// ~270 workgroups. Mode 2 is one launch whose node / slot waves derive each entry's
+// boxes from its record over the host link themselves (72 us). The node-set role never
+// runs with AF_GROW entries in the same flush (flush_updates applies host node records
+// first), so no two roles write the same box.
+__global__ __launch_bounds__(64) void k_refit(AnimMaps m, AnimOut o, RefitArgs r) {
+    const int lane = threadIdx.x;
+    unsigned t = blockIdx.x;  // without waits the launch order does not matter
+    if (r.wait) {
+        if (lane == 0) t = __hip_atomic_fetch_add(r.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.tbase;
+        t = __shfl(t, 0);
     }
+    if (t < static_cast<unsigned>(r.na)) {
+        refit_record(m, o, r, static_cast<int>(t) * 64 + lane);
+        if (r.wait && lane == 0) __hip_atomic_fetch_add(r.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    t -= r.na;
+    if (t < static_cast<unsigned>(r.nd)) {
+        set_node(o, r, static_cast<int>(t) * 64 + lane);
+        return;
+    }
+    t -= r.nd;
+    if (r.wait) {
+        if (lane == 0)
+            while (__hip_atomic_load(r.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.abase <
+                   static_cast<unsigned>(r.na))
+                __builtin_amdgcn_s_sleep(2);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    const int w = static_cast<int>(t);
+    if (w < r.nb)
+        grow_node(m, o, r, w, lane);
+    else if (w - r.nb < r.n_dirty)
+        refit_slot(m, o, r, w - r.nb, lane);
 }
 
 // Scene-tree wide slots of the unbounded subtree (kNoPrune): their boxes are the
@@ -2367,7 +2465,6 @@ struct rt_ctx {
     std::vector<int> refit_of;          // per shape: its refit entry, -1 if none
     std::vector<int> anim_cls;          // per refit entry: accelerator class at the last build (accel_bound.h)
     std::vector<FlatShape> anim_base;   // per refit entry: the record the accelerator's cones were built from
-    std::vector<int> refit_flags;       // per refit entry: AF_BOUNDED / AF_CONE of its current record
     // rt_update_shapes / rt_update_nodes only write the host copies; the next device
     // operation (flush_updates) applies them in one refit, like glBufferSubData
     // calls that take effect at the next dispatch.
@@ -2376,23 +2473,35 @@ struct rt_ctx {
     std::vector<std::pair<int, FlatShape>> upd_base;  // their build-time records (shapes new to the refit set)
     bool nodes_dirty = false;           // host_nodes newer than every device copy
     bool nodes_rebuild = false;         // host_nodes break a condition the accelerator was built on
+    bool bounds_rebuild = false;        // a refit reported a shape whose bound changed kind
     int updates_flushed = 0;            // flushes that refit instead of rebuilding (diagnostics)
+    // rt_debug_refit: 0 one launch (box roles wait on tickets), 1 two launches (default:
+    // the car's waited animated frame 0.262 ms against 0.268 and 0.299, r05d), 2 one
+    // launch (box roles read the records over the host link themselves)
+    int refit_mode = 1;
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
     size_t anim_maps_cap = 0;
     AnimMaps anim{};
     // Per-frame records, FlatShape[count] then int flags[count]: a ring of pinned, mapped
-    // host buffers that k_animate reads directly, so rt_animate waits only for the
-    // k_animate kAnimRing frames back (not for the previous frame's render).
+    // host buffers that k_refit reads directly, so a flush waits only for the
+    // k_refit kAnimRing flushes back (not for the previous frame's render). Each slot
+    // ends in a report word k_refit sets when a shape's bound changed kind.
     static constexpr int kAnimRing = 3;
     void* anim_pinned[kAnimRing] = {nullptr, nullptr, nullptr};
     void* anim_pinned_dev[kAnimRing] = {nullptr, nullptr, nullptr};  // the same buffers as the device sees them
     size_t anim_pinned_cap[kAnimRing] = {0, 0, 0};
-    hipEvent_t anim_copied[kAnimRing] = {nullptr, nullptr, nullptr};  // that slot's k_animate has read it
+    hipEvent_t anim_copied[kAnimRing] = {nullptr, nullptr, nullptr};  // that slot's k_refit has run
+    size_t report_at[kAnimRing] = {0, 0, 0};       // offset of the slot's report word
+    bool report_pending[kAnimRing] = {false, false, false};  // its k_refit not yet checked
+    unsigned* refit_ctr = nullptr;      // k_refit's ticket and done counters (never reset)
+    unsigned ctr_tickets = 0, ctr_done = 0;  // their values after the last launch
+    float4* anim_enorm = nullptr;       // per refit entry: base stored normal + type (AnimMaps::enorm)
+    size_t anim_enorm_cap = 0;
     int anim_slot = 0;
     float4* anim_sbox = nullptr;        // per animated shape boxes (AnimOut::sbox)
     size_t anim_sbox_cap = 0;
     float4* pbox = nullptr;             // per prim conservative box (AnimOut::pbox)
-    int4* refit_dirty = nullptr;        // k_anim_refit's refit work list
+    int4* refit_dirty = nullptr;        // k_refit's slot work list
     int n_dirty = 0;
     int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
@@ -2751,7 +2860,6 @@ int prepare_animation(rt_ctx* c) {
     c->anim = AnimMaps{};
     c->refit_of.assign(c->S, -1);
     for (int i = 0; i < n; ++i) c->refit_of[c->refit_ids[i]] = i;
-    c->refit_flags.assign(n, -1);  // -1: derive at the next flush
     if (n == 0) return RT_OK;
     const int N = c->N;
     const std::vector<int>& which = c->refit_of;  // shape -> refit entry
@@ -2759,7 +2867,7 @@ int prepare_animation(rt_ctx* c) {
     c->anim_cls.assign(n, rta::UNBOUNDED);
     for (int i = 0; i < n; ++i) {
         rta::Box3 b;
-        c->anim_cls[i] = rta::classify(c->anim_base[i], b, A.origin_lim);
+        c->anim_cls[i] = rta::classify(c->anim_base[i], b, A.origin_lim, A.mt);
     }
     // reference nodes listing each shape: the leaves that list it and every node above
     std::vector<std::vector<int>> parents(N);
@@ -2850,7 +2958,7 @@ int prepare_animation(rt_ctx* c) {
         // nodes follow the local ones in lnodes (global slot 4*nw + q), a subtree's
         // prims are contiguous. Its unbounded part (kNoPrune: boxes are the padded
         // reference-leaf boxes, which grow) goes infinite while the set is animated;
-        // the items' exact boxes follow the grown leaves (k_anim_refit).
+        // the items' exact boxes follow the grown leaves (k_refit).
         const rta::SceneTree& T = A.st;
         if (T.wroot >= 0) {
             const size_t nw = A.wchild.size() / rta::kWide, Ms = T.box.size();
@@ -2929,7 +3037,7 @@ int prepare_animation(rt_ctx* c) {
         list_at = buf.size();
         for (const auto& l : lists) buf.insert(buf.end(), l.begin(), l.end());
     };
-    // per reference node, the animated shapes it lists (k_anim_refit)
+    // per reference node, the animated shapes it lists (k_refit's node role)
     std::vector<int> node_ids;
     std::vector<std::vector<int>> lists_of;
     {
@@ -2944,7 +3052,7 @@ int prepare_animation(rt_ctx* c) {
                 lists_of[slot[k]].push_back(i);
             }
     }
-    // per grown node, where its box is copied (k_anim_refit writes them through): the
+    // per grown node, where its box is copied (k_refit writes them through): the
     // wnodes child slots of its parent(s) and the scene-tree items it gates
     std::vector<std::vector<int>> wn_of(node_ids.size()), items_of(node_ids.size());
     {
@@ -2971,14 +3079,28 @@ int prepare_animation(rt_ctx* c) {
     append(items_of, o[10], o[11]);
     const size_t o_ids = buf.size();
     buf.insert(buf.end(), node_ids.begin(), node_ids.end());
+    const size_t o_cls = buf.size();  // per entry: the class the accelerator was built with
+    buf.insert(buf.end(), c->anim_cls.begin(), c->anim_cls.end());
+    const size_t o_pe = buf.size();   // per accelerator prim: its shape's refit entry (-1: none)
+    for (size_t p = 0; p < (c->accel_ok ? A.prim_shape.size() : 0); ++p) buf.push_back(which[A.prim_shape[p]]);
     int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
     if (rc != RT_OK) return rc;
+    std::vector<float4> en(n);  // per entry: the base record's stored normal and type (the cone test)
+    for (int i = 0; i < n; ++i) {
+        const FlatShape& b0 = c->anim_base[i];
+        en[i] = make_float4(b0.planeNormal.x, b0.planeNormal.y, b0.planeNormal.z, bits_f(b0.type));
+    }
+    if ((rc = ensure_staging(c->anim_enorm, c->anim_enorm_cap, static_cast<size_t>(n))) != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->anim_enorm, en.data(), en.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int* d = c->anim_maps;
     c->anim = AnimMaps{d,        d + o[0], d + o[1],  d + o[2],  d + o[3], d + o[4], d + o[5], d + o_ids,
-                       d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], n,
+                       d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], d + o_cls, d + o_pe,
+                       c->anim_enorm, n,
                        static_cast<int>(node_ids.size())};
+    // the degraded-bound reports of earlier refits concern the accelerator this replaced
+    for (bool& pend : c->report_pending) pend = false;
     return ensure_staging(c->anim_sbox, c->anim_sbox_cap, 4 * static_cast<size_t>(n));
 }
 
@@ -2990,7 +3112,7 @@ int upload_accel(rt_ctx* c) {
     // the refit set stays (its shapes tend to move again), with the records just built from
     c->anim_base.resize(c->refit_ids.size());
     for (size_t i = 0; i < c->refit_ids.size(); ++i) c->anim_base[i] = c->host_shapes[c->refit_ids[i]];
-    c->nodes_rebuild = false;
+    c->nodes_rebuild = c->bounds_rebuild = false;
     const int rc2 = prepare_animation(c);
     return rc != RT_OK ? rc : rc2;
 }
@@ -3025,131 +3147,169 @@ bool host_nodes_nest(const rt_ctx* c) {
     return true;
 }
 
-// A slot of the pinned ring k_animate / k_set_nodes read from, at least `bytes`
-// large; waits for that slot's previous reader (kAnimRing flushes back).
+// Reads the report words of earlier refits whose k_refit has run (block: wait for
+// them): a shape whose bound changed kind leaves the accelerator exact but slower
+// (k_refit enters every box above it) until the host rebuilds it.
+int check_reports(rt_ctx* c, bool block = false) {
+    for (int s = 0; s < rt_ctx::kAnimRing; ++s) {
+        if (!c->report_pending[s]) continue;
+        if (block) {
+            HIP_TRY(hipEventSynchronize(c->anim_copied[s]));
+        } else {
+            const hipError_t e = hipEventQuery(c->anim_copied[s]);
+            if (e == hipErrorNotReady) continue;
+            if (e != hipSuccess) return RT_ERR_DEVICE;
+        }
+        c->report_pending[s] = false;
+        const int* rep = reinterpret_cast<const int*>(static_cast<const char*>(c->anim_pinned[s]) + c->report_at[s]);
+        if (*rep) c->bounds_rebuild = true;
+    }
+    return RT_OK;
+}
+
+// A slot of the pinned ring k_refit reads from, `bytes` large plus its report word;
+// waits for that slot's previous k_refit (kAnimRing flushes back).
 int pinned_slot(rt_ctx* c, size_t bytes, char** host, const char** dev) {
     const int slot = c->anim_slot;
     c->anim_slot = (slot + 1) % rt_ctx::kAnimRing;
     if (!c->anim_copied[slot]) {
         HIP_TRY(hipEventCreateWithFlags(&c->anim_copied[slot], hipEventDisableTiming));
-    } else {
-        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // this slot's last readers have run
+    } else if (c->report_pending[slot]) {
+        HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // this slot's last k_refit has run
+        if (const int rc = check_reports(c)) return rc;
     }
-    if (c->anim_pinned_cap[slot] < bytes) {
+    bytes = (bytes + 15) / 16 * 16;
+    if (c->anim_pinned_cap[slot] < bytes + 16) {
         if (c->anim_pinned[slot]) hipHostFree(c->anim_pinned[slot]);
         c->anim_pinned[slot] = nullptr;
         c->anim_pinned_dev[slot] = nullptr;
         c->anim_pinned_cap[slot] = 0;
-        // mapped and coherent: the kernels read it over the host link, never a stale cached copy
-        if (hipHostMalloc(&c->anim_pinned[slot], bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        // mapped and coherent: the kernel reads it over the host link, never a stale cached copy
+        if (hipHostMalloc(&c->anim_pinned[slot], bytes + 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
             return RT_ERR_NO_MEMORY;
         if (hipHostGetDevicePointer(&c->anim_pinned_dev[slot], c->anim_pinned[slot], 0) != hipSuccess)
             return RT_ERR_DEVICE;
-        c->anim_pinned_cap[slot] = bytes;
+        c->anim_pinned_cap[slot] = bytes + 16;
     }
+    c->report_at[slot] = bytes;
     *host = static_cast<char*>(c->anim_pinned[slot]);
     *dev = static_cast<const char*>(c->anim_pinned_dev[slot]);
+    *reinterpret_cast<int*>(*host + bytes) = 0;
     return slot;
 }
 
 // Applies what rt_update_shapes / rt_update_nodes left on the host, and an
 // rt_animate frame (grow: the animated entries grow the nodes listing them, as
-// updateBVH does), to every device copy in one refit on the stream:
-//   k_animate    every refit entry's records, read from the pinned ring;
-//   k_anim_refit the nodes listing an entry (their content boxes; with grow their
-//                exact boxes) and the local / scene-tree boxes above its prims;
-//   k_set_nodes  the host's node records (rt_update_nodes), exact boxes only.
-// No host rebuild unless a moved shape changed its kind of bound or the new node
-// boxes break the nesting the scene tree was built on (then after the refit, as
-// rt_animate always did). Called by every operation that reads the device scene.
+// updateBVH does), to every device copy with one launch of k_refit on the stream:
+// every refit entry's records (read from the pinned ring), the nodes listing an
+// entry (their content boxes; with grow their exact boxes), the local and
+// scene-tree boxes above its prims, and the host's node records (rt_update_nodes).
+// The host does no per-shape work beyond copying the records: whether a bound
+// changed kind is decided by k_refit, which keeps such a frame exact and reports it.
+// The host rebuilds the accelerator (for speed) once a report comes in, and (for
+// exactness of the scene tree) when new node boxes stop nesting. Called by every
+// operation that reads the device scene.
 int flush_updates(rt_ctx* c, bool grow = false) {
-    if (!c->have_scene || (c->upd_ids.empty() && !c->nodes_dirty && !grow)) return RT_OK;
-    int rc = RT_OK;
-    // shapes new to the refit set join it with their build-time records
-    bool added = false;
-    for (const auto& ub : c->upd_base)
-        if (c->refit_of[ub.first] < 0) {
-            c->refit_of[ub.first] = static_cast<int>(c->refit_ids.size());
-            c->refit_ids.push_back(ub.first);
-            c->anim_base.push_back(ub.second);
-            added = true;
-        }
-    if (added && (rc = prepare_animation(c)) != RT_OK) return rc;
-    const int n = static_cast<int>(c->refit_ids.size());
-    // per entry: class (a change rebuilds), cone (a moved normal drops its cones), grow
-    bool rebuild = c->nodes_rebuild;
-    std::vector<char> grows(n, 0);
-    if (grow)
-        for (int id : c->anim_ids)
-            if (c->refit_of[id] >= 0) grows[c->refit_of[id]] = 1;
-    std::vector<int> flags(n);
-    for (int i = 0; i < n; ++i) {
-        const int id = c->refit_ids[i];
-        if (c->refit_flags[i] < 0 || c->upd_mark[id] || grows[i]) {  // a record written since the last flush
-            const FlatShape &s = c->host_shapes[id], &b0 = c->anim_base[i];
-            int cls = rta::UNBOUNDED;
-            if (c->accel_ok) cls = rta::classify_class(s, c->accel.origin_lim);  // classify's class, without the box
-            const bool cone = s.type != b0.type || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
-                                                    std::memcmp(&s.planeNormal, &b0.planeNormal, sizeof(rt_vec3)) != 0);
-            c->refit_flags[i] = (cls == rta::BOUNDED ? AF_BOUNDED : 0) | (cone ? AF_CONE : 0) |
-                                (c->accel_ok && cls != c->anim_cls[i] ? 8 : 0);
-        }
-        if (c->refit_flags[i] & 8) rebuild = true;  // a bound changed kind since the build
-        flags[i] = (c->refit_flags[i] & (AF_BOUNDED | AF_CONE)) | (grows[i] ? AF_GROW : 0);
-    }
-    const bool nodes = c->nodes_dirty && c->N > 0;
-    const size_t rec_bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
-    const size_t bytes = rec_bytes + (nodes ? static_cast<size_t>(c->N) * sizeof(FlatNode) : 0);
-    if (bytes > 0) {
-        char* pin = nullptr;
-        const char* pin_dev = nullptr;
-        const int slot = pinned_slot(c, bytes, &pin, &pin_dev);
-        if (slot < 0) return slot;
-        for (int i = 0; i < n; ++i)
-            std::memcpy(pin + i * sizeof(FlatShape), &c->host_shapes[c->refit_ids[i]], sizeof(FlatShape));
-        std::memcpy(pin + n * sizeof(FlatShape), flags.data(), n * sizeof(int));
-        if (nodes) std::memcpy(pin + rec_bytes, c->host_nodes.data(), c->N * sizeof(FlatNode));
-        const bool acc = c->accel_ok;
-        const size_t P = c->accel.prim_shape.size();
-        if (n > 0) {
+    if (!c->have_scene) return RT_OK;
+    int rc = check_reports(c);
+    if (rc != RT_OK) return rc;
+    const bool work = !c->upd_ids.empty() || c->nodes_dirty || grow;
+    if (!work && !c->bounds_rebuild) return RT_OK;
+    if (work) {
+        // shapes new to the refit set join it with their build-time records
+        bool added = false;
+        for (const auto& ub : c->upd_base)
+            if (c->refit_of[ub.first] < 0) {
+                c->refit_of[ub.first] = static_cast<int>(c->refit_ids.size());
+                c->refit_ids.push_back(ub.first);
+                c->anim_base.push_back(ub.second);
+                added = true;
+            }
+        if (added && (rc = prepare_animation(c)) != RT_OK) return rc;
+        const int n = static_cast<int>(c->refit_ids.size());
+        const bool nodes = c->nodes_dirty && c->N > 0;
+        const size_t rec_bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
+        const size_t bytes = rec_bytes + (nodes ? static_cast<size_t>(c->N) * sizeof(FlatNode) : 0);
+        if (bytes > 0) {
+            char* pin = nullptr;
+            const char* pin_dev = nullptr;
+            const int slot = pinned_slot(c, bytes, &pin, &pin_dev);
+            if (slot < 0) return slot;
+            for (int i = 0; i < n; ++i)
+                std::memcpy(pin + i * sizeof(FlatShape), &c->host_shapes[c->refit_ids[i]], sizeof(FlatShape));
+            int* flags = reinterpret_cast<int*>(pin + n * sizeof(FlatShape));
+            std::memset(flags, 0, n * sizeof(int));
+            if (grow)
+                for (int id : c->anim_ids) flags[c->refit_of[id]] = AF_GROW;
+            if (nodes) std::memcpy(pin + rec_bytes, c->host_nodes.data(), c->N * sizeof(FlatNode));
+            const bool acc = c->accel_ok;
+            const size_t P = c->accel.prim_shape.size();
             const AnimOut out{c->staging_shapes, c->staging_nodes, c->geo_lin, c->geo_leaf, c->mat, c->nodes,
                               acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
                               acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
                               acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
                               c->accel.origin_lim, c->accel.mt ? 1 : 0};
-            // 1. the entries' records and boxes, read from the pinned buffer
-            hipLaunchKernelGGL(k_animate, dim3((n + 63) / 64), dim3(64), 0, c->stream,
-                               reinterpret_cast<const FlatShape*>(pin_dev),
-                               reinterpret_cast<const int*>(pin_dev + n * sizeof(FlatShape)), c->anim, out);
-            // 2. the nodes listing them (written through to every copy) and the refit local boxes
-            const int nd = acc ? c->n_dirty : 0;
-            if (c->anim.nodes + nd > 0)
-                hipLaunchKernelGGL(k_anim_refit, dim3((c->anim.nodes + nd + 3) / 4), dim3(256), 0, c->stream, c->anim,
-                                   out, c->refit_dirty, nd, c->accel.mt ? kWideRecMt : kWideRec);
+            if (!c->refit_ctr) {
+                if (hipMalloc(&c->refit_ctr, 2 * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, 2 * sizeof(unsigned), c->stream));
+                c->ctr_tickets = c->ctr_done = 0;
+            }
+            RefitArgs r{};
+            r.fresh = reinterpret_cast<const FlatShape*>(pin_dev);
+            r.flags = reinterpret_cast<const int*>(pin_dev + n * sizeof(FlatShape));
+            r.nsrc = nodes ? reinterpret_cast<const FlatNode*>(pin_dev + rec_bytes) : nullptr;
+            r.report = reinterpret_cast<int*>(const_cast<char*>(pin_dev) + c->report_at[slot]);
+            r.ctr = c->refit_ctr;
+            r.tbase = c->ctr_tickets;
+            r.abase = c->ctr_done;
+            r.na = (n + 63) / 64;
+            r.N = c->N;
+            r.n_items = nodes && acc ? c->n_titems : 0;
+            r.titem_ref = c->titem_ref;
+            r.nd = nodes ? (c->N + r.n_items + 63) / 64 : 0;
+            r.nb = n > 0 ? c->anim.nodes : 0;
+            r.dirty = c->refit_dirty;
+            r.n_dirty = n > 0 && acc ? c->n_dirty : 0;
+            r.rec = c->accel.mt ? kWideRecMt : kWideRec;
+            r.wait = c->refit_mode == 0;
+            r.direct = c->refit_mode == 2;
+            auto go = [&](const RefitArgs& ra) -> int {
+                const int grid = ra.na + ra.nd + ra.nb + ra.n_dirty;
+                if (grid == 0) return RT_OK;
+                hipLaunchKernelGGL(k_refit, dim3(grid), dim3(64), 0, c->stream, c->anim, out, ra);
+                HIP_TRY(hipGetLastError());
+                c->ctr_tickets += static_cast<unsigned>(grid);
+                if (ra.wait) c->ctr_done += static_cast<unsigned>(ra.na);
+                return RT_OK;
+            };
+            if (c->refit_mode == 1) {  // records and node sets, then (a kernel boundary later) the boxes
+                RefitArgs r1 = r, r2 = r;
+                r1.nb = r1.n_dirty = 0;
+                r2.na = r2.nd = 0;
+                r2.tbase = c->ctr_tickets + static_cast<unsigned>(r1.na + r1.nd);
+                if ((rc = go(r1)) != RT_OK || (rc = go(r2)) != RT_OK) return rc;
+            } else if ((rc = go(r)) != RT_OK) {
+                return rc;
+            }
+            HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));  // the slot may be refilled after this
+            c->report_pending[slot] = n > 0 && acc;
+            if (nodes && (rc = open_inf_slots(c)) != RT_OK) return rc;
         }
-        if (nodes) {
-            // 3. rt_update_nodes: the host's records to every copy of the exact boxes
-            const int items = acc ? c->n_titems : 0;
-            hipLaunchKernelGGL(k_set_nodes, dim3((c->N + items + 255) / 256), dim3(256), 0, c->stream,
-                               reinterpret_cast<const FlatNode*>(pin_dev + rec_bytes), c->N, c->staging_nodes,
-                               c->nodes, acc ? c->anodes : nullptr, acc ? c->wnodes : nullptr,
-                               acc ? c->titems : nullptr, c->titem_ref, items);
-        }
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));  // the slot may be refilled after this
-        if (nodes && (rc = open_inf_slots(c)) != RT_OK) return rc;
+        if (grow) c->nodes_on_device_newer = true;  // the device grew the nodes past host_nodes
+        c->nodes_dirty = false;
+        for (int id : c->upd_ids) c->upd_mark[id] = 0;
+        c->upd_ids.clear();
+        c->upd_base.clear();
     }
-    if (grow) c->nodes_on_device_newer = true;  // the device grew the nodes past host_nodes
-    c->nodes_dirty = false;
-    for (int id : c->upd_ids) c->upd_mark[id] = 0;
-    c->upd_ids.clear();
-    c->upd_base.clear();
-    if (!rebuild) {
+    if (!c->nodes_rebuild && !c->bounds_rebuild) {
         ++c->updates_flushed;
         return RT_OK;
     }
+    // a bound changed kind (reported by an earlier k_refit), or the node boxes stopped
+    // nesting: rebuild from the host copies (which the refit above brought to the device)
     ++c->anim_rebuilds;
-    return upload_accel(c);  // a bound changed kind, or the boxes stopped nesting: rebuild from the host copies
+    c->bounds_rebuild = false;
+    return upload_accel(c);
 }
 
 size_t sched_set_words(int tiles) {
@@ -3326,6 +3486,8 @@ rt_ctx* mt_ctx(rt_ctx* c, const KParams& kp) {
 // (Moller-Trumbore) when they apply and their accelerator can take the frame,
 // timed by this context's events (rt_kernel_times) like any other dispatch.
 int render(rt_ctx* c, const KParams& kp) {
+    // this context's own pending writes first, also when a sub-context renders the frame
+    if (const int rc = flush_updates(c)) return rc;
     rt_ctx* t = c;
     KParams kt = kp;
     for (int hop = 0; hop < 2; ++hop) {
@@ -3777,6 +3939,8 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->sched_sets);
     hipFree(c->anim_maps);
     hipFree(c->anim_sbox);
+    hipFree(c->anim_enorm);
+    hipFree(c->refit_ctr);
     for (int k = 0; k < rt_ctx::kAnimRing; ++k) {
         if (c->anim_pinned[k]) hipHostFree(c->anim_pinned[k]);
         if (c->anim_copied[k]) hipEventDestroy(c->anim_copied[k]);
@@ -3857,7 +4021,7 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->upd_ids.clear();
     c->upd_base.clear();
     c->upd_mark.assign(S, 0);
-    c->nodes_dirty = c->nodes_rebuild = false;
+    c->nodes_dirty = c->nodes_rebuild = c->bounds_rebuild = false;
     c->brute_stale = c->mtc_stale = true;
     return upload_accel(c);
 }
@@ -3953,8 +4117,8 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
         for (int i = 0; i < n && !c->brute_stale; ++i)
             if (rt_update_shapes(c->brute, c->anim_ids[i], 1, &shapes[i]) != RT_OK) c->brute_stale = true;
     c->mtc_stale = true;
-    // the records and the growth on the device (k_animate + k_anim_refit); a host
-    // rebuild only when a bound changed kind
+    // the records and the growth on the device (one k_refit launch); a host rebuild
+    // only after a bound changed kind
     return flush_updates(c, true);
 }
 
@@ -4223,6 +4387,14 @@ extern "C" int rt_set_tree(rt_ctx* c, int mode) {
 
 extern "C" int rt_debug_anim_rebuilds(rt_ctx* c) { return c ? c->anim_rebuilds : -1; }
 extern "C" int rt_debug_refits(rt_ctx* c) { return c ? c->updates_flushed : -1; }
+// Diagnostics: how flush_updates launches the refit (RefitArgs: 0 one launch whose box
+// roles wait for the record role, 1 two launches, 2 one launch deriving every box from
+// the records). Same device state either way.
+extern "C" int rt_debug_refit(rt_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 2) return RT_ERR_INVALID;
+    c->refit_mode = mode;
+    return RT_OK;
+}
 
 extern "C" int rt_set_walk(rt_ctx* c, int lane_from_depth) {
     if (!c || lane_from_depth < -1) return RT_ERR_INVALID;

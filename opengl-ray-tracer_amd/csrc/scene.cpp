@@ -10,6 +10,7 @@
 // the reference's IEEE sequence.
 #include "../../include/rt_scene.h"
 
+#include <algorithm>
 #include <cerrno>
 #include <cmath>
 #include <cstdio>
@@ -912,28 +913,33 @@ int rts_update_bvh(const FlatShape* shapes, int S, FlatNode* nodes, int N, const
         if (ids[j] < 0 || ids[j] >= S) return -1;
         animated[ids[j]] = 1;
     }
-    std::vector<std::vector<int>> parents(static_cast<size_t>(N));
+    // the nodes above each node (split()'s trees: one parent each; any others are kept too)
+    std::vector<int> parent(static_cast<size_t>(N), -1);
+    std::vector<std::pair<int, int>> extra;  // (child, another parent)
     for (int k = 0; k < N; ++k) {
         const FlatNode& nd = nodes[k];
         if (nd.leftChild == -1) continue;
         if (nd.leftChild < 0 || nd.leftChild >= N || nd.rightChild < 0 || nd.rightChild >= N) return -1;
-        parents[nd.leftChild].push_back(k);
-        if (nd.rightChild != nd.leftChild) parents[nd.rightChild].push_back(k);
+        for (int ch : {nd.leftChild, nd.rightChild}) {
+            if (parent[ch] < 0) parent[ch] = k;
+            else if (parent[ch] != k) extra.push_back({ch, k});
+        }
     }
-    // per shape (ascending), the nodes listing it: its leaves and every node above them
-    std::vector<std::vector<int>> leaves_of(static_cast<size_t>(S));
+    // (shape, leaf) for every animated shape a leaf lists, in shape order
+    std::vector<std::pair<int, int>> occ;
     for (int k = 0; k < N; ++k) {
         const FlatNode& nd = nodes[k];
         if (nd.leftChild != -1 || nd.numShapes <= 0) continue;
         if (nd.startShapeIdx < 0 || nd.startShapeIdx > I - nd.numShapes) return -1;
         for (int j = nd.startShapeIdx; j < nd.startShapeIdx + nd.numShapes; ++j) {
             if (idx[j] < 0 || idx[j] >= S) return -1;
-            if (animated[idx[j]]) leaves_of[idx[j]].push_back(k);
+            if (animated[idx[j]]) occ.push_back({idx[j], k});
         }
     }
+    std::sort(occ.begin(), occ.end());
     std::vector<int> stamp(static_cast<size_t>(N), -1), todo;
-    for (int a = 0; a < S; ++a) {
-        if (!animated[a] || leaves_of[a].empty()) continue;
+    for (size_t q = 0; q < occ.size();) {
+        const int a = occ[q].first;
         const FlatShape& f = shapes[a];
         Prim p;
         p.kind = f.type;
@@ -944,9 +950,13 @@ int rts_update_bvh(const FlatShape* shapes, int S, FlatNode* nodes, int N, const
         p.p0 = f.type == RT_SPHERE ? V3(&f.sphereCenter.x) : f.type == RT_WALL ? V3(&f.wallStart.x) : V3(&f.triP1.x);
         p.p1 = V3(&f.triP2.x);
         p.p2 = V3(&f.triP3.x);
-        todo.assign(leaves_of[a].begin(), leaves_of[a].end());
-        for (int k : todo) stamp[k] = a;
-        while (!todo.empty()) {
+        todo.clear();
+        for (; q < occ.size() && occ[q].first == a; ++q)
+            if (stamp[occ[q].second] != a) {
+                stamp[occ[q].second] = a;
+                todo.push_back(occ[q].second);
+            }
+        while (!todo.empty()) {  // each node listing shape a grows once by it
             const int k = todo.back();
             todo.pop_back();
             Box b;
@@ -955,11 +965,15 @@ int rts_update_bvh(const FlatShape* shapes, int S, FlatNode* nodes, int N, const
             b.grow(p);
             nodes[k].boundsMin = flat(b.lo);
             nodes[k].boundsMax = flat(b.hi);
-            for (int q : parents[k])
-                if (stamp[q] != a) {
-                    stamp[q] = a;
-                    todo.push_back(q);
+            auto up = [&](int u) {
+                if (u >= 0 && stamp[u] != a) {
+                    stamp[u] = a;
+                    todo.push_back(u);
                 }
+            };
+            up(parent[k]);
+            for (const auto& e : extra)
+                if (e.first == k) up(e.second);
         }
     }
     return 0;

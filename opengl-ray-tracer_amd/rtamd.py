@@ -734,6 +734,13 @@ class ComputeShader:
         fn.restype = _I
         return int(fn(self._h))
 
+    def debug_refit(self, mode):
+        """rt_debug_refit: 0 one launch (box roles wait), 1 two launches, 2 one launch (direct)."""
+        fn = self._lib.rt_debug_refit
+        fn.argtypes = [_P, _I]
+        fn.restype = _I
+        self._chk(fn(self._h, int(mode)), "rt_debug_refit")
+
     def debug_refits(self):
         """Device refits that applied rt_update_shapes / rt_update_nodes / rt_animate
         without a host rebuild, since the context was made."""

@@ -174,3 +174,36 @@ def test_bouncing_spheres_and_their_oracle_scene():
         assert (root["boundsMin"] <= (c - r[:, None]).min(0)).all()
         assert (root["boundsMax"] >= (c + r[:, None]).max(0)).all()
     assert (fk.nodes["boundsMin"] <= fs.nodes["boundsMin"]).all()  # grow-only
+
+
+@pytest.mark.parametrize("kind", ["orbit", "dolly"])
+def test_camera_paths(kind):
+    """--camera-path: orbit = 720 cameras 0.5 degrees apart about the look-at point, each
+    looking at it; dolly = Camera::ProcessKeyboard steps of SPEED / 60 along Front, 96 in
+    and 96 back to the start (src/camera.hpp:75-90)."""
+    cfg, W, H, mb, _, target = bench.WORKLOADS[3]
+    sc = rtamd.Scene().generate(cfg, 0, W / H)
+    fs = sc.serializeScene()
+    cams = bench.camera_path(rtamd, sc, fs, kind, target)
+    assert cams.dtype == rtamd.CAMERA_DTYPE and cams.flags["C_CONTIGUOUS"]
+    p0 = fs.camera["Position"][0].astype(np.float64)
+    t = np.asarray(target, np.float64)
+    if kind == "orbit":
+        assert len(cams) == 720
+        r0 = np.linalg.norm(p0 - t)
+        for k in (0, 179, 359, 719):
+            p = cams["Position"][k].astype(np.float64)
+            assert abs(np.linalg.norm(p - t) - r0) < 1e-3 * r0
+            d = (t - p) / np.linalg.norm(t - p)
+            assert np.dot(d, cams["Front"][k]) > 0.9999  # looks at the target
+        a = (cams["Position"][0].astype(np.float64) - t)[[0, 2]]  # azimuth about the vertical axis
+        b = (cams["Position"][1].astype(np.float64) - t)[[0, 2]]
+        ang = np.degrees(np.arccos(np.dot(a, b) / np.linalg.norm(a) / np.linalg.norm(b)))
+        assert abs(ang - 0.5) < 1e-3
+    else:
+        assert len(cams) == 192
+        step = np.linalg.norm(cams["Position"][1].astype(np.float64) - cams["Position"][0])
+        assert abs(step - 0.25) < 1e-5
+        assert np.allclose(cams["Position"][0], p0) and np.allclose(cams["Position"][-1], cams["Position"][1], atol=1e-4)
+        assert (cams["Front"] == fs.camera["Front"][0]).all()
+    assert bench.camera_path(rtamd, sc, fs, "static", target).shape == (1,)
