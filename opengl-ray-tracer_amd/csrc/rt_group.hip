@@ -547,6 +547,21 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
         stripe > 65535 / (g->share + g->nranks - 1))
         return RT_ERR_INVALID;
     if (g->broken) return RT_ERR_COMM;
+    const int jj = static_cast<int>(g->next % g->frames);
+    // Rows that can only be background (sky_rows.h) stay off the links: every rank
+    // computes the same band [yb0, yb1) from the same camera, box and parameters; a
+    // peer sends its compact rows inside it, rank 0 writes the rest as background.
+    // Only where the reference draws the background for a ray missing the root:
+    // the BVH branch with at least one bounce and a root box. The band is the
+    // group's: a member whose camera or node boxes were changed through its own
+    // context (rt_group_member: rt_set_camera, rt_animate, rt_update_nodes) would
+    // draw geometry in rows the band calls sky, so such a frame is refused before
+    // anything is posted (RT_ERR_INVALID; rt_group_set_sky_rows(g, 0) lifts it).
+    const bool sky = g->sky_rows && g->nranks > 1 && g->have_cam && g->have_params && g->have_root &&
+                     g->params.useBVH && g->params.maxBounces >= 1 && g->params.resY > 0;
+    if (sky)
+        for (Member& b : g->m)
+            if (!rtx::matches_view(b.slot[jj].ctx, g->cam, g->root_lo, g->root_hi)) return RT_ERR_INVALID;
     // Every error from here on goes through fail(): in a multi-rank RCCL group the
     // peers may already wait on this frame's fan-in, so the communicator is aborted.
 #define F_HIP(x)                                                     \
@@ -597,15 +612,8 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
             }
         }
     }
-    // Rows that can only be background (sky_rows.h) stay off the links: every rank
-    // computes the same band [yb0, yb1) from the same camera, box and parameters; a
-    // peer sends its compact rows inside it, rank 0 writes the rest as background.
-    // Only where the reference draws the background for a ray missing the root:
-    // the BVH branch with at least one bounce and a root box.
-    int yb0 = 0, yb1 = height;
-    if (g->sky_rows && P > 1 && g->have_cam && g->have_params && g->have_root && g->params.useBVH &&
-        g->params.maxBounces >= 1 && g->params.resY > 0)
-        rtg::sky_band(g->cam, g->root_lo, g->root_hi, height, g->params.resY, &yb0, &yb1);
+    int yb0 = 0, yb1 = height;  // the sky-row band (above)
+    if (sky) rtg::sky_band(g->cam, g->root_lo, g->root_hi, height, g->params.resY, &yb0, &yb1);
     // the peers' compact row range inside the band (one contiguous run each)
     auto band_of = [&](int rank, int& c0, int& c1) {
         const Rows w = rank_rows(height, P, stripe, k, rank);
@@ -615,6 +623,28 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     for (Member& b : g->m) {  // the streams this frame queues work on (mark_streams), errors included
         b.slot[j].dirty = true;
         b.cdirty = b.cdirty || P > 1;
+    }
+    if (!g->phase_timing && P > 1) {
+        // Back-pressure without the phase events: the host issues this frame into slot j
+        // only once slot j's frame F frames back has released its buffers (bounded, so a
+        // stalled peer surfaces here within F frames, not only at the final sync).
+        for (Member& b : g->m) {
+            const Slot& s = b.slot[j];
+            if (!s.used) continue;
+            F_HIP(hipSetDevice(b.device));
+            const hipEvent_t rel = s.released;
+            const rtg::WaitResult w = rtg::wait_bounded(
+                [rel] {
+                    const hipError_t e = hipEventQuery(rel);
+                    return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+                },
+                [g] { return comm_error(g); }, g->timeout_ms);
+            if (w == rtg::kWaitDeviceError) return fail(g, RT_ERR_DEVICE);
+            if (w != rtg::kWaitDone) {
+                abort_comms(g);
+                return w == rtg::kWaitTimeout ? RT_ERR_TIMEOUT : RT_ERR_COMM;
+            }
+        }
     }
     PhaseRec& ph = g->ring[g->ring_pos];
     if (ph.pending) {

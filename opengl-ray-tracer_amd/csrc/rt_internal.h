@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "../../include/rt_flat.h"
+
 struct rt_ctx;
 
 namespace rtx {
@@ -25,5 +27,12 @@ int create_ctx(rt_ctx** out, int device, hipStream_t stream);
 // 0.183 in frames mode; profiles/r04c_strong1_queues.txt). Contexts made by
 // rt_create take it when RT_STREAMS_CUMASK=1 is set.
 hipError_t make_stream(hipStream_t* s, bool own_queue);
+
+// Whether the context renders with camera `cam` and a root box equal to [lo, hi]:
+// its camera as last set, its node records current on the host (no rt_animate growth
+// on the device, whatever rt_update_nodes left pending included). rt_group computes
+// the sky-row band from the group's own camera and root box on every rank; a member
+// changed behind the group's back would get background rows where it draws geometry.
+bool matches_view(const rt_ctx* c, const FlatCamera& cam, const float lo[3], const float hi[3]);
 
 }  // namespace rtx

@@ -576,6 +576,7 @@ struct AccelPtrs {
     int split_g;                        // ... over groups of at most this many lanes (a power of two)
     const int* __restrict__ prim_shape; // shape index per prim slot (the winner's material)
     float mt_z[3];                      // AccelHost::mt_z (Moller-Trumbore per-ray padding)
+    const float4* __restrict__ mtfloor; // MT: per wide node 4 x 2 float4, mt_pad's floor case per child (mt_floor)
 };
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
@@ -909,6 +910,10 @@ __host__ __device__ __forceinline__ float* wide_box_f(float4* lnodes, int rec, i
     return rec == kWideRecMt ? base + 16 * sl + comp : base + 4 * comp + sl;
 }
 
+#ifndef RT_MT_FLOOR
+#define RT_MT_FLOOR 1  // MT child test: 0 per-lane mt_pad only; 1 / 2 the wave-uniform floor case (2: no slab there)
+#endif
+
 template <bool MT = false>
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
     const float4* q = A.lnodes + (MT ? kWideRecMt : kWideRec) * static_cast<size_t>(uc & 0x3fffffffu);
@@ -928,18 +933,43 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
         h[0] = h[1] = h[2] = h[3] = false;
         cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
         cc[3] = __float_as_int(cd.w);
+        const float4* fq = A.mtfloor + 8 * static_cast<size_t>(uc & 0x3fffffffu);
 #pragma unroll kMtUnroll
         for (int s2 = 0; s2 < 4; ++s2) {
             const float4 f0 = q[4 * s2], f1 = q[4 * s2 + 1], f2v = q[4 * s2 + 2], f3 = q[4 * s2 + 3];
             const float k[4] = {f1.z, f1.w, f2v.x, f2v.y};
             const float m[6] = {f2v.z, f2v.w, f3.x, f3.y, f3.z, f3.w};
             float pad, lf, q2, pt, ilf, tt = 0.0f;
-            bool hh = true;
-            if (rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt, ilf)) {
+            bool hh = true, ok, slab = true;
+#if RT_MT_FLOOR
+            // mt_pad's floor case for every lane of the wave (the child's cone straddles
+            // the rays' directions: the top levels of the car's tree for every camera
+            // ray): the child's precomputed constants (mt_floor), no per-lane chain
+            const float cn0 = std::fabs(std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz))) - k[3];
+            const bool floor_lane = c.dlen <= rta::kMtDmax && !(c.dlen * std::fmax(cn0, 0.0f) * m[0] > 1e-5f);
+            if (__ballot(in && !floor_lane) == 0) {
+                const float4 fa = fq[2 * s2], fb = fq[2 * s2 + 1];
+                ok = fb.z > 0.0f;
+                pad = std::fma(fa.y, c.so, fa.x);
+                lf = fb.z;
+                ilf = fb.w;
+#if RT_MT_FLOOR == 1
+                q2 = std::fma(fa.w, c.so, fa.z);
+                pt = std::fma(fb.y, c.so, fb.x);
+#else
+                q2 = pt = 0.0f;
+                slab = false;  // the slab is a further cut only: skipped in the floor case
+#endif
+            } else
+#endif
+            {
+                ok = rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt, ilf);
+            }
+            if (ok) {
                 float tn, tf;
                 hh = rta::box_span(c, f0.x - pad, f0.y - pad, f0.z - pad, f0.w + pad, f1.x + pad, f1.y + pad,
                                    tl * lf, tn, tf);
-                if (hh && c.ix != 0.0f && m[5] < 3e38f)
+                if (hh && slab && c.ix != 0.0f && m[5] < 3e38f)
                     hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
 #if RT_MT_ILF
                 tt = tn * ilf;  // the stack's prune compares with tl, not tl * lf (ilf <= 1 / lf)
@@ -2048,6 +2078,8 @@ struct AnimOut {
     float4* sbox;                     // per entry: reference box, conservative box (4 float4)
     float origin_lim;
     int mt;                           // the accelerator's wide nodes: kWideRecMt float cones, else kWideRec
+    float mt_z[3];                    // MT accelerators: AccelHost::mt_z (the per-ray padding's centre Z)
+    float4* mtfloor;                  // MT accelerators: mt_pad's floor case per wide child (AccelPtrs::mtfloor)
 };
 
 // One refit launch (k_refit) of flush_updates: what it reads from the pinned ring
@@ -2125,10 +2157,13 @@ __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArg
     }
     const float4 bn = m.enorm[i];
     const int btype = __float_as_int(bn.w);
-    const bool cone = s.type != btype || ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
-                                          (__float_as_int(s.planeNormal.x) != __float_as_int(bn.x) ||
-                                           __float_as_int(s.planeNormal.y) != __float_as_int(bn.y) ||
-                                           __float_as_int(s.planeNormal.z) != __float_as_int(bn.z)));
+    // barycentric cones hold the stored normals (the INNER test's N); an MT cone holds
+    // the vertices' normals, which any move of a refit entry may turn
+    const bool cone = o.mt || s.type != btype ||
+                      ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
+                       (__float_as_int(s.planeNormal.x) != __float_as_int(bn.x) ||
+                        __float_as_int(s.planeNormal.y) != __float_as_int(bn.y) ||
+                        __float_as_int(s.planeNormal.z) != __float_as_int(bn.z)));
     if (cone)
         for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
             const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
@@ -2293,10 +2328,53 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
         hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
     }
     wave_minmax(lo, hi);
+    const int w = d.x >> 2, sl = d.x & 3;
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
-        const int w = d.x >> 2, sl = d.x & 3;
         const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
         *wide_box_f(o.lnodes, r.rec, w, sl, lane) = v;
+    }
+    if (!o.mt) return;
+    // Moller-Trumbore: the child's per-ray padding constants (accel.cpp build_cones_mt:
+    // smallest |e1 x e2|, largest u X, M = |p1 - Z| and 18 M + 10.5 (E1 + E2) over the
+    // triangles below) merged with the moved triangles' own, grow-only like the boxes;
+    // the slab along the cone axis is dropped (m[5] = inf: its triangles moved off it).
+    // The moved records are the record role's, in the staging copy (launch 1).
+    double cr = INFINITY, X = 0, es = 0, mm = 0;
+    for (int p = d.y + lane; p < d.z; p += 64) {
+        const int e = m.prim_entry[p];
+        if (e < 0) continue;
+        rta::MtTri t;
+        rta::Box3 tb;
+        const FlatShape& s = r.direct ? r.fresh[e] : o.shapes[m.ids[e]];
+        if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) continue;
+        const double dz[3] = {t.p1[0] - o.mt_z[0], t.p1[1] - o.mt_z[1], t.p1[2] - o.mt_z[2]};
+        cr = fmin(cr, t.cr);
+        X = fmax(X, t.X);
+        es = fmax(es, t.esum);
+        mm = fmax(mm, sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        cr = fmin(cr, __shfl_xor(cr, off));
+        X = fmax(X, __shfl_xor(X, off));
+        es = fmax(es, __shfl_xor(es, off));
+        mm = fmax(mm, __shfl_xor(mm, off));
+    }
+    if (lane != 0) return;
+    float* k = wide_box_f(o.lnodes, kWideRecMt, w, sl, 0) + 10;  // {cr, u X, M, 18 M + 10.5 Esum, w, h0}
+    const double up = 1.0 + 1e-5;
+    if (X > 0) {
+        k[0] = fminf(k[0], static_cast<float>(cr * (1.0 - 1e-5)));
+        k[1] = fmaxf(k[1], static_cast<float>(rta::kU * X * up));
+        k[2] = fmaxf(k[2], static_cast<float>(mm * up + 1e-5));
+        k[3] = fmaxf(k[3], static_cast<float>((18.0 * mm + 10.5 * es) * up + 1e-5));
+    }
+    k[5] = INFINITY;
+    if (o.mtfloor) {  // the floor-case constants follow the merged ones
+        float f8[8];
+        rta::mt_floor(k, f8);
+        float4* fq = o.mtfloor + 8 * static_cast<size_t>(w) + 2 * sl;
+        fq[0] = make_float4(f8[0], f8[1], f8[2], f8[3]);
+        fq[1] = make_float4(f8[4], f8[5], f8[6], f8[7]);
     }
 }
 
@@ -2389,6 +2467,7 @@ struct rt_ctx {
     std::vector<FlatShape> host_shapes;
     // exact-result accelerator (accel.h); device copies in the layouts of AccelPtrs
     float4 *anodes = nullptr, *lnodes = nullptr, *wnodes = nullptr, *prims = nullptr;
+    float4* mtfloor = nullptr;  // MT accelerator: mt_pad's floor case per wide child (AccelPtrs::mtfloor)
     int4* tleaf = nullptr;
     float4* titems = nullptr;  // scene-tree items (AccelPtrs::titems)
     int* titem_ref = nullptr;  // per titems record: its reference leaf (device copy)
@@ -2551,6 +2630,8 @@ void free_accel(rt_ctx* c) {
     hipFree(c->anodes);
     hipFree(c->lnodes);
     hipFree(c->wnodes);
+    hipFree(c->mtfloor);
+    c->mtfloor = nullptr;
     hipFree(c->tleaf);
     hipFree(c->titems);
     c->titems = nullptr;
@@ -2709,6 +2790,21 @@ int build_upload_accel(rt_ctx* c) {
     for (size_t w = 0; w < nw; ++w)
         emit_wide(w, w, A.wchild, A.wsub, A.lbox, A.lcone, [&](int j) { return leaf_code(static_cast<size_t>(j)); },
                   0);
+    // MT: per wide child the floor case of mt_pad as constants (accel_math.h mt_floor)
+    std::vector<float4> mf;
+    if (A.mt) {
+        mf.assign(8 * (nw ? nw : 1), make_float4(0.f, 0.f, 0.f, 0.f));
+        for (size_t w = 0; w < nw; ++w)
+            for (int s2 = 0; s2 < 4; ++s2) {
+                const int j = A.wchild[rta::kWide * w + s2];
+                float o8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (j >= 0) rta::mt_floor(&A.lmt[rta::kMtPadF * static_cast<size_t>(j)], o8);
+                mf[8 * w + 2 * s2] = make_float4(o8[0], o8[1], o8[2], o8[3]);
+                mf[8 * w + 2 * s2 + 1] = make_float4(o8[4], o8[5], o8[6], o8[7]);
+            }
+        if (hipMalloc(&c->mtfloor, mf.size() * sizeof(float4)) != hipSuccess) return RT_ERR_NO_MEMORY;
+        HIP_TRY(hipMemcpyAsync(c->mtfloor, mf.data(), mf.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
+    }
     // Items: with <= 8 distinct reference leaves (few-leaf mode, few_mask) a
     // local-leaf code kLocal|kLeaf|kItem|start<<6|leaf<<3|count and titems =
     // the leaves' exact boxes; otherwise kTopLeaf|kItem|item and titems = per
@@ -3004,7 +3100,7 @@ int prepare_animation(rt_ctx* c) {
         std::vector<float4> pb(2 * (P ? P : 1), make_float4(INFINITY, INFINITY, INFINITY, 0.f));
         for (size_t p = 0; p < P; ++p) {
             rta::Box3 b;
-            if (rta::classify(c->host_shapes[A.prim_shape[p]], b, A.origin_lim) != rta::BOUNDED) {
+            if (rta::classify(c->host_shapes[A.prim_shape[p]], b, A.origin_lim, A.mt) != rta::BOUNDED) {
                 pb[2 * p + 1] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
                 continue;
             }
@@ -3248,7 +3344,8 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                               acc ? c->anodes : nullptr, acc ? c->lnodes : nullptr, acc ? c->prims : nullptr,
                               acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
                               acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
-                              c->accel.origin_lim, c->accel.mt ? 1 : 0};
+                              c->accel.origin_lim, c->accel.mt ? 1 : 0,
+                              {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}, acc ? c->mtfloor : nullptr};
             if (!c->refit_ctr) {
                 if (hipMalloc(&c->refit_ctr, 2 * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
                 HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, 2 * sizeof(unsigned), c->stream));
@@ -3465,7 +3562,7 @@ rt_ctx* brute_ctx(rt_ctx* c, const KParams& kp) {
 // Moller-Trumbore frames through `mtc` (rt_ctx::mtc): the same shapes and tree,
 // the accelerator built for the MT test.
 rt_ctx* mt_ctx(rt_ctx* c, const KParams& kp) {
-    if (!kp.useBVH || !kp.useMT || c->build_mt || !c->anim_ids.empty() || c->S <= 0 || c->N <= 0 ||
+    if (!kp.useBVH || !kp.useMT || c->build_mt || c->S <= 0 || c->N <= 0 ||
         (c->kernel != RT_KERNEL_AUTO && c->kernel != RT_KERNEL_ACCEL))
         return nullptr;
     rt_ctx* b = sub_ctx(c, c->mtc, c->mtc_stale);
@@ -3474,7 +3571,9 @@ rt_ctx* mt_ctx(rt_ctx* c, const KParams& kp) {
         b->build_mt = true;
         if (sync_host_nodes(c) != RT_OK ||
             rt_upload_scene(b, c->host_shapes.data(), c->S, c->host_nodes.data(), c->N, c->host_idx.data(),
-                            c->I) != RT_OK)
+                            c->I) != RT_OK ||
+            (!c->anim_ids.empty() &&  // rt_animate frames forward to it from now on
+             rt_set_animated(b, c->anim_ids.data(), static_cast<int>(c->anim_ids.size())) != RT_OK))
             return nullptr;
         c->mtc_stale = false;
     }
@@ -3510,6 +3609,7 @@ int render(rt_ctx* c, const KParams& kp) {
     if (!c->timing) {
         const int rc = launch(t, kt, false);
         c->last_kind = t->last_kind;
+        c->timed = false;  // no events recorded for this dispatch
         return rc;
     }
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
@@ -3718,7 +3818,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
                           c->boxes_finite, c->split_max, c->split_g, c->prim_idx_dev,
-                          {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}};
+                          {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}, c->mtfloor};
         // compaction: bounces >= tail_from of the rays still alive run in k_accel_tail
         k2.tail_queue = nullptr;
         // RT_TAIL_AUTO: from bounce 2 on scenes of many scene-tree items (measured: config 5's
@@ -3827,6 +3927,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         c->last1 = e1;
         if (c->ring_used < static_cast<int>(c->ring0.size())) ++c->ring_used;
         c->timed = true;
+    } else if (!stats) {
+        c->timed = false;  // rt_set_kernel_timing(0): rt_last_kernel_ms has no dispatch to report
     }
     return RT_OK;
 }
@@ -3910,6 +4012,15 @@ int rtx::create_ctx(rt_ctx** out, int device, hipStream_t stream) {
         }
     *out = c;
     return RT_OK;
+}
+
+bool rtx::matches_view(const rt_ctx* c, const FlatCamera& cam, const float lo[3], const float hi[3]) {
+    if (!c || !c->have_cam || std::memcmp(&c->cam, &cam, sizeof cam) != 0) return false;
+    if (c->N <= 0) return true;
+    if (c->nodes_on_device_newer || static_cast<int>(c->host_nodes.size()) != c->N) return false;
+    const FlatNode& r = c->host_nodes[c->N - 1];
+    const float rl[3] = {r.boundsMin.x, r.boundsMin.y, r.boundsMin.z}, rh[3] = {r.boundsMax.x, r.boundsMax.y, r.boundsMax.z};
+    return std::memcmp(rl, lo, sizeof rl) == 0 && std::memcmp(rh, hi, sizeof rh) == 0;
 }
 
 extern "C" {
@@ -4043,12 +4154,11 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
         }
         c->host_shapes[id] = shapes[j];
     }
-    // the brute-force context holds the same shapes in the same order: it refits too
-    if (c->brute && !c->brute_stale) {
-        const int rc = rt_update_shapes(c->brute, first, count, shapes);
-        if (rc != RT_OK) c->brute_stale = true;
-    }
-    c->mtc_stale = true;
+    // the sub-contexts hold the same shapes in the same order (brute: under its one
+    // leaf; mtc: the MT accelerator): they refit too
+    if (c->brute && !c->brute_stale && rt_update_shapes(c->brute, first, count, shapes) != RT_OK)
+        c->brute_stale = true;
+    if (c->mtc && !c->mtc_stale && rt_update_shapes(c->mtc, first, count, shapes) != RT_OK) c->mtc_stale = true;
     return RT_OK;
 }
 
@@ -4073,7 +4183,7 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
             if (std::isnan(v)) c->boxes_finite = 0;
     // the scene tree holds only while the boxes nest (accel.h SceneTree)
     if (c->accel_ok && c->accel.st.wroot >= 0 && !host_nodes_nest(c)) c->nodes_rebuild = true;
-    c->mtc_stale = true;
+    if (c->mtc && !c->mtc_stale && rt_update_nodes(c->mtc, nodes, N) != RT_OK) c->mtc_stale = true;
     return RT_OK;
 }
 
@@ -4102,6 +4212,7 @@ int rt_set_animated(rt_ctx* c, const int* ids, int count) {
         c->anim_base.push_back(base);
         added = true;
     }
+    if (c->mtc && !c->mtc_stale && rt_set_animated(c->mtc, ids, count) != RT_OK) c->mtc_stale = true;
     return added ? prepare_animation(c) : RT_OK;
 }
 
@@ -4116,7 +4227,8 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (c->brute && !c->brute_stale)  // the brute-force context: the same records, no nodes to grow
         for (int i = 0; i < n && !c->brute_stale; ++i)
             if (rt_update_shapes(c->brute, c->anim_ids[i], 1, &shapes[i]) != RT_OK) c->brute_stale = true;
-    c->mtc_stale = true;
+    // the MT context: the same frame, its nodes grown the same way (its set follows c's)
+    if (c->mtc && !c->mtc_stale && rt_animate(c->mtc, shapes) != RT_OK) c->mtc_stale = true;
     // the records and the growth on the device (one k_refit launch); a host rebuild
     // only after a bound changed kind
     return flush_updates(c, true);

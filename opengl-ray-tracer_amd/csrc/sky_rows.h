@@ -7,10 +7,14 @@
 // every direction of the row lies in the plane spanned by (front + ndcY h/2 up)
 // and right, whose normal is n(ndcY) = right x front + ndcY h/2 (right x up). If
 // all 8 corners of the root box lie strictly on one side of that plane, no ray of
-// the row can enter the box. The side test takes a margin of 1e-4 of the corner's
-// distance (an angle of 1e-4 rad, against the ~1e-6 rad by which getRay's float
-// rounding can tilt a ray out of the exact plane), so the conclusion holds for the
-// float rays too. n is linear in ndcY and the rows that meet a box form one band
+// the row can enter the box. The side test takes an angular margin so that the
+// conclusion holds for the float rays too: getRay forms P = pos + front + ... in
+// float and subtracts pos again, so a ray's direction is off the exact plane by up
+// to ~u (|pos| + |front| + w/2 |right| + h/2 |up|) / |P - pos| (u = 2^-24), which
+// grows with the camera's distance from the origin; the margin is 1e-4 rad plus 32
+// times that bound, with |P - pos| >= |front| for the orthogonal camera frames
+// updateCameraVectors makes (others get no band). The slab test's own rounding is
+// ~2u of the corner directions, inside the 1e-4. n is linear in ndcY and the rows that meet a box form one band
 // (the planes turn about the axis through pos along `right`), so the scan stops at
 // the first row from the top and from the bottom that may meet it.
 //
@@ -52,6 +56,14 @@ inline bool sky_band(const FlatCamera& cam, const float lo[3], const float hi[3]
         if (!std::isfinite(R[a]) || !std::isfinite(F[a]) || !std::isfinite(U[a]) || !std::isfinite(o[a])) return false;
     }
     if (!std::isfinite(h) || !(resY > 0) || height <= 0) return false;
+    auto dot = [](const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+    auto l1 = [](const double a[3]) { return std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]); };
+    const double fl = std::sqrt(dot(F, F)), rl = std::sqrt(dot(R, R)), ul = std::sqrt(dot(U, U));
+    // |P - pos| >= |front| needs right and up orthogonal to front (to 1e-3)
+    if (!(fl > 0) || std::fabs(dot(R, F)) > 1e-3 * rl * fl || std::fabs(dot(U, F)) > 1e-3 * ul * fl) return false;
+    const double w = h * std::fabs(static_cast<double>(cam.aspectRatio));
+    if (!std::isfinite(w)) return false;
+    const double ang = 1e-4 + 32.0 * 5.9604644775390625e-08 * (l1(o) + l1(F) + 0.5 * w * l1(R) + 0.5 * h * l1(U)) / fl;
     // per corner: s(ndcY) = a + ndcY b, the side of the corner; m its margin
     double ca[8], cb[8], cm[8];
     for (int k = 0; k < 8; ++k) {
@@ -69,7 +81,7 @@ inline bool sky_band(const FlatCamera& cam, const float lo[3], const float hi[3]
         if (!(nl > 0)) return false;
         int pos = 0, neg = 0;
         for (int k = 0; k < 8; ++k) {
-            const double s = ca[k] + ny * cb[k], m = 1e-4 * nl * cm[k] + 1e-9;
+            const double s = ca[k] + ny * cb[k], m = ang * nl * cm[k] + 1e-9;
             pos += s > m;
             neg += s < -m;
         }

@@ -36,10 +36,18 @@ int main() {
     std::uniform_real_distribution<float> u(-1, 1);
     long bad = 0, cases = 0, rows_total = 0, rows_sky = 0;
     const int W = 320, H = 180;
-    for (int it = 0; it < 3000; ++it) {
+    // 3000 cameras within 40 of the origin, 1500 at distances 1e3-1e5 looking at a
+    // box near it or near themselves (getRay's rounding grows with |pos|), some with a
+    // non-unit Front (the shader uses the uploaded vector as it is)
+    for (int it = 0; it < 4500; ++it) {
         FlatCamera cam{};
-        const V3 pos{40 * u(g), 40 * u(g), 40 * u(g)}, tgt{5 * u(g), 5 * u(g), 5 * u(g)};
-        const V3 f = norm(sub(tgt, pos)), r = norm(cross(f, V3{0, 1, 0})), up = norm(cross(r, f));
+        const bool far = it >= 3000;
+        const float dist = far ? std::pow(10.0f, 3.0f + 2.0f * (u(g) + 1) / 2) : 40.0f;
+        V3 pos{dist * u(g), dist * u(g), dist * u(g)}, tgt{5 * u(g), 5 * u(g), 5 * u(g)};
+        if (far && it % 2) tgt = add(pos, V3{30 * u(g), 30 * u(g), 30 * u(g)});  // a box near the camera
+        const float fs = far && it % 3 == 0 ? 0.5f + 2.5f * (u(g) + 1) / 2 : 1.0f;
+        const V3 fu = norm(sub(tgt, pos)), r = norm(cross(fu, V3{0, 1, 0})), up = norm(cross(r, fu));
+        const V3 f = mul(fs, fu);
         cam.Position = {pos.x, pos.y, pos.z};
         cam.Front = {f.x, f.y, f.z};
         cam.Right = {r.x, r.y, r.z};
@@ -47,10 +55,12 @@ int main() {
         cam.fov = 30 + 60 * (u(g) + 1) / 2;
         cam.aspectRatio = static_cast<float>(W) / H;
         float lo[3], hi[3];
+        const V3 bc = far && it % 2 ? tgt : V3{10 * u(g), 10 * u(g), 10 * u(g)};
+        const float cc[3] = {bc.x, bc.y, bc.z};
         for (int a = 0; a < 3; ++a) {
-            const float c = 10 * u(g), e = 0.1f + 10 * (u(g) + 1);
-            lo[a] = c - e;
-            hi[a] = c + e;
+            const float e = 0.1f + 10 * (u(g) + 1);
+            lo[a] = cc[a] - e;
+            hi[a] = cc[a] + e;
         }
         if (it % 7 == 0) lo[1] = hi[1] = 25.0f;  // a flat floor (zero-thickness box)
         int y0, y1;

@@ -670,3 +670,49 @@ def test_group_sky_rows_identical(ctx, ranks, share):
                     assert np.array_equal(g.render(W, H, 8), ref), f"bvh={bvh} sky_rows={on}"
     finally:
         g.close()
+
+
+def test_group_refuses_members_changed_behind_its_back(ctx):
+    """The sky-row band is computed from the group's camera and root box on every
+    rank. A member whose camera or node boxes were changed through its own context
+    would draw geometry in rows the band sends as sky, so with sky rows on the frame
+    is refused (RT_ERR_INVALID) before anything is posted; with sky rows off it is
+    that member's view; group calls make the members agree again. With the phase
+    events off, frames stay bounded by slot back-pressure and exact."""
+    W, H = 480, 270
+    base = rtamd.generate(3, 0, W, H)
+    sc = rtamd.Scene().generate(3, 0, W / H)
+    sc.LookAt((0.0, 30.0, 0.0))
+    other = sc.serializeScene().camera
+    g = rtamd.Group([0, 0], rtamd.GATHER_COPY, frames=2)
+    try:
+        g.upload(base)
+        g.set_params(W, H, 3, True)
+        ctx.upload(base)
+        ctx.set_params(W, H, 3, True)
+        assert np.array_equal(g.render(W, H, 8), ctx.render(W, H))
+        for m in g.contexts:
+            m.set_camera(other)
+        with pytest.raises(rtamd.RTError) as e:
+            g.dispatch(W, H, 8)
+        assert e.value.code == -1
+        ctx.set_camera(other)
+        want = ctx.render(W, H)
+        g.set_sky_rows(False)
+        assert np.array_equal(g.render(W, H, 8), want)
+        g.set_sky_rows(True)
+        g.set_camera(other)
+        assert np.array_equal(g.render(W, H, 8), want)
+        nodes = base.nodes.copy()
+        nodes["boundsMax"][-1] += np.float32(1.0)
+        g.members[1].update_nodes(nodes)
+        with pytest.raises(rtamd.RTError):
+            g.dispatch(W, H, 8)
+        g.set_sky_rows(False)
+        g.set_phase_timing(False)
+        for _ in range(6):
+            g.dispatch(W, H, 8)
+        g.sync()
+        assert np.array_equal(g.read_image(W, H), want)
+    finally:
+        g.close()

@@ -231,3 +231,64 @@ def test_update_then_animate_and_readback(ctx):
             assert np.array_equal(got[f].view(np.uint32), host.nodes[f].view(np.uint32)), (k, f)
         want, _ = oracle.render(host, W, H, oracle.params(W, H, 1))
         check(ctx.render(W, H), want, f"frame {k}")
+
+
+def test_kernel_timing_off_reports_nothing(ctx):
+    """rt_set_kernel_timing(0): a dispatch records no events, and rt_last_kernel_ms
+    refuses (RT_ERR_INVALID) instead of returning an earlier dispatch's time."""
+    W, H = 64, 48
+    fs = rtamd.generate(2, 0, W, H)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 1, True)
+    ctx.set_kernel_timing(1)
+    ctx.render(W, H)
+    assert ctx.last_kernel_ms() > 0
+    ctx.set_kernel_timing(0)
+    try:
+        ctx.render(W, H)
+        with pytest.raises(rtamd.RTError):
+            ctx.last_kernel_ms()
+        ctx.set_params(W, H, 1, False)  # the brute-force sub-context's path too
+        ctx.render(W, H)
+        with pytest.raises(rtamd.RTError):
+            ctx.last_kernel_ms()
+    finally:
+        ctx.set_kernel_timing(1)
+
+
+@pytest.mark.parametrize("mode", ["mt", "brute", "mt_brute"])
+def test_animated_mt_and_brute_frames_refit(ctx, fresh, mode):
+    """Moller-Trumbore and brute-force frames of an animated scene: the sub-contexts
+    (the MT accelerator, the one-leaf brute tree) follow rt_animate / rt_update_shapes
+    by the same device refit (MT: boxes, cones and per-ray padding constants merged
+    grow-only, the axis slab dropped) instead of the literal scan or a rebuild. Every
+    frame equals a fresh upload of the same scene (the accelerator built from scratch)
+    bit for bit, and the oracle at the end."""
+    W, H = 192, 108
+    fs = rtamd.generate(3, 0, W, H)
+    ids, frames = bench.wheel_frames(fs, 8)
+    mt, bvh = "mt" in mode, mode != "brute" and mode != "mt_brute"
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3, bvh, False, mt)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    ctx.set_animated(ids)
+    host = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    ctx.render(W, H)  # the sub-context exists from here on
+    for k in range(8):
+        ctx.animate(frames[k])
+        host.shapes[ids] = frames[k]
+        oracle.update_bvh(host, ids)
+        fresh.upload(host)
+        fresh.set_params(W, H, 3, bvh, False, mt)
+        fresh.set_kernel(rtamd.KERNEL_AUTO)
+        same(ctx.render(W, H), fresh.render(W, H), f"{mode} frame {k}")
+    assert ctx.accel_info()["last_kernel"] == rtamd.KERNEL_ACCEL
+    want, _ = oracle.render(host, W, H, oracle.params(W, H, 3, bvh, False, mt))
+    check(ctx.render(W, H), want, f"{mode} vs oracle")
+    # the reference's own upload on the same context (no rt_animate): MT / brute too
+    ctx.set_animated(np.zeros(0, np.int32))
+    ru = rtamd.ReferenceUpload(host, ids)
+    for k in range(4):
+        ru.upload(ctx, frames[(k + 3) % 8])
+        fresh.upload(ru.scene(host))
+        same(ctx.render(W, H), fresh.render(W, H), f"{mode} reference upload {k}")
