@@ -58,6 +58,14 @@ int rth_render_loop_ref(struct rt_ctx* ctx, const FlatCamera* cams, int ncams, c
                         int num_shapes, const int* ids, int count, const FlatShape* anim, int anim_frames,
                         FlatNode* nodes, int num_nodes, const int* indices, int num_indices, double* frame_ms);
 
+/* rth_render_loop over one rank's rows of a split frame (rt_dispatch_rows_ex: compact
+ * row r is image row y0 + (r / stripe) * period + r % stripe, out_rows of them, in
+ * rt_format `format`): the per-rank floor of a multi-GPU frame (rt_group.h), timed
+ * like the single-GPU loop. */
+int rth_render_rows_loop(struct rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
+                         int height, int y0, int stripe, int period, int out_rows, int format, float* dst,
+                         size_t pitch, int frames, int wait_each, double* frame_ms);
+
 #ifdef __cplusplus
 }
 #endif

@@ -231,37 +231,4 @@ RTA_HD bool mt_slab(float ox, float oy, float oz, float on, const RayC& c, const
     return !(lo > hi + 1e-4f * std::fabs(hi) + 1e-6f);
 }
 
-// The floor case of mt_pad as per-child constants (AccelPtrs::mtfloor, 8 floats
-// per child): a ray with |d| <= kMtDmax whose cone term leaves A at the 1e-5 floor
-// (D max(cn, 0) m0 <= 1e-5, every ray of a child whose cone straddles its
-// direction) gets a pad, q2 and pt linear in so = |o - Z| and a fixed lf / ilf.
-// o = {pad0, pad1, q20, q21, pt0, pt1, lf, ilf}: pad <= pad0 + pad1 so, q2 <= q20 +
-// q21 so, pt <= pt0 + pt1 so, lf <= lf, ilf >= ilf for every such ray, mt_pad's own
-// float values included (the constants carry a 1e-5 relative margin above the
-// double evaluation of mt_pad's formula at D = kMtDmax, beyond its float rounding).
-// lf = 0: the floor gives no finite bound (mt_pad returns false: entered at 0).
-// The walks take it when every lane of a wave is in the floor case for the child
-// (a wave-uniform test): no per-lane reciprocal or product chain.
-constexpr float kMtDmax = 1.0001f;
-RTA_HD void mt_floor(const float* m, float* o) {
-    for (int i = 0; i < 8; ++i) o[i] = 0.0f;
-    const double D = kMtDmax, up = 1.0 + 1e-5, m1 = m[1];
-    const double A = static_cast<double>(1e-5f) - 7.0 * D * m1 * up;  // mt_pad's floor A, from below
-    if (!(A > 2.5e-6 * up) || !(m1 >= 0.0) || !(m[2] >= 0.0f) || !(m[3] >= 0.0f)) return;
-    const double ia = 1.0001 / A * up;
-    const double r = 7.07 * D * m1 * ia + 3.0 * 5.9604644775390625e-08;
-    if (!(r < 0.5 / up)) return;
-    const double lf = 1.0001 / (1.0 - r) * up;
-    const double ilf = (1.0 - r) * 0.99989 / up;
-    // q = D m1 (18 so + m3) ia; dl = 9.09 m1 (so + m2) ia; q2 = 2q; pt = 2 D dl lf
-    const double q20 = 2.0 * D * m1 * m[3] * ia * up, q21 = 36.0 * D * m1 * ia * up;
-    const double pt0 = 18.18 * D * m1 * m[2] * ia * lf * up, pt1 = 18.18 * D * m1 * ia * lf * up;
-    const double v[8] = {(q20 + pt0) * up, (q21 + pt1) * up, q20, q21, pt0, pt1, lf, ilf};
-    for (int i = 0; i < 8; ++i) o[i] = static_cast<float>(v[i]);
-    // rounding to float: the bounds from above up, ilf down
-    for (int i = 0; i < 7; ++i) o[i] = nextafterf(o[i], INFINITY);
-    o[7] = nextafterf(o[7], 0.0f);
-    if (!(o[0] < 1e30f && o[1] < 1e30f)) o[6] = 0.0f;
-}
-
 }  // namespace rta

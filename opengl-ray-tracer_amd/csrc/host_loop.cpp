@@ -49,9 +49,13 @@ struct RefUpload {  // rth_render_loop_ref's scene, moved by the reference's upl
     int num_indices;
 };
 
+struct Rows {  // the rows one dispatch renders (rt_dispatch_rows_ex)
+    int y0, stripe, period, out_rows, format;
+};
+
 int render_loop(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width, int height,
                 float* dst, size_t pitch, int frames, int wait_each, const FlatShape* anim, int anim_count,
-                int anim_frames, const RefUpload* ref, double* frame_ms) {
+                int anim_frames, const RefUpload* ref, double* frame_ms, const Rows* rows = nullptr) {
     if (!ctx || !cams || ncams < 1 || !light || !dst || frames < 0 || !frame_ms) return RT_ERR_INVALID;
     if (anim && (anim_count < 1 || anim_frames < 1)) return RT_ERR_INVALID;
     using clk = std::chrono::steady_clock;
@@ -66,7 +70,10 @@ int render_loop(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight*
             rc = rth_upload_animated(ctx, ref->shapes, ref->num_shapes, ref->ids,
                                      ref->anim + static_cast<size_t>(i % ref->anim_frames) * ref->count, ref->count,
                                      ref->nodes, ref->num_nodes, ref->indices, ref->num_indices);
-        if (rc == RT_OK) rc = rt_dispatch_rows(ctx, width, height, 0, 1, 1, height, dst, pitch);  // dispatch
+        if (rc == RT_OK)  // dispatch
+            rc = rows ? rt_dispatch_rows_ex(ctx, width, height, rows->y0, rows->stripe, rows->period, rows->out_rows,
+                                            dst, pitch, rows->format)
+                      : rt_dispatch_rows(ctx, width, height, 0, 1, 1, height, dst, pitch);
         if (rc == RT_OK && wait_each) rc = rt_sync(ctx);                                       // the frame's end
         if (rc != RT_OK) return rc;
         if (wait_each) frame_ms[i] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
@@ -103,4 +110,12 @@ extern "C" int rth_render_loop_ref(rt_ctx* ctx, const FlatCamera* cams, int ncam
     const RefUpload ref{shapes, num_shapes, ids, count, anim, anim_frames, nodes, num_nodes, indices, num_indices};
     return render_loop(ctx, cams, ncams, light, width, height, dst, pitch, frames, wait_each, nullptr, 0, 0, &ref,
                        frame_ms);
+}
+
+extern "C" int rth_render_rows_loop(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight* light, int width,
+                                    int height, int y0, int stripe, int period, int out_rows, int format, float* dst,
+                                    size_t pitch, int frames, int wait_each, double* frame_ms) {
+    const Rows rows{y0, stripe, period, out_rows, format};
+    return render_loop(ctx, cams, ncams, light, width, height, dst, pitch, frames, wait_each, nullptr, 0, 0, nullptr,
+                       frame_ms, &rows);
 }

@@ -576,7 +576,6 @@ struct AccelPtrs {
     int split_g;                        // ... over groups of at most this many lanes (a power of two)
     const int* __restrict__ prim_shape; // shape index per prim slot (the winner's material)
     float mt_z[3];                      // AccelHost::mt_z (Moller-Trumbore per-ray padding)
-    const float4* __restrict__ mtfloor; // MT: per wide node 4 x 2 float4, mt_pad's floor case per child (mt_floor)
 };
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
@@ -910,9 +909,6 @@ __host__ __device__ __forceinline__ float* wide_box_f(float4* lnodes, int rec, i
     return rec == kWideRecMt ? base + 16 * sl + comp : base + 4 * comp + sl;
 }
 
-#ifndef RT_MT_FLOOR
-#define RT_MT_FLOOR 1  // MT child test: 0 per-lane mt_pad only; 1 / 2 the wave-uniform floor case (2: no slab there)
-#endif
 
 template <bool MT = false>
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
@@ -933,43 +929,22 @@ __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, cons
         h[0] = h[1] = h[2] = h[3] = false;
         cc[0] = __float_as_int(cd.x), cc[1] = __float_as_int(cd.y), cc[2] = __float_as_int(cd.z);
         cc[3] = __float_as_int(cd.w);
-        const float4* fq = A.mtfloor + 8 * static_cast<size_t>(uc & 0x3fffffffu);
 #pragma unroll kMtUnroll
         for (int s2 = 0; s2 < 4; ++s2) {
             const float4 f0 = q[4 * s2], f1 = q[4 * s2 + 1], f2v = q[4 * s2 + 2], f3 = q[4 * s2 + 3];
             const float k[4] = {f1.z, f1.w, f2v.x, f2v.y};
             const float m[6] = {f2v.z, f2v.w, f3.x, f3.y, f3.z, f3.w};
             float pad, lf, q2, pt, ilf, tt = 0.0f;
-            bool hh = true, ok, slab = true;
-#if RT_MT_FLOOR
-            // mt_pad's floor case for every lane of the wave (the child's cone straddles
-            // the rays' directions: the top levels of the car's tree for every camera
-            // ray): the child's precomputed constants (mt_floor), no per-lane chain
-            const float cn0 = std::fabs(std::fma(k[0], c.dx, std::fma(k[1], c.dy, k[2] * c.dz))) - k[3];
-            const bool floor_lane = c.dlen <= rta::kMtDmax && !(c.dlen * std::fmax(cn0, 0.0f) * m[0] > 1e-5f);
-            if (__ballot(in && !floor_lane) == 0) {
-                const float4 fa = fq[2 * s2], fb = fq[2 * s2 + 1];
-                ok = fb.z > 0.0f;
-                pad = std::fma(fa.y, c.so, fa.x);
-                lf = fb.z;
-                ilf = fb.w;
-#if RT_MT_FLOOR == 1
-                q2 = std::fma(fa.w, c.so, fa.z);
-                pt = std::fma(fb.y, c.so, fb.x);
-#else
-                q2 = pt = 0.0f;
-                slab = false;  // the slab is a further cut only: skipped in the floor case
-#endif
-            } else
-#endif
-            {
-                ok = rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt, ilf);
-            }
+            bool hh = true;
+            // (r05: a wave-uniform floor case of mt_pad from per-child constants spilled
+            // 28 VGPRs in the production MT instance: car MT frame 1.293 -> 1.455 ms in
+            // flight, 1.577 without its slab; profiles/r05e_abf_floor*.json. Not kept.)
+            const bool ok = rta::mt_pad(c, c.so, k, m, pad, lf, q2, pt, ilf);
             if (ok) {
                 float tn, tf;
                 hh = rta::box_span(c, f0.x - pad, f0.y - pad, f0.z - pad, f0.w + pad, f1.x + pad, f1.y + pad,
                                    tl * lf, tn, tf);
-                if (hh && slab && c.ix != 0.0f && m[5] < 3e38f)
+                if (hh && c.ix != 0.0f && m[5] < 3e38f)
                     hh = rta::mt_slab(c.mox, c.moy, c.moz, c.on, c, k, m, q2, pt, tn, tf);
 #if RT_MT_ILF
                 tt = tn * ilf;  // the stack's prune compares with tl, not tl * lf (ilf <= 1 / lf)
@@ -2079,7 +2054,6 @@ struct AnimOut {
     float origin_lim;
     int mt;                           // the accelerator's wide nodes: kWideRecMt float cones, else kWideRec
     float mt_z[3];                    // MT accelerators: AccelHost::mt_z (the per-ray padding's centre Z)
-    float4* mtfloor;                  // MT accelerators: mt_pad's floor case per wide child (AccelPtrs::mtfloor)
 };
 
 // One refit launch (k_refit) of flush_updates: what it reads from the pinned ring
@@ -2369,13 +2343,6 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
         k[3] = fmaxf(k[3], static_cast<float>((18.0 * mm + 10.5 * es) * up + 1e-5));
     }
     k[5] = INFINITY;
-    if (o.mtfloor) {  // the floor-case constants follow the merged ones
-        float f8[8];
-        rta::mt_floor(k, f8);
-        float4* fq = o.mtfloor + 8 * static_cast<size_t>(w) + 2 * sl;
-        fq[0] = make_float4(f8[0], f8[1], f8[2], f8[3]);
-        fq[1] = make_float4(f8[4], f8[5], f8[6], f8[7]);
-    }
 }
 
 // The per-frame refit of flush_updates, in one-wave workgroups with four roles:
@@ -2467,7 +2434,6 @@ struct rt_ctx {
     std::vector<FlatShape> host_shapes;
     // exact-result accelerator (accel.h); device copies in the layouts of AccelPtrs
     float4 *anodes = nullptr, *lnodes = nullptr, *wnodes = nullptr, *prims = nullptr;
-    float4* mtfloor = nullptr;  // MT accelerator: mt_pad's floor case per wide child (AccelPtrs::mtfloor)
     int4* tleaf = nullptr;
     float4* titems = nullptr;  // scene-tree items (AccelPtrs::titems)
     int* titem_ref = nullptr;  // per titems record: its reference leaf (device copy)
@@ -2630,8 +2596,6 @@ void free_accel(rt_ctx* c) {
     hipFree(c->anodes);
     hipFree(c->lnodes);
     hipFree(c->wnodes);
-    hipFree(c->mtfloor);
-    c->mtfloor = nullptr;
     hipFree(c->tleaf);
     hipFree(c->titems);
     c->titems = nullptr;
@@ -2790,21 +2754,6 @@ int build_upload_accel(rt_ctx* c) {
     for (size_t w = 0; w < nw; ++w)
         emit_wide(w, w, A.wchild, A.wsub, A.lbox, A.lcone, [&](int j) { return leaf_code(static_cast<size_t>(j)); },
                   0);
-    // MT: per wide child the floor case of mt_pad as constants (accel_math.h mt_floor)
-    std::vector<float4> mf;
-    if (A.mt) {
-        mf.assign(8 * (nw ? nw : 1), make_float4(0.f, 0.f, 0.f, 0.f));
-        for (size_t w = 0; w < nw; ++w)
-            for (int s2 = 0; s2 < 4; ++s2) {
-                const int j = A.wchild[rta::kWide * w + s2];
-                float o8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (j >= 0) rta::mt_floor(&A.lmt[rta::kMtPadF * static_cast<size_t>(j)], o8);
-                mf[8 * w + 2 * s2] = make_float4(o8[0], o8[1], o8[2], o8[3]);
-                mf[8 * w + 2 * s2 + 1] = make_float4(o8[4], o8[5], o8[6], o8[7]);
-            }
-        if (hipMalloc(&c->mtfloor, mf.size() * sizeof(float4)) != hipSuccess) return RT_ERR_NO_MEMORY;
-        HIP_TRY(hipMemcpyAsync(c->mtfloor, mf.data(), mf.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-    }
     // Items: with <= 8 distinct reference leaves (few-leaf mode, few_mask) a
     // local-leaf code kLocal|kLeaf|kItem|start<<6|leaf<<3|count and titems =
     // the leaves' exact boxes; otherwise kTopLeaf|kItem|item and titems = per
@@ -3345,7 +3294,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                               acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
                               acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
                               c->accel.origin_lim, c->accel.mt ? 1 : 0,
-                              {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}, acc ? c->mtfloor : nullptr};
+                              {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}};
             if (!c->refit_ctr) {
                 if (hipMalloc(&c->refit_ctr, 2 * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
                 HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, 2 * sizeof(unsigned), c->stream));
@@ -3818,7 +3767,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
                           c->scene_stack > 0 ? c->scene_stack : kMaxStack, c->nfew, kp.N, c->accel.origin_lim,
                           c->boxes_finite, c->split_max, c->split_g, c->prim_idx_dev,
-                          {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}, c->mtfloor};
+                          {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}};
         // compaction: bounces >= tail_from of the rays still alive run in k_accel_tail
         k2.tail_queue = nullptr;
         // RT_TAIL_AUTO: from bounce 2 on scenes of many scene-tree items (measured: config 5's

@@ -182,6 +182,7 @@ HOST_SYMBOLS = {
     "rth_render_loop": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P]),
     "rth_render_loop_anim": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _I, _P]),
     "rth_upload_animated": (_I, [_P, _P, _I, _P, _P, _I, _P, _I, _P, _I]),
+    "rth_render_rows_loop": (_I, [_P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I, _I, _P]),
     "rth_render_loop_ref": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _P, _I, _P, _I, _P, _I,
                                  _P, _I, _P]),
 }
@@ -353,6 +354,21 @@ def render_loop(ctx, cams, light, width, height, dst_ptr, pitch, frames, wait_ea
                                         _ptr(out))
     if rc != 0:
         raise RTError("rth_render_loop", rc)
+    return out if wait_each else out[:1]
+
+
+def render_rows_loop(ctx, cams, light, width, height, y0, stripe, period, out_rows, dst_ptr, pitch, frames,
+                     wait_each=True, fmt=FORMAT_RGB32F):
+    """rth_render_rows_loop: rth_render_loop over one rank's rows (rt_dispatch_rows_ex).
+    Returns the host wall times in ms: one per frame, or [total] when not waiting."""
+    cams = as_records(np.asarray(cams), CAMERA_DTYPE).reshape(-1)
+    light = as_records(np.asarray(light), LIGHT_DTYPE).reshape(1)
+    out = np.zeros(max(1, frames), np.float64)
+    rc = host_lib().rth_render_rows_loop(ctx._h, _ptr(cams), len(cams), _ptr(light), int(width), int(height), int(y0),
+                                         int(stripe), int(period), int(out_rows), int(fmt), C.c_void_p(dst_ptr),
+                                         int(pitch), int(frames), int(bool(wait_each)), _ptr(out))
+    if rc != 0:
+        raise RTError("rth_render_rows_loop", rc)
     return out if wait_each else out[:1]
 
 

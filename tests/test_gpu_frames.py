@@ -705,7 +705,8 @@ def test_group_refuses_members_changed_behind_its_back(ctx):
         assert np.array_equal(g.render(W, H, 8), want)
         nodes = base.nodes.copy()
         nodes["boundsMax"][-1] += np.float32(1.0)
-        g.members[1].update_nodes(nodes)
+        for m in g.contexts[g.frames:2 * g.frames]:  # every frame slot of member 1
+            m.update_nodes(nodes)
         with pytest.raises(rtamd.RTError):
             g.dispatch(W, H, 8)
         g.set_sky_rows(False)
