@@ -329,7 +329,6 @@ struct Cone {
     bool full() const { return theta >= 1.5; }
 };
 
-const double kConeMargin = 2e-3;  // radians beyond float error of N.d and of the cone test
 Cone full_cone() { return Cone{{0, 0, 0}, 10.0}; }
 
 // The INNER-capable normal of a shape: np = N.d must be > 0 for plane, wall

@@ -32,6 +32,7 @@ namespace rta {
 
 constexpr float kInvCap = 1e20f;     // |1/d| clamp of the padded slab test
 constexpr float kConeEps = 1e-5f;    // rounding allowance of the cone test (the margin is 2e-3 rad)
+constexpr double kConeMargin = 2e-3;  // radians beyond float error of N.d and of the cone test (build_cones)
 constexpr float kPruneRel = 1.002f;  // distance margin for skipping a box
 
 struct RayC {
@@ -84,8 +85,9 @@ RTA_HD int ray_dq(float dx, float dy, float dz) {
     return b(dx) | (b(dy) << 8) | (b(dz) << 16) | static_cast<int>(0x80000000u);
 }
 
-// Host: the cone word of a float cone (axis, thr) as AccelHost holds it.
-inline int cone_word(float ax, float ay, float az, float thr) {
+// The cone word of a float cone (axis, thr) as AccelHost holds it (the host's
+// build, the device's refit).
+RTA_HD int cone_word(float ax, float ay, float az, float thr) {
     if (thr <= -6.0f) return kConeNp;  // kNoPrune (accel.h)
     const double t = std::floor((16129.0 * static_cast<double>(thr) - 222.0) / 128.0);
     if (!(t > -128.0) || !std::isfinite(ax) || !std::isfinite(ay) || !std::isfinite(az)) return kConeNever;

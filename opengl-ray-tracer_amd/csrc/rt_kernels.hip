@@ -2033,7 +2033,6 @@ struct AnimMaps {
     const int *wn_off, *wn_list, *item_off, *item_list;
     const int* ecls;       // per entry: its class when the accelerator was built (accel_bound.h)
     const int* prim_entry; // per accelerator prim: its shape's refit entry, -1 if none
-    const float4* enorm;   // per entry: that record's stored normal (xyz) and type (w, int bits)
     int count, nodes;
 };
 // the per-frame flag of a refit entry: the nodes listing it grow to hold it
@@ -2054,6 +2053,8 @@ struct AnimOut {
     float origin_lim;
     int mt;                           // the accelerator's wide nodes: kWideRecMt float cones, else kWideRec
     float mt_z[3];                    // MT accelerators: AccelHost::mt_z (the per-ray padding's centre Z)
+    const int* prim_shape;            // accelerator: shape index per prim (AccelPtrs::prim_shape)
+    int cone_cull;                    // rt_debug_cone_cull: 0 keeps every cone full
 };
 
 // One refit launch (k_refit) of flush_updates: what it reads from the pinned ring
@@ -2089,8 +2090,7 @@ __device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
 // build (a triangle collapsing to a sliver, a sphere going infinite) gets an
 // infinite conservative box, so every box above it is entered and it is tested like
 // an always-tested shape -- the frame stays exact -- and `report` asks the host to
-// rebuild the accelerator for speed. A moved stored normal drops the back-face
-// cones above the shape (they were built from the old normals).
+// rebuild the accelerator for speed. The cones above the shape are the slot role's.
 // The conservative box an entry's current record contributes to the boxes above it
 // (b): its classify() box; empty if it was always tested since the build (no box
 // above it); infinite if its bound changed kind since (every box above it then
@@ -2129,23 +2129,6 @@ __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArg
         const int p = m.prim_list[q];
         store_prim(o.prims, p, pack_prim(g, o.prim_seq[p]));  // rank in the reference walk (k_pack_prims)
     }
-    const float4 bn = m.enorm[i];
-    const int btype = __float_as_int(bn.w);
-    // barycentric cones hold the stored normals (the INNER test's N); an MT cone holds
-    // the vertices' normals, which any move of a refit entry may turn
-    const bool cone = o.mt || s.type != btype ||
-                      ((s.type == RT_WALL || s.type == RT_TRIANGLE) &&
-                       (__float_as_int(s.planeNormal.x) != __float_as_int(bn.x) ||
-                        __float_as_int(s.planeNormal.y) != __float_as_int(bn.y) ||
-                        __float_as_int(s.planeNormal.z) != __float_as_int(bn.z)));
-    if (cone)
-        for (int q = m.wpos_off[i]; q < m.wpos_off[i + 1]; ++q) {  // the back-face cones no longer hold
-            const int w = m.wpos_list[q] >> 2, sl = m.wpos_list[q] & 3;
-            if (o.mt)
-                wide_box_f(o.lnodes, kWideRecMt, w, sl, 0)[9] = 2.f;  // s: a full cone (mt_pad's floor)
-            else  // never cull
-                reinterpret_cast<int*>(o.lnodes + kWideRec * static_cast<size_t>(w) + 6)[sl] = rta::kConeNever;
-        }
     rta::Box3 b;
     const int was = m.ecls[i];
     if (entry_cbox(o, s, was, b)) *r.report = 1;  // the host rebuilds at its next flush
@@ -2279,6 +2262,171 @@ __device__ void set_node(const AnimOut& o, const RefitArgs& r, int k) {
     }
 }
 
+// The current record of the shape of accelerator prim p, for the slot role: the
+// staging copy (which the record role has brought up to date), or with `direct` a
+// moved shape's record itself.
+__device__ __forceinline__ const FlatShape& slot_shape(const AnimMaps& m, const AnimOut& o, const RefitArgs& r,
+                                                       int p) {
+    const int e = r.direct ? m.prim_entry[p] : -1;
+    return e >= 0 ? r.fresh[e] : o.shapes[o.prim_shape[p]];
+}
+
+// The slot role's back-face cone (barycentric accelerators, accel.cpp build_cones
+// and shape_cone): moved walls and triangles turn their stored normals (a wheel's),
+// so the child's cone is recomputed from the current records below: axis = the unit
+// normals' sum, half angle = the largest angle to the stored (float) axis, plus
+// kConeMargin; any other shape or a normal sum near 0 makes it full. A child whose
+// cone is full already (kConeNever: the build found it so, or culling is off) keeps
+// it -- a word that never culls always holds -- which spares the large subtrees
+// near the roots a pass over their prims.
+__device__ void refit_slot_cone(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int4 d, int w, int sl,
+                                int lane) {
+    int* cw = reinterpret_cast<int*>(o.lnodes + kWideRec * static_cast<size_t>(w) + 6) + sl;
+    if (*cw == rta::kConeNever) return;  // the same word for the whole wave
+    auto unit_normal = [](const FlatShape& s, double n[3]) {
+        if (s.type != RT_WALL && s.type != RT_TRIANGLE) return false;
+        n[0] = s.planeNormal.x, n[1] = s.planeNormal.y, n[2] = s.planeNormal.z;
+        const double l = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        if (!(l > 1e-20) || !isfinite(l)) return false;
+        for (int a = 0; a < 3; ++a) n[a] /= l;
+        return true;
+    };
+    double sn[3] = {0, 0, 0};
+    int full = 0;
+    for (int p = d.y + lane; p < d.z; p += 64) {
+        double n[3];
+        if (!unit_normal(slot_shape(m, o, r, p), n)) {
+            full = 1;
+            continue;
+        }
+        for (int a = 0; a < 3; ++a) sn[a] += n[a];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        for (int a = 0; a < 3; ++a) sn[a] += __shfl_xor(sn[a], off);
+        full |= __shfl_xor(full, off);
+    }
+    const double l = sqrt(sn[0] * sn[0] + sn[1] * sn[1] + sn[2] * sn[2]);
+    if (full || !(l > 1e-6) || d.y >= d.z) {
+        if (lane == 0) *cw = rta::kConeNever;
+        return;
+    }
+    float af[3];  // the axis as lane 0 rounds it (the butterfly's sums may differ in the last bits)
+    for (int a = 0; a < 3; ++a) af[a] = __shfl(static_cast<float>(sn[a] / l), 0);
+    const double al = sqrt(static_cast<double>(af[0]) * af[0] + static_cast<double>(af[1]) * af[1] +
+                           static_cast<double>(af[2]) * af[2]);
+    double cmin = 1.0;  // the smallest cosine to the axis
+    for (int p = d.y + lane; p < d.z; p += 64) {
+        double n[3];
+        unit_normal(slot_shape(m, o, r, p), n);
+        cmin = fmin(cmin, (n[0] * af[0] + n[1] * af[1] + n[2] * af[2]) / al);
+    }
+    for (int off = 32; off > 0; off >>= 1) cmin = fmin(cmin, __shfl_xor(cmin, off));
+    if (lane != 0) return;
+    const double t = acos(fmax(-1.0, fmin(1.0, cmin))) + rta::kConeMargin;
+    *cw = t >= 1.5707 ? rta::kConeNever : rta::cone_word(af[0], af[1], af[2], static_cast<float>(-sin(t)));
+}
+
+// The slot role's Moller-Trumbore part (MT accelerators have local trees only):
+// the child's grazing cone, per-ray padding constants and slab (accel.cpp
+// build_cones_mt), recomputed from the current records of every triangle below,
+// since a refit moves and turns them (a wheel's). Two passes over the slot's prims:
+// the normals' sum (each flipped towards the old axis) gives the new axis, stored as
+// float; then s = the largest min(|n - a|, |n + a|) against that stored axis (for
+// any a, |d.n| >= |d.a| - |n -+ a|: what mt_pad's cone term needs) and the slab of
+// a . vertex. The constants take the worst triangle as the build's do, without its
+// grow-only margin. A shape other than a bounded triangle below: no slab, as built.
+__device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int4 d, int w, int sl,
+                              int lane) {
+    float* k = wide_box_f(o.lnodes, kWideRecMt, w, sl, 0) + 6;  // axis xyz, s, {cr, u X, M, 18 M + 10.5 Esum, w, h0}
+    const double a0[3] = {k[0], k[1], k[2]};                      // every lane reads before lane 0 writes
+    auto shape_of = [&](int p) -> const FlatShape& { return slot_shape(m, o, r, p); };
+    auto tri_normal = [](const FlatShape& s, double n[3]) {  // accel.cpp mt_normal, with |e1 x e2|
+        const float e1[3] = {s.triP2.x - s.triP1.x, s.triP2.y - s.triP1.y, s.triP2.z - s.triP1.z};
+        const float e2[3] = {s.triP3.x - s.triP1.x, s.triP3.y - s.triP1.y, s.triP3.z - s.triP1.z};
+        n[0] = static_cast<double>(e1[1]) * e2[2] - static_cast<double>(e1[2]) * e2[1];
+        n[1] = static_cast<double>(e1[2]) * e2[0] - static_cast<double>(e1[0]) * e2[2];
+        n[2] = static_cast<double>(e1[0]) * e2[1] - static_cast<double>(e1[1]) * e2[0];
+        const double l = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+        for (int a = 0; a < 3; ++a) n[a] /= l;
+    };
+    double sn[3] = {0, 0, 0}, cr = INFINITY, X = 0, es = 0, mm = 0;
+    int other = 0;
+    for (int p = d.y + lane; p < d.z; p += 64) {
+        const FlatShape& s = shape_of(p);
+        rta::MtTri t;
+        rta::Box3 tb;
+        if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) {
+            other = 1;
+            continue;
+        }
+        double n[3];
+        tri_normal(s, n);
+        const double sg = n[0] * a0[0] + n[1] * a0[1] + n[2] * a0[2] < 0 ? -1.0 : 1.0;
+        for (int a = 0; a < 3; ++a) sn[a] += sg * n[a];
+        const double dz[3] = {t.p1[0] - o.mt_z[0], t.p1[1] - o.mt_z[1], t.p1[2] - o.mt_z[2]};
+        cr = fmin(cr, t.cr);
+        X = fmax(X, t.X);
+        es = fmax(es, t.esum);
+        mm = fmax(mm, sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        for (int a = 0; a < 3; ++a) sn[a] += __shfl_xor(sn[a], off);
+        cr = fmin(cr, __shfl_xor(cr, off));
+        X = fmax(X, __shfl_xor(X, off));
+        es = fmax(es, __shfl_xor(es, off));
+        mm = fmax(mm, __shfl_xor(mm, off));
+        other |= __shfl_xor(other, off);
+    }
+    // the axis as lane 0 rounds it (the butterfly's sums may differ in the last bits)
+    const double l = sqrt(sn[0] * sn[0] + sn[1] * sn[1] + sn[2] * sn[2]);
+    const bool full = !(l > 1e-6) || !(X > 0);  // no triangle, or normals cancelling: a full cone
+    float af[3];
+    for (int a = 0; a < 3; ++a) af[a] = __shfl(full ? static_cast<float>(a0[a]) : static_cast<float>(sn[a] / l), 0);
+    double sm = 0, lo = INFINITY, hi = -INFINITY;
+    for (int p = d.y + lane; p < d.z && !full; p += 64) {
+        const FlatShape& s = shape_of(p);
+        rta::MtTri t;
+        rta::Box3 tb;
+        if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) continue;
+        double n[3], dm = 0, dp = 0;
+        tri_normal(s, n);
+        for (int a = 0; a < 3; ++a) {
+            dm += (n[a] - af[a]) * (n[a] - af[a]);
+            dp += (n[a] + af[a]) * (n[a] + af[a]);
+        }
+        sm = fmax(sm, sqrt(fmin(dm, dp)));
+        for (const rt_vec3& v : {s.triP1, s.triP2, s.triP3}) {
+            const double x = static_cast<double>(af[0]) * v.x + static_cast<double>(af[1]) * v.y +
+                             static_cast<double>(af[2]) * v.z;
+            lo = fmin(lo, x);
+            hi = fmax(hi, x);
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sm = fmax(sm, __shfl_xor(sm, off));
+        lo = fmin(lo, __shfl_xor(lo, off));
+        hi = fmax(hi, __shfl_xor(hi, off));
+    }
+    if (lane != 0) return;
+    const double up = 1.0 + 1e-5, sv = sm * (1.0 + 1e-6) + 2e-5;
+    k[0] = af[0], k[1] = af[1], k[2] = af[2];
+    // build_cones_mt: theta >= 1.5 is a full cone; so is every cone with culling off (the build's)
+    k[3] = full || sv >= 1.3633 || !o.cone_cull ? 2.f : static_cast<float>(sv);
+    if (!(X > 0)) {  // no triangle below: pad 0, no slab
+        for (int a = 4; a < 9; ++a) k[a] = 0.f;
+        k[9] = INFINITY;
+        return;
+    }
+    k[4] = static_cast<float>(cr * (1.0 - 1e-5));
+    k[5] = static_cast<float>(rta::kU * X * up);
+    k[6] = static_cast<float>(mm * up + 1e-5);
+    k[7] = static_cast<float>((18.0 * mm + 10.5 * es) * up + 1e-5);
+    const bool slab = !full && !other && lo <= hi;
+    const double wc = slab ? 0.5 * (lo + hi) : 0.0;
+    k[8] = static_cast<float>(wc);
+    k[9] = slab ? static_cast<float>(0.5 * (hi - lo) * up + 1e-5 * (fabs(wc) + 1.0)) : INFINITY;
+}
+
 // Slot role: exact refit of the local / scene-tree boxes above moved prims (they
 // are the accelerator's own, so unlike the reference nodes they may shrink): one
 // wave per dirty wide-record slot, the union of pbox over the slot's prim range (a
@@ -2307,42 +2455,10 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
         const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
         *wide_box_f(o.lnodes, r.rec, w, sl, lane) = v;
     }
-    if (!o.mt) return;
-    // Moller-Trumbore: the child's per-ray padding constants (accel.cpp build_cones_mt:
-    // smallest |e1 x e2|, largest u X, M = |p1 - Z| and 18 M + 10.5 (E1 + E2) over the
-    // triangles below) merged with the moved triangles' own, grow-only like the boxes;
-    // the slab along the cone axis is dropped (m[5] = inf: its triangles moved off it).
-    // The moved records are the record role's, in the staging copy (launch 1).
-    double cr = INFINITY, X = 0, es = 0, mm = 0;
-    for (int p = d.y + lane; p < d.z; p += 64) {
-        const int e = m.prim_entry[p];
-        if (e < 0) continue;
-        rta::MtTri t;
-        rta::Box3 tb;
-        const FlatShape& s = r.direct ? r.fresh[e] : o.shapes[m.ids[e]];
-        if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) continue;
-        const double dz[3] = {t.p1[0] - o.mt_z[0], t.p1[1] - o.mt_z[1], t.p1[2] - o.mt_z[2]};
-        cr = fmin(cr, t.cr);
-        X = fmax(X, t.X);
-        es = fmax(es, t.esum);
-        mm = fmax(mm, sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]));
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        cr = fmin(cr, __shfl_xor(cr, off));
-        X = fmax(X, __shfl_xor(X, off));
-        es = fmax(es, __shfl_xor(es, off));
-        mm = fmax(mm, __shfl_xor(mm, off));
-    }
-    if (lane != 0) return;
-    float* k = wide_box_f(o.lnodes, kWideRecMt, w, sl, 0) + 10;  // {cr, u X, M, 18 M + 10.5 Esum, w, h0}
-    const double up = 1.0 + 1e-5;
-    if (X > 0) {
-        k[0] = fminf(k[0], static_cast<float>(cr * (1.0 - 1e-5)));
-        k[1] = fmaxf(k[1], static_cast<float>(rta::kU * X * up));
-        k[2] = fmaxf(k[2], static_cast<float>(mm * up + 1e-5));
-        k[3] = fmaxf(k[3], static_cast<float>((18.0 * mm + 10.5 * es) * up + 1e-5));
-    }
-    k[5] = INFINITY;
+    if (o.mt)
+        refit_slot_mt(m, o, r, d, w, sl, lane);
+    else
+        refit_slot_cone(m, o, r, d, w, sl, lane);
 }
 
 // The per-frame refit of flush_updates, in one-wave workgroups with four roles:
@@ -2540,8 +2656,6 @@ struct rt_ctx {
     bool report_pending[kAnimRing] = {false, false, false};  // its k_refit not yet checked
     unsigned* refit_ctr = nullptr;      // k_refit's ticket and done counters (never reset)
     unsigned ctr_tickets = 0, ctr_done = 0;  // their values after the last launch
-    float4* anim_enorm = nullptr;       // per refit entry: base stored normal + type (AnimMaps::enorm)
-    size_t anim_enorm_cap = 0;
     int anim_slot = 0;
     float4* anim_sbox = nullptr;        // per animated shape boxes (AnimOut::sbox)
     size_t anim_sbox_cap = 0;
@@ -3130,19 +3244,12 @@ int prepare_animation(rt_ctx* c) {
     for (size_t p = 0; p < (c->accel_ok ? A.prim_shape.size() : 0); ++p) buf.push_back(which[A.prim_shape[p]]);
     int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
     if (rc != RT_OK) return rc;
-    std::vector<float4> en(n);  // per entry: the base record's stored normal and type (the cone test)
-    for (int i = 0; i < n; ++i) {
-        const FlatShape& b0 = c->anim_base[i];
-        en[i] = make_float4(b0.planeNormal.x, b0.planeNormal.y, b0.planeNormal.z, bits_f(b0.type));
-    }
-    if ((rc = ensure_staging(c->anim_enorm, c->anim_enorm_cap, static_cast<size_t>(n))) != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->anim_enorm, en.data(), en.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const int* d = c->anim_maps;
     c->anim = AnimMaps{d,        d + o[0], d + o[1],  d + o[2],  d + o[3], d + o[4], d + o[5], d + o_ids,
                        d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], d + o_cls, d + o_pe,
-                       c->anim_enorm, n,
+                       n,
                        static_cast<int>(node_ids.size())};
     // the degraded-bound reports of earlier refits concern the accelerator this replaced
     for (bool& pend : c->report_pending) pend = false;
@@ -3294,7 +3401,8 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                               acc ? c->wnodes : nullptr, acc ? c->titems : nullptr,
                               acc ? c->pbox : nullptr, acc ? c->prim_idx_dev + P : nullptr, c->anim_sbox,
                               c->accel.origin_lim, c->accel.mt ? 1 : 0,
-                              {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]}};
+                              {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]},
+                              acc ? c->prim_idx_dev : nullptr, c->cone_cull};
             if (!c->refit_ctr) {
                 if (hipMalloc(&c->refit_ctr, 2 * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
                 HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, 2 * sizeof(unsigned), c->stream));
@@ -3999,7 +4107,6 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->sched_sets);
     hipFree(c->anim_maps);
     hipFree(c->anim_sbox);
-    hipFree(c->anim_enorm);
     hipFree(c->refit_ctr);
     for (int k = 0; k < rt_ctx::kAnimRing; ++k) {
         if (c->anim_pinned[k]) hipHostFree(c->anim_pinned[k]);
