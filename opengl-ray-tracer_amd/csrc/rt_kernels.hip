@@ -1977,6 +1977,33 @@ __global__ __launch_bounds__(kOrderThreads) void k_tile_order(const unsigned* __
     }
 }
 
+// The cost order's input dilated (rt_debug_cost_dilate): each tile's cost replaced by
+// the largest within r tiles in x and y, and the per-group bucket rows k_tile_order
+// reads recounted from those. A camera that moved since the costs were recorded sees
+// its heavy tiles a few tiles away from where they were; ranking their neighbourhood
+// high too puts them early anyway.
+__global__ __launch_bounds__(kOrderThreads) void k_cost_dilate(const unsigned* __restrict__ cost, int n, int tiles_x,
+                                                               int r, unsigned* __restrict__ out,
+                                                               unsigned* __restrict__ hist) {
+    __shared__ unsigned cnt[kOrderBuckets];
+    const int t = threadIdx.x, i = blockIdx.x * kOrderThreads + t;
+    if (t < kOrderBuckets) cnt[t] = 0u;
+    __syncthreads();
+    if (i < n) {
+        const int x = i % tiles_x, y = i / tiles_x, rows = (n + tiles_x - 1) / tiles_x;
+        unsigned m = 0u;
+        for (int yy = max(0, y - r); yy <= min(rows - 1, y + r); ++yy)
+            for (int xx = max(0, x - r); xx <= min(tiles_x - 1, x + r); ++xx) {
+                const int j = yy * tiles_x + xx;
+                if (j < n) m = max(m, cost[j]);
+            }
+        out[i] = m;
+        atomicAdd(&cnt[work_bucket(m)], 1u);
+    }
+    __syncthreads();
+    if (t < kOrderBuckets) hist[blockIdx.x * kOrderBuckets + t] = cnt[t];
+}
+
 // ---------------------------------------------------------------------------
 // Device animation (rt_animate): updateScene + updateBVH on the device.
 
@@ -2075,6 +2102,26 @@ struct RefitArgs {
     int direct;                // node / slot roles derive the entries' boxes from `fresh` themselves
 };
 
+// A lane-strided loop over [b, e) in steps of 4 x 64 whose four loads are issued
+// before any is used: a long range (a slot near a local root spans thousands of
+// prims) then costs a memory latency per step, not per prim.
+template <class Load, class Use>
+__device__ __forceinline__ void range4(int b, int e, int lane, Load load, Use use) {
+    for (int p0 = b + lane; p0 < e; p0 += 256) {
+        decltype(load(0)) v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (p0 + 64 * u < e) v[u] = load(p0 + 64 * u);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (p0 + 64 * u < e) use(v[u]);
+    }
+}
+
+struct Box4 {
+    float4 a, b;
+};
+
 __device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
     for (int off = 32; off > 0; off >>= 1)
         for (int a = 0; a < 3; ++a) {
@@ -2108,13 +2155,22 @@ __device__ bool entry_cbox(const AnimOut& o, const FlatShape& s, int was, rta::B
 
 __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int i) {
     if (i >= m.count) return;
+    // Every map read first: the stores below may alias them as far as the compiler
+    // knows, so a read after one would wait out its own latency, in a chain. The
+    // first slot and prim of each list (most entries have one of each) are prefetched
+    // with their dependants.
+    const int id = m.ids[i], fl = r.flags[i], was = m.ecls[i];
+    const int s0 = m.slot_off[i], s1 = m.slot_off[i + 1], p0 = m.prim_off[i], p1 = m.prim_off[i + 1];
+    const int slot0 = s0 < s1 ? m.slot_list[s0] : 0;
+    const int prim0 = o.anodes && p0 < p1 ? m.prim_list[p0] : 0;
+    const int seq0 = o.anodes && p0 < p1 ? o.prim_seq[prim0] : 0;
     const FlatShape s = r.fresh[i];
-    const int id = m.ids[i], fl = r.flags[i];
     o.shapes[id] = s;
     const GeoRec g = pack_geo(s, id);
     store_geo(o.geo_lin + 5 * static_cast<size_t>(id), g);
     store_mat(o.mat, id, s.material);
-    for (int q = m.slot_off[i]; q < m.slot_off[i + 1]; ++q) store_geo(o.geo_leaf + 5 * static_cast<size_t>(m.slot_list[q]), g);
+    if (s0 < s1) store_geo(o.geo_leaf + 5 * static_cast<size_t>(slot0), g);
+    for (int q = s0 + 1; q < s1; ++q) store_geo(o.geo_leaf + 5 * static_cast<size_t>(m.slot_list[q]), g);
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     if (fl & AF_GROW) reference_box(s, lo, hi);  // else the nodes keep their boxes
     float4* sb = o.sbox + 4 * static_cast<size_t>(i);
@@ -2125,20 +2181,22 @@ __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArg
         sb[3] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
         return;
     }
-    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {
+    // rank in the reference walk (k_pack_prims)
+    if (p0 < p1) store_prim(o.prims, prim0, pack_prim(g, seq0));
+    for (int q = p0 + 1; q < p1; ++q) {
         const int p = m.prim_list[q];
-        store_prim(o.prims, p, pack_prim(g, o.prim_seq[p]));  // rank in the reference walk (k_pack_prims)
+        store_prim(o.prims, p, pack_prim(g, o.prim_seq[p]));
     }
     rta::Box3 b;
-    const int was = m.ecls[i];
     if (entry_cbox(o, s, was, b)) *r.report = 1;  // the host rebuilds at its next flush
-    sb[2] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
-    sb[3] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
+    const float4 c0 = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f), c1 = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
+    sb[2] = c0;
+    sb[3] = c1;
     if (was != rta::BOUNDED) return;  // always tested since the build: no box above it
-    for (int q = m.prim_off[i]; q < m.prim_off[i + 1]; ++q) {  // the prim's box for the slot refit
-        float4* pb = o.pbox + 2 * static_cast<size_t>(m.prim_list[q]);
-        pb[0] = sb[2];
-        pb[1] = sb[3];
+    for (int q = p0; q < p1; ++q) {    // the prim's box for the slot refit
+        float4* pb = o.pbox + 2 * static_cast<size_t>(q == p0 ? prim0 : m.prim_list[q]);
+        pb[0] = c0;
+        pb[1] = c1;
     }
 }
 
@@ -2154,27 +2212,36 @@ __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArg
 __device__ void grow_node(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, int lane) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int q = m.node_off[j] + lane; q < m.node_off[j + 1]; q += 64) {
-        const int i = m.node_list[q];
-        float4 a, b, c, d;
-        if (r.direct) {  // from the record itself (no wait for the record role)
-            const FlatShape s = r.fresh[i];
-            float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
-            if (r.flags[i] & AF_GROW) reference_box(s, rl, rh);
-            rta::Box3 cb;
-            if (o.anodes) entry_cbox(o, s, m.ecls[i], cb);
-            else cb = rta::Box3{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
-            a = make_float4(rl[0], rl[1], rl[2], 0.f), b = make_float4(rh[0], rh[1], rh[2], 0.f);
-            c = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], 0.f), d = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
-        } else {
-            const float4* sb = o.sbox + 4 * static_cast<size_t>(i);
-            a = sb[0], b = sb[1], c = sb[2], d = sb[3];
-        }
-        lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
-        hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
-        clo[0] = fminf(clo[0], c.x), clo[1] = fminf(clo[1], c.y), clo[2] = fminf(clo[2], c.z);
-        chi[0] = fmaxf(chi[0], d.x), chi[1] = fmaxf(chi[1], d.y), chi[2] = fmaxf(chi[2], d.z);
-    }
+    struct Two {
+        Box4 ref, con;
+    };
+    range4(m.node_off[j], m.node_off[j + 1], lane,
+        [&](int q) {
+            const int i = m.node_list[q];
+            Two v;
+            if (r.direct) {  // from the record itself (no wait for the record role)
+                const FlatShape s = r.fresh[i];
+                float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
+                if (r.flags[i] & AF_GROW) reference_box(s, rl, rh);
+                rta::Box3 cb;
+                if (o.anodes) entry_cbox(o, s, m.ecls[i], cb);
+                else cb = rta::Box3{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+                v.ref = Box4{make_float4(rl[0], rl[1], rl[2], 0.f), make_float4(rh[0], rh[1], rh[2], 0.f)};
+                v.con = Box4{make_float4(cb.lo[0], cb.lo[1], cb.lo[2], 0.f), make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f)};
+            } else {
+                const float4* sb = o.sbox + 4 * static_cast<size_t>(i);
+                v.ref = Box4{sb[0], sb[1]};
+                v.con = Box4{sb[2], sb[3]};
+            }
+            return v;
+        },
+        [&](const Two& v) {
+            const float4 a = v.ref.a, b = v.ref.b, c = v.con.a, d = v.con.b;
+            lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
+            hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
+            clo[0] = fminf(clo[0], c.x), clo[1] = fminf(clo[1], c.y), clo[2] = fminf(clo[2], c.z);
+            chi[0] = fmaxf(chi[0], d.x), chi[1] = fmaxf(chi[1], d.y), chi[2] = fmaxf(chi[2], d.z);
+        });
     wave_minmax(lo, hi);
     wave_minmax(clo, chi);
     if (lane != 0) return;
@@ -2283,24 +2350,28 @@ __device__ void refit_slot_cone(const AnimMaps& m, const AnimOut& o, const Refit
                                 int lane) {
     int* cw = reinterpret_cast<int*>(o.lnodes + kWideRec * static_cast<size_t>(w) + 6) + sl;
     if (*cw == rta::kConeNever) return;  // the same word for the whole wave
-    auto unit_normal = [](const FlatShape& s, double n[3]) {
-        if (s.type != RT_WALL && s.type != RT_TRIANGLE) return false;
-        n[0] = s.planeNormal.x, n[1] = s.planeNormal.y, n[2] = s.planeNormal.z;
+    auto load = [&](int p) {  // the stored normal (w: 0 for a shape without a cone)
+        const FlatShape& s = slot_shape(m, o, r, p);
+        const bool cone = s.type == RT_WALL || s.type == RT_TRIANGLE;
+        return make_float4(s.planeNormal.x, s.planeNormal.y, s.planeNormal.z, cone ? 1.f : 0.f);
+    };
+    auto unit_normal = [](const float4& v, double n[3]) {  // accel.cpp shape_cone
+        n[0] = v.x, n[1] = v.y, n[2] = v.z;
         const double l = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-        if (!(l > 1e-20) || !isfinite(l)) return false;
+        if (v.w == 0.f || !(l > 1e-20) || !isfinite(l)) return false;
         for (int a = 0; a < 3; ++a) n[a] /= l;
         return true;
     };
     double sn[3] = {0, 0, 0};
     int full = 0;
-    for (int p = d.y + lane; p < d.z; p += 64) {
+    range4(d.y, d.z, lane, load, [&](const float4& v) {
         double n[3];
-        if (!unit_normal(slot_shape(m, o, r, p), n)) {
+        if (!unit_normal(v, n)) {
             full = 1;
-            continue;
+            return;
         }
         for (int a = 0; a < 3; ++a) sn[a] += n[a];
-    }
+    });
     for (int off = 32; off > 0; off >>= 1) {
         for (int a = 0; a < 3; ++a) sn[a] += __shfl_xor(sn[a], off);
         full |= __shfl_xor(full, off);
@@ -2315,11 +2386,11 @@ __device__ void refit_slot_cone(const AnimMaps& m, const AnimOut& o, const Refit
     const double al = sqrt(static_cast<double>(af[0]) * af[0] + static_cast<double>(af[1]) * af[1] +
                            static_cast<double>(af[2]) * af[2]);
     double cmin = 1.0;  // the smallest cosine to the axis
-    for (int p = d.y + lane; p < d.z; p += 64) {
+    range4(d.y, d.z, lane, load, [&](const float4& v) {
         double n[3];
-        unit_normal(slot_shape(m, o, r, p), n);
+        unit_normal(v, n);
         cmin = fmin(cmin, (n[0] * af[0] + n[1] * af[1] + n[2] * af[2]) / al);
-    }
+    });
     for (int off = 32; off > 0; off >>= 1) cmin = fmin(cmin, __shfl_xor(cmin, off));
     if (lane != 0) return;
     const double t = acos(fmax(-1.0, fmin(1.0, cmin))) + rta::kConeMargin;
@@ -2339,7 +2410,19 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
                               int lane) {
     float* k = wide_box_f(o.lnodes, kWideRecMt, w, sl, 0) + 6;  // axis xyz, s, {cr, u X, M, 18 M + 10.5 Esum, w, h0}
     const double a0[3] = {k[0], k[1], k[2]};                      // every lane reads before lane 0 writes
-    auto shape_of = [&](int p) -> const FlatShape& { return slot_shape(m, o, r, p); };
+    struct Tri {
+        int type;
+        rt_vec3 p1, p2, p3;
+    };
+    auto load = [&](int p) {
+        const FlatShape& s = slot_shape(m, o, r, p);
+        return Tri{s.type, s.triP1, s.triP2, s.triP3};
+    };
+    auto as_shape = [](const Tri& v) {  // what classify_mt_tight reads
+        FlatShape s{};
+        s.type = v.type, s.triP1 = v.p1, s.triP2 = v.p2, s.triP3 = v.p3;
+        return s;
+    };
     auto tri_normal = [](const FlatShape& s, double n[3]) {  // accel.cpp mt_normal, with |e1 x e2|
         const float e1[3] = {s.triP2.x - s.triP1.x, s.triP2.y - s.triP1.y, s.triP2.z - s.triP1.z};
         const float e2[3] = {s.triP3.x - s.triP1.x, s.triP3.y - s.triP1.y, s.triP3.z - s.triP1.z};
@@ -2351,13 +2434,13 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
     };
     double sn[3] = {0, 0, 0}, cr = INFINITY, X = 0, es = 0, mm = 0;
     int other = 0;
-    for (int p = d.y + lane; p < d.z; p += 64) {
-        const FlatShape& s = shape_of(p);
+    range4(d.y, d.z, lane, load, [&](const Tri& v) {
+        const FlatShape s = as_shape(v);
         rta::MtTri t;
         rta::Box3 tb;
         if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) {
             other = 1;
-            continue;
+            return;
         }
         double n[3];
         tri_normal(s, n);
@@ -2368,7 +2451,7 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
         X = fmax(X, t.X);
         es = fmax(es, t.esum);
         mm = fmax(mm, sqrt(dz[0] * dz[0] + dz[1] * dz[1] + dz[2] * dz[2]));
-    }
+    });
     for (int off = 32; off > 0; off >>= 1) {
         for (int a = 0; a < 3; ++a) sn[a] += __shfl_xor(sn[a], off);
         cr = fmin(cr, __shfl_xor(cr, off));
@@ -2383,11 +2466,11 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
     float af[3];
     for (int a = 0; a < 3; ++a) af[a] = __shfl(full ? static_cast<float>(a0[a]) : static_cast<float>(sn[a] / l), 0);
     double sm = 0, lo = INFINITY, hi = -INFINITY;
-    for (int p = d.y + lane; p < d.z && !full; p += 64) {
-        const FlatShape& s = shape_of(p);
+    range4(d.y, full ? d.y : d.z, lane, load, [&](const Tri& v) {
+        const FlatShape s = as_shape(v);
         rta::MtTri t;
         rta::Box3 tb;
-        if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) continue;
+        if (s.type != RT_TRIANGLE || rta::classify_mt_tight(s, tb, 0.0, t) != rta::BOUNDED) return;
         double n[3], dm = 0, dp = 0;
         tri_normal(s, n);
         for (int a = 0; a < 3; ++a) {
@@ -2401,7 +2484,7 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
             lo = fmin(lo, x);
             hi = fmax(hi, x);
         }
-    }
+    });
     for (int off = 32; off > 0; off >>= 1) {
         sm = fmax(sm, __shfl_xor(sm, off));
         lo = fmin(lo, __shfl_xor(lo, off));
@@ -2436,19 +2519,21 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
     const int4 d = r.dirty[j];
     const float4* __restrict__ pbox = o.pbox;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int p = d.y + lane; p < d.z; p += 64) {
-        const int e = r.direct ? m.prim_entry[p] : -1;
-        float4 a, b;
-        if (e >= 0 && m.ecls[e] == rta::BOUNDED) {  // a moved prim, from its record itself
-            rta::Box3 cb;
-            entry_cbox(o, r.fresh[e], rta::BOUNDED, cb);
-            a = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], 0.f), b = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
-        } else {
-            a = pbox[2 * static_cast<size_t>(p)], b = pbox[2 * static_cast<size_t>(p) + 1];
-        }
-        lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
-        hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
-    }
+    range4(d.y, d.z, lane,
+        [&](int p) {
+            const int e = r.direct ? m.prim_entry[p] : -1;
+            if (e >= 0 && m.ecls[e] == rta::BOUNDED) {  // a moved prim, from its record itself
+                rta::Box3 cb;
+                entry_cbox(o, r.fresh[e], rta::BOUNDED, cb);
+                return Box4{make_float4(cb.lo[0], cb.lo[1], cb.lo[2], 0.f), make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f)};
+            }
+            return Box4{pbox[2 * static_cast<size_t>(p)], pbox[2 * static_cast<size_t>(p) + 1]};
+        },
+        [&](const Box4& v) {
+            const float4 a = v.a, b = v.b;
+            lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
+            hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
+        });
     wave_minmax(lo, hi);
     const int w = d.x >> 2, sl = d.x & 3;
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
@@ -2604,6 +2689,21 @@ struct rt_ctx {
     // count changes); the dispatches between reuse it and record no work counts. 16:
     // car in flight -1.0 % against 8 (32: -0.9 %, 4: +1.5 %; profiles/r04z2_*)
     int sched_period = 16, sched_frame = 0;
+    int cost_dilate = 0;                 // rt_debug_cost_dilate: radius in tiles (0: off)
+    // The cost order of a dispatch whose camera differs from the last accelerated
+    // dispatch's (rt_debug_moving; period 0: as any other): re-derived after every such
+    // dispatch from whole-tile wall times dilated by one tile. The car's waited frame
+    // along the orbit / dolly paths of bench.py --camera-path, against the same cameras
+    // held still (median ratio over 8 cameras, tools/camera_probe.py, r05h / r05i):
+    // the still policy (every 16th frame, undilated) 1.53 / 1.46; every frame undilated
+    // 1.26; every 4th dilated by 2 1.16; every frame dilated by 1 1.09 / 1.06, with split
+    // tiles on those frames 1.15 / 1.14.
+    int moving_period = 1, moving_dilate = 1, moving_split = 0;
+    FlatCamera sched_cam{};
+    bool have_sched_cam = false;
+    bool moving = false;  // this dispatch's camera moved
+    unsigned* dil_cost = nullptr;        // its dilated costs (sched_cap) + bucket rows
+    size_t dil_cap = 0;
     // compaction (rt_set_tail): bounces >= tail_from run in k_accel_tail (0: off)
     int tail_from = RT_TAIL_AUTO;
     float4* tail_queue = nullptr;
@@ -2654,6 +2754,15 @@ struct rt_ctx {
     hipEvent_t anim_copied[kAnimRing] = {nullptr, nullptr, nullptr};  // that slot's k_refit has run
     size_t report_at[kAnimRing] = {0, 0, 0};       // offset of the slot's report word
     bool report_pending[kAnimRing] = {false, false, false};  // its k_refit not yet checked
+    bool slot_busy[kAnimRing] = {false, false, false};       // a k_refit reads it (anim_copied ends that)
+    // The slot of the last k_refit whose anim_copied is not recorded yet. An event
+    // costs the stream ~6 us wherever it sits (the car's animated frame: between k_refit
+    // and the render kernel it held the render kernel back, behind the render kernel
+    // it delayed rt_sync's own event; rocprofv3 --hip-trace, r05h / r05i), so it is
+    // recorded only when needed: before the next k_refit (frames in flight), or when
+    // the slot is wanted back. A wait that drains the stream (rt_sync) retires it
+    // unrecorded (stream_drained).
+    int mark_slot = -1;
     unsigned* refit_ctr = nullptr;      // k_refit's ticket and done counters (never reset)
     unsigned ctr_tickets = 0, ctr_done = 0;  // their values after the last launch
     int anim_slot = 0;
@@ -3302,9 +3411,28 @@ bool host_nodes_nest(const rt_ctx* c) {
 // Reads the report words of earlier refits whose k_refit has run (block: wait for
 // them): a shape whose bound changed kind leaves the accelerator exact but slower
 // (k_refit enters every box above it) until the host rebuilds it.
+// Every refit slot is free once the stream has drained: no event needed.
+void stream_drained(rt_ctx* c) {
+    c->mark_slot = -1;
+    for (bool& b : c->slot_busy) b = false;
+}
+
+// Records the anim_copied event of the last k_refit's slot if it is still pending.
+int record_mark(rt_ctx* c) {
+    if (c->mark_slot < 0) return RT_OK;
+    const int s = c->mark_slot;
+    c->mark_slot = -1;
+    HIP_TRY(hipEventRecord(c->anim_copied[s], c->stream));
+    return RT_OK;
+}
+
 int check_reports(rt_ctx* c, bool block = false) {
     for (int s = 0; s < rt_ctx::kAnimRing; ++s) {
         if (!c->report_pending[s]) continue;
+        if (s == c->mark_slot) {  // its event is not recorded yet: not done unless waited for
+            if (!block) continue;
+            if (const int rc = record_mark(c)) return rc;
+        }
         if (block) {
             HIP_TRY(hipEventSynchronize(c->anim_copied[s]));
         } else {
@@ -3326,8 +3454,10 @@ int pinned_slot(rt_ctx* c, size_t bytes, char** host, const char** dev) {
     c->anim_slot = (slot + 1) % rt_ctx::kAnimRing;
     if (!c->anim_copied[slot]) {
         HIP_TRY(hipEventCreateWithFlags(&c->anim_copied[slot], hipEventDisableTiming));
-    } else if (c->report_pending[slot]) {
+    } else if (c->slot_busy[slot]) {
+        if (slot == c->mark_slot && record_mark(c) != RT_OK) return RT_ERR_DEVICE;
         HIP_TRY(hipEventSynchronize(c->anim_copied[slot]));  // this slot's last k_refit has run
+        c->slot_busy[slot] = false;
         if (const int rc = check_reports(c)) return rc;
     }
     bytes = (bytes + 15) / 16 * 16;
@@ -3445,7 +3575,10 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             } else if ((rc = go(r)) != RT_OK) {
                 return rc;
             }
-            HIP_TRY(hipEventRecord(c->anim_copied[slot], c->stream));  // the slot may be refilled after this
+            // the slot may be refilled once its event (recorded behind the next dispatch) is done
+            if ((rc = record_mark(c)) != RT_OK) return rc;
+            c->mark_slot = slot;
+            c->slot_busy[slot] = true;
             c->report_pending[slot] = n > 0 && acc;
             if (nodes && (rc = open_inf_slots(c)) != RT_OK) return rc;
         }
@@ -3713,6 +3846,12 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                            c->nodes, kp);
     } else if (kind == RT_KERNEL_ACCEL) {
         KParams k2 = kp;
+        c->moving = c->have_sched_cam && std::memcmp(&c->sched_cam, &c->cam, sizeof c->cam) != 0 &&
+                    c->moving_period > 0;
+        c->sched_cam = c->cam;
+        c->have_sched_cam = true;
+        const int period = c->moving ? c->moving_period : c->sched_period;
+        const int dilate = c->moving ? c->moving_dilate : c->cost_dilate;
         k2.tiles_x = (kp.width + 7) / 8;
         k2.tiles = k2.tiles_x * ((kp.out_rows + 7) / 8);
         k2.tile_counter = c->tile_counter;
@@ -3757,7 +3896,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             k2.sched_hist = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
             const bool have = c->sched_valid == k2.tiles;
             if (have) k2.tile_order = c->sched_order;
-            if (!have || c->sched_frame % c->sched_period == 0) {
+            if (!have || c->sched_frame % period == 0) {
                 k2.tile_cost = c->sched_cost;
                 c->sched_frame = 0;
             }
@@ -3847,7 +3986,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             // 16th frame keeps the split set the longest whole tiles. The all-packet frames'
             // own split (8 waves, above) stays on their cost frames: whole, those took 1.5x
             // (config 2, the MT car; r04zz profiles), and in flight the ranking matters less.
-            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times && latency;
+            const bool whole = k2.tile_cost && c->cost_time != 0 && !c->tile_times && latency &&
+                               !(c->moving && c->moving_split);
             if (!c->persistent && stamps_fit && hp > 1 && hk > 0 && !whole) {
                 k2.heavy_k = std::min(hk, k2.tiles);
                 k2.heavy_parts = hp;
@@ -3963,10 +4103,26 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             // end event, so rt_kernel_times is the render kernel alone), before the next
             if (rec) HIP_TRY(hipEventRecord(e1, c->stream));
             order_after = true;
-            unsigned* set = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
+            const unsigned* set = c->sched_sets + c->sched_parity * sched_set_words(c->sched_cap);
             unsigned* next = c->sched_sets + (1 - c->sched_parity) * sched_set_words(c->sched_cap);
-            hipLaunchKernelGGL(k_tile_order, dim3((k2.tiles + kOrderThreads - 1) / kOrderThreads), dim3(kOrderThreads),
-                               0, c->stream, c->sched_cost, k2.tiles, set, next,
+            const int groups = (k2.tiles + kOrderThreads - 1) / kOrderThreads;
+            const unsigned* cost = c->sched_cost;
+            if (dilate > 0) {
+                const size_t need = static_cast<size_t>(k2.tiles) + static_cast<size_t>(groups) * kOrderBuckets;
+                if (c->dil_cap < need) {
+                    hipFree(c->dil_cost);
+                    c->dil_cost = nullptr;
+                    c->dil_cap = 0;
+                    if (hipMalloc(&c->dil_cost, need * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                    c->dil_cap = need;
+                }
+                hipLaunchKernelGGL(k_cost_dilate, dim3(groups), dim3(kOrderThreads), 0, c->stream, c->sched_cost,
+                                   k2.tiles, k2.tiles_x, dilate, c->dil_cost, c->dil_cost + k2.tiles);
+                cost = c->dil_cost;
+                set = c->dil_cost + k2.tiles;
+            }
+            hipLaunchKernelGGL(k_tile_order, dim3(groups), dim3(kOrderThreads),
+                               0, c->stream, cost, k2.tiles, set, next,
                                static_cast<int>(sched_set_words(c->sched_cap)), c->sched_order,
                                c->schedule == RT_SCHED_COST_XCD ? 1 : 0);
             c->sched_parity = 1 - c->sched_parity;
@@ -4102,6 +4258,7 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->tile_times);
     hipFree(c->tile_order);
     hipFree(c->sched_cost);
+    hipFree(c->dil_cost);
     hipFree(c->heavy_acc);
     hipFree(c->sched_order);
     hipFree(c->sched_sets);
@@ -4125,6 +4282,7 @@ int rt_destroy(rt_ctx* c) {
 int rt_set_stream(rt_ctx* c, void* s) {
     if (!c) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    if (const int rc = record_mark(c)) return rc;  // on the stream the k_refit ran on
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->own_stream) hipStreamDestroy(c->stream);
     if (s) {
@@ -4442,7 +4600,10 @@ int rt_sync(rt_ctx* c) {
             return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
         },
         [] { return false; }, 0.0);
-    return w == rtg::kWaitDone ? RT_OK : RT_ERR_DEVICE;
+    if (w != rtg::kWaitDone) return RT_ERR_DEVICE;
+    for (rt_ctx* x : {c, c->brute, c->mtc})  // the sub-contexts run on this stream
+        if (x) stream_drained(x);
+    return RT_OK;
 }
 
 int rt_read_image(rt_ctx* c, float* dst, size_t pitch, int width, int height) {
@@ -4612,6 +4773,20 @@ extern "C" int rt_debug_sched_period(rt_ctx* c, int period) {
     if (!c || period < 1) return RT_ERR_INVALID;
     c->sched_period = period;
     c->sched_frame = 0;
+    return RT_OK;
+}
+
+extern "C" int rt_debug_moving(rt_ctx* c, int period, int dilate, int split) {
+    if (!c || period < 0 || dilate < 0 || dilate > 64) return RT_ERR_INVALID;
+    c->moving_period = period;
+    c->moving_dilate = dilate;
+    c->moving_split = split ? 1 : 0;
+    return RT_OK;
+}
+
+extern "C" int rt_debug_cost_dilate(rt_ctx* c, int r) {
+    if (!c || r < 0 || r > 64) return RT_ERR_INVALID;
+    c->cost_dilate = r;
     return RT_OK;
 }
 

@@ -792,6 +792,20 @@ class ComputeShader:
             raise RTError("rt_debug_sched_order", k)
         return buf[:k].copy()
 
+    def debug_moving(self, period, dilate, split):
+        """Cost order of dispatches whose camera moved: re-derived every `period` frames
+        (0: as still frames), over costs dilated by `dilate` tiles, split tiles kept on
+        its cost frames (`split`)."""
+        fn = self._lib.rt_debug_moving
+        fn.argtypes = [_P, _I, _I, _I]
+        self._chk(fn(self._h, int(period), int(dilate), int(split)), "rt_debug_moving")
+
+    def debug_cost_dilate(self, r):
+        """Cost order over each tile's largest cost within r tiles (0: off)."""
+        fn = self._lib.rt_debug_cost_dilate
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(r)), "rt_debug_cost_dilate")
+
     def debug_cost_time(self, mode):
         """Cost-order measure: 1 the tiles' wave wall time, 0 their lanes' steps + tests, -1 default."""
         fn = self._lib.rt_debug_cost_time
