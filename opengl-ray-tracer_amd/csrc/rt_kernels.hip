@@ -2091,31 +2091,38 @@ struct RefitArgs {
     const int* flags;          // per entry: AF_GROW (pinned)
     const FlatNode* nsrc;      // rt_update_nodes: the host's node records (pinned), or null
     int* report;               // pinned: set to 1 when an entry's bound changed kind
-    unsigned* ctr;             // [0] workgroup tickets, [1] finished record workgroups
+    unsigned* ctr;             // [0] workgroup tickets, [1] finished record workgroups, then the flags
     unsigned tbase, abase;     // their values before this launch
     int na, nd, nb;            // workgroups of the record, node-set and node roles
-    const int4* dirty;         // slot refit work list (n_dirty entries after the nb node waves)
+    const int4* dirty;         // slot refit work list (n_dirty entries after the nb node waves, + 1 end)
+    const float4* dstatic;     // per dirty slot: the box of its prims outside the refit set (lo, hi)
+    const int* dlist;          // the refit set's prims of each dirty slot (dirty[j].w ..)
     int n_dirty, rec;          // its length; the wide record size (kWideRec / kWideRecMt)
     const int* titem_ref;      // per scene-tree item: its reference leaf
     int n_items, N;
-    int wait;                  // node / slot roles wait for the record role (one launch, rt_debug_refit 0)
+    int wait;                  // node / slot roles wait for the record role: 1 by tickets, 2 in start order
     int direct;                // node / slot roles derive the entries' boxes from `fresh` themselves
 };
 
 // A lane-strided loop over [b, e) in steps of 4 x 64 whose four loads are issued
 // before any is used: a long range (a slot near a local root spans thousands of
 // prims) then costs a memory latency per step, not per prim.
+// nt threads (a wave or a workgroup), this one tid.
 template <class Load, class Use>
-__device__ __forceinline__ void range4(int b, int e, int lane, Load load, Use use) {
-    for (int p0 = b + lane; p0 < e; p0 += 256) {
+__device__ __forceinline__ void range4(int b, int e, int tid, int nt, Load load, Use use) {
+    for (int p0 = b + tid; p0 < e; p0 += 4 * nt) {
         decltype(load(0)) v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (p0 + 64 * u < e) v[u] = load(p0 + 64 * u);
+            if (p0 + nt * u < e) v[u] = load(p0 + nt * u);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-            if (p0 + 64 * u < e) use(v[u]);
+            if (p0 + nt * u < e) use(v[u]);
     }
+}
+template <class Load, class Use>
+__device__ __forceinline__ void range4(int b, int e, int lane, Load load, Use use) {
+    range4(b, e, lane, 64, load, use);
 }
 
 struct Box4 {
@@ -2128,6 +2135,28 @@ __device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
             lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
             hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
         }
+}
+
+// wave_minmax over the workgroup (up to kRefitWaves waves; every thread gets the
+// result); sh: LDS scratch of the workgroup, free again on return.
+constexpr int kRefitWaves = 4;
+constexpr int kRefitFlag0 = 16, kRefitFlags = 16;  // k_refit's all-done flags: ctr[16 + 16 k]
+__device__ __forceinline__ void block_minmax(float lo[3], float hi[3], float (*sh)[6]) {
+    wave_minmax(lo, hi);
+    const int nw = blockDim.x >> 6;
+    if (nw == 1) return;
+    if ((threadIdx.x & 63) == 0)
+        for (int a = 0; a < 3; ++a) {
+            sh[threadIdx.x >> 6][a] = lo[a];
+            sh[threadIdx.x >> 6][3 + a] = hi[a];
+        }
+    __syncthreads();
+    for (int k = 0; k < nw; ++k)
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], sh[k][a]);
+            hi[a] = fmaxf(hi[a], sh[k][3 + a]);
+        }
+    __syncthreads();
 }
 
 // Record role, one lane per refit entry: rewrites its records and derives its two
@@ -2209,13 +2238,14 @@ __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArg
 // copy the kernels read: the packed node, the accelerator's exact box, its
 // parent's child copy (wnodes: exact + content box) and the scene-tree items gated
 // by it. Nodes listing no entry never change, so no other copy needs refreshing.
-__device__ void grow_node(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, int lane) {
+__device__ void grow_node(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, float (*sh)[6]) {
+    const int tid = threadIdx.x;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     float clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
     struct Two {
         Box4 ref, con;
     };
-    range4(m.node_off[j], m.node_off[j + 1], lane,
+    range4(m.node_off[j], m.node_off[j + 1], tid, blockDim.x,
         [&](int q) {
             const int i = m.node_list[q];
             Two v;
@@ -2242,9 +2272,9 @@ __device__ void grow_node(const AnimMaps& m, const AnimOut& o, const RefitArgs& 
             clo[0] = fminf(clo[0], c.x), clo[1] = fminf(clo[1], c.y), clo[2] = fminf(clo[2], c.z);
             chi[0] = fmaxf(chi[0], d.x), chi[1] = fmaxf(chi[1], d.y), chi[2] = fmaxf(chi[2], d.z);
         });
-    wave_minmax(lo, hi);
-    wave_minmax(clo, chi);
-    if (lane != 0) return;
+    block_minmax(lo, hi, sh);
+    block_minmax(clo, chi, sh);
+    if (tid != 0) return;
     const int k = m.node_ids[j];
     FlatNode& nd = o.nodes[k];
     float mn[3] = {nd.boundsMin.x, nd.boundsMin.y, nd.boundsMin.z};
@@ -2512,15 +2542,21 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
 
 // Slot role: exact refit of the local / scene-tree boxes above moved prims (they
 // are the accelerator's own, so unlike the reference nodes they may shrink): one
-// wave per dirty wide-record slot, the union of pbox over the slot's prim range (a
-// subtree's prims are contiguous, accel.cpp LocalBuilder). dirty[j] = (4*w + s,
-// first prim, end prim, 0).
-__device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, int lane) {
+// workgroup per dirty wide-record slot, the union of the box of the slot's prims
+// that are not in the refit set (fixed: prepare_animation, dstatic) and of pbox over
+// those that are (dlist) -- a subtree's prims are contiguous (accel.cpp
+// LocalBuilder), the scene tree's top slots span every prim (the car: 4,020, against
+// 640 refit prims). dirty[j] = (4*w + s, first prim, end prim, first of its dlist
+// entries); dirty[j + 1].w ends them.
+__device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, float (*sh)[6]) {
+    const int tid = threadIdx.x, lane = tid & 63;
     const int4 d = r.dirty[j];
     const float4* __restrict__ pbox = o.pbox;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    range4(d.y, d.z, lane,
-        [&](int p) {
+    const float4 s0 = r.dstatic[2 * j], s1 = r.dstatic[2 * j + 1];
+    float lo[3] = {s0.x, s0.y, s0.z}, hi[3] = {s1.x, s1.y, s1.z};
+    range4(d.w, r.dirty[j + 1].w, tid, blockDim.x,
+        [&](int q) {
+            const int p = r.dlist[q];
             const int e = r.direct ? m.prim_entry[p] : -1;
             if (e >= 0 && m.ecls[e] == rta::BOUNDED) {  // a moved prim, from its record itself
                 rta::Box3 cb;
@@ -2534,7 +2570,8 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
             lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
             hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
         });
-    wave_minmax(lo, hi);
+    block_minmax(lo, hi, sh);
+    if (tid >= 64) return;  // the cones: one wave
     const int w = d.x >> 2, sl = d.x & 3;
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
         const float v = lane == 0 ? lo[0] : lane == 1 ? lo[1] : lane == 2 ? lo[2] : lane == 3 ? hi[0] : lane == 4 ? hi[1] : hi[2];
@@ -2546,51 +2583,73 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
         refit_slot_cone(m, o, r, d, w, sl, lane);
 }
 
-// The per-frame refit of flush_updates, in one-wave workgroups with four roles:
-//   [0, na)             record role (refit_record), 64 entries each;
-//   [na, na + nd)       node-set role (set_node), 64 nodes or items each;
-//   [na + nd, ...)      one wave each: node role (grow_node) for the first nb, then
+// The per-frame refit of flush_updates, in workgroups of four roles:
+//   [0, na)             record role (refit_record), a lane per entry;
+//   [na, na + nd)       node-set role (set_node), a lane per node or item;
+//   [na + nd, ...)      a workgroup each: node role (grow_node) for the first nb, then
 //                       slot role (refit_slot); both read what the record role wrote.
-// Default (rt_debug_refit 1): two launches, records and node sets, then nodes and
-// slots: the kernel boundary orders them (GPU time ~12 + ~12 us on the car's wheels,
-// no gap between the two). Mode 0 is ONE launch whose workgroups take tickets on
-// arrival (handed out in the order they start, so a later ticket waits only for work
-// already running) and whose node / slot waves spin until every record workgroup has
-// released its writes: measured slower (35 us), the single ticket counter serialising
-// ~270 workgroups. Mode 2 is one launch whose node / slot waves derive each entry's
-// boxes from its record over the host link themselves (72 us). The node-set role never
-// runs with AF_GROW entries in the same flush (flush_updates applies host node records
-// first), so no two roles write the same box.
-__global__ __launch_bounds__(64) void k_refit(AnimMaps m, AnimOut o, RefitArgs r) {
-    const int lane = threadIdx.x;
-    unsigned t = blockIdx.x;  // without waits the launch order does not matter
-    if (r.wait) {
-        if (lane == 0) t = __hip_atomic_fetch_add(r.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.tbase;
-        t = __shfl(t, 0);
+// Modes (rt_debug_refit), on the car's wheels (640 entries, 650 dirty slots):
+//   1 two launches, records and node sets in one-wave workgroups, then nodes and slots
+//     in kRefitWaves-wave ones: the kernel boundary orders them (11.4 + 8.4 us, r05n);
+//   3 default: ONE launch of kRefitWaves-wave workgroups whose node / slot workgroups
+//     wait (wait 2) until every record workgroup has released its writes. Workgroups
+//     start in index order, record workgroups first, and every one of them runs to its
+//     end without waiting, so the waits end;
+//   0 as 3 with the start order made explicit by a ticket per workgroup (wait 1): the
+//     ticket counter serialises the launch (35 us when measured with one-wave slots);
+//   2 one launch whose node / slot roles derive each entry's boxes from its record over
+//     the host link themselves (direct; 72 us).
+// Copying the records to the device before the launches instead of reading them over
+// the host link measured no faster (r05k: waited car frame 0.259 against 0.252 ms).
+// The node-set role never runs with AF_GROW entries in the same flush (flush_updates
+// applies host node records first), so no two roles write the same box.
+__global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut o, RefitArgs r) {
+    __shared__ float sh[kRefitWaves][6];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    unsigned t = blockIdx.x;
+    if (r.wait == 1) {
+        __shared__ unsigned ticket;
+        if (tid == 0) ticket = __hip_atomic_fetch_add(r.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.tbase;
+        __syncthreads();
+        t = ticket;
     }
     if (t < static_cast<unsigned>(r.na)) {
-        refit_record(m, o, r, static_cast<int>(t) * 64 + lane);
-        if (r.wait && lane == 0) __hip_atomic_fetch_add(r.ctr + 1, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        refit_record(m, o, r, static_cast<int>(t) * nt + tid);
+        if (r.wait) {
+            __threadfence();  // this thread's writes, then the workgroup's release
+            __syncthreads();
+            if (tid == 0) {
+                const unsigned done = __hip_atomic_fetch_add(r.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+                if (done - r.abase == static_cast<unsigned>(r.na) - 1u)  // the last one: raise the flags
+                    for (int k = 0; k < kRefitFlags; ++k)
+                        __hip_atomic_store(r.ctr + kRefitFlag0 + 16 * k, r.abase + r.na, __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         return;
     }
     t -= r.na;
     if (t < static_cast<unsigned>(r.nd)) {
-        set_node(o, r, static_cast<int>(t) * 64 + lane);
+        set_node(o, r, static_cast<int>(t) * nt + tid);
         return;
     }
     t -= r.nd;
     if (r.wait) {
-        if (lane == 0)
-            while (__hip_atomic_load(r.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.abase <
+        // one of kRefitFlags copies of the all-done flag, a cache line each: ~650 waiting
+        // workgroups polling the counter itself held its increments back (car: 42 us)
+        const unsigned* flag = r.ctr + kRefitFlag0 + 16 * (blockIdx.x % kRefitFlags);
+        if (tid == 0)
+            while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.abase <
                    static_cast<unsigned>(r.na))
                 __builtin_amdgcn_s_sleep(2);
+        __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     const int w = static_cast<int>(t);
     if (w < r.nb)
-        grow_node(m, o, r, w, lane);
+        grow_node(m, o, r, w, sh);
     else if (w - r.nb < r.n_dirty)
-        refit_slot(m, o, r, w - r.nb, lane);
+        refit_slot(m, o, r, w - r.nb, sh);
 }
 
 // Scene-tree wide slots of the unbounded subtree (kNoPrune): their boxes are the
@@ -2739,7 +2798,9 @@ struct rt_ctx {
     // rt_debug_refit: 0 one launch (box roles wait on tickets), 1 two launches (default:
     // the car's waited animated frame 0.262 ms against 0.268 and 0.299, r05d), 2 one
     // launch (box roles read the records over the host link themselves)
-    int refit_mode = 1;
+    int refit_mode = 3;
+    long long dirty_sum = 0;  // rt_debug_refit_stats: the slot refit's prim ranges (largest, total)
+    int dirty_max = 0;
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
     size_t anim_maps_cap = 0;
     AnimMaps anim{};
@@ -2769,7 +2830,9 @@ struct rt_ctx {
     float4* anim_sbox = nullptr;        // per animated shape boxes (AnimOut::sbox)
     size_t anim_sbox_cap = 0;
     float4* pbox = nullptr;             // per prim conservative box (AnimOut::pbox)
-    int4* refit_dirty = nullptr;        // k_refit's slot work list
+    int4* refit_dirty = nullptr;        // k_refit's slot work list (RefitArgs::dirty)
+    float4* refit_static = nullptr;     // RefitArgs::dstatic
+    int* refit_list = nullptr;          // RefitArgs::dlist
     int n_dirty = 0;
     int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
@@ -2835,8 +2898,12 @@ void free_accel(rt_ctx* c) {
     hipFree(c->prim_idx_dev);
     hipFree(c->pbox);
     hipFree(c->refit_dirty);
+    hipFree(c->refit_static);
+    hipFree(c->refit_list);
     c->pbox = nullptr;
     c->refit_dirty = nullptr;
+    c->refit_static = nullptr;
+    c->refit_list = nullptr;
     c->n_dirty = 0;
     c->anodes = c->lnodes = c->wnodes = c->prims = nullptr;
     c->tleaf = nullptr;
@@ -3279,19 +3346,53 @@ int prepare_animation(rt_ctx* c) {
             pb[2 * p] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
             pb[2 * p + 1] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
         }
+        // per dirty slot: the box of its prims outside the refit set (they never move
+        // while this set stands) and the list of those in it, which k_refit unions per frame
+        c->dirty_max = c->dirty_sum = 0;
+        std::vector<float4> st(2 * (work.empty() ? 1 : work.size()));
+        std::vector<int> dl;
+        for (size_t q = 0; q < work.size(); ++q) {
+            int4& w4 = work[q];
+            c->dirty_max = std::max(c->dirty_max, w4.z - w4.y);
+            c->dirty_sum += w4.z - w4.y;
+            w4.w = static_cast<int>(dl.size());
+            float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int p = w4.y; p < w4.z; ++p) {
+                if (which[A.prim_shape[p]] >= 0) {
+                    dl.push_back(p);
+                    continue;
+                }
+                const float4 a = pb[2 * static_cast<size_t>(p)], b = pb[2 * static_cast<size_t>(p) + 1];
+                lo[0] = std::min(lo[0], a.x), lo[1] = std::min(lo[1], a.y), lo[2] = std::min(lo[2], a.z);
+                hi[0] = std::max(hi[0], b.x), hi[1] = std::max(hi[1], b.y), hi[2] = std::max(hi[2], b.z);
+            }
+            st[2 * q] = make_float4(lo[0], lo[1], lo[2], 0.f);
+            st[2 * q + 1] = make_float4(hi[0], hi[1], hi[2], 0.f);
+        }
+        const int nw = static_cast<int>(work.size());
+        work.push_back(make_int4(0, 0, 0, static_cast<int>(dl.size())));  // the end of the last list
+        if (dl.empty()) dl.push_back(0);
         hipFree(c->pbox);
         hipFree(c->refit_dirty);
+        hipFree(c->refit_static);
+        hipFree(c->refit_list);
         c->pbox = nullptr;
         c->refit_dirty = nullptr;
+        c->refit_static = nullptr;
+        c->refit_list = nullptr;
         c->n_dirty = 0;
         if (hipMalloc(&c->pbox, pb.size() * sizeof(float4)) != hipSuccess ||
-            hipMalloc(&c->refit_dirty, (work.empty() ? 1 : work.size()) * sizeof(int4)) != hipSuccess)
+            hipMalloc(&c->refit_dirty, work.size() * sizeof(int4)) != hipSuccess ||
+            hipMalloc(&c->refit_static, st.size() * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&c->refit_list, dl.size() * sizeof(int)) != hipSuccess)
             return RT_ERR_NO_MEMORY;
         HIP_TRY(hipMemcpyAsync(c->pbox, pb.data(), pb.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
-        if (!work.empty())
-            HIP_TRY(hipMemcpyAsync(c->refit_dirty, work.data(), work.size() * sizeof(int4), hipMemcpyHostToDevice,
-                                   c->stream));
-        c->n_dirty = static_cast<int>(work.size());
+        HIP_TRY(hipMemcpyAsync(c->refit_dirty, work.data(), work.size() * sizeof(int4), hipMemcpyHostToDevice,
+                               c->stream));
+        HIP_TRY(hipMemcpyAsync(c->refit_static, st.data(), st.size() * sizeof(float4), hipMemcpyHostToDevice,
+                               c->stream));
+        HIP_TRY(hipMemcpyAsync(c->refit_list, dl.data(), dl.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
+        c->n_dirty = nw;
         const int rc = open_inf_slots(c);
         if (rc != RT_OK) return rc;
     }
@@ -3534,35 +3635,43 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                               {c->accel.mt_z[0], c->accel.mt_z[1], c->accel.mt_z[2]},
                               acc ? c->prim_idx_dev : nullptr, c->cone_cull};
             if (!c->refit_ctr) {
-                if (hipMalloc(&c->refit_ctr, 2 * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
-                HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, 2 * sizeof(unsigned), c->stream));
+                const size_t words = kRefitFlag0 + 16 * kRefitFlags;  // tickets, done, then the flags
+                if (hipMalloc(&c->refit_ctr, words * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, words * sizeof(unsigned), c->stream));
                 c->ctr_tickets = c->ctr_done = 0;
             }
+            const char* src = pin_dev;
+            const int waves = c->refit_mode == 2 ? 1 : kRefitWaves;  // per workgroup of a single launch
             RefitArgs r{};
-            r.fresh = reinterpret_cast<const FlatShape*>(pin_dev);
-            r.flags = reinterpret_cast<const int*>(pin_dev + n * sizeof(FlatShape));
-            r.nsrc = nodes ? reinterpret_cast<const FlatNode*>(pin_dev + rec_bytes) : nullptr;
+            r.fresh = reinterpret_cast<const FlatShape*>(src);
+            r.flags = reinterpret_cast<const int*>(src + n * sizeof(FlatShape));
+            r.nsrc = nodes ? reinterpret_cast<const FlatNode*>(src + rec_bytes) : nullptr;
             r.report = reinterpret_cast<int*>(const_cast<char*>(pin_dev) + c->report_at[slot]);
             r.ctr = c->refit_ctr;
             r.tbase = c->ctr_tickets;
             r.abase = c->ctr_done;
-            r.na = (n + 63) / 64;
+            const int per = 64 * (c->refit_mode == 1 ? 1 : waves);  // record / node-set lanes per workgroup
+            r.na = (n + per - 1) / per;
             r.N = c->N;
             r.n_items = nodes && acc ? c->n_titems : 0;
             r.titem_ref = c->titem_ref;
-            r.nd = nodes ? (c->N + r.n_items + 63) / 64 : 0;
+            r.nd = nodes ? (c->N + r.n_items + per - 1) / per : 0;
             r.nb = n > 0 ? c->anim.nodes : 0;
             r.dirty = c->refit_dirty;
+            r.dstatic = c->refit_static;
+            r.dlist = c->refit_list;
             r.n_dirty = n > 0 && acc ? c->n_dirty : 0;
             r.rec = c->accel.mt ? kWideRecMt : kWideRec;
-            r.wait = c->refit_mode == 0;
+            r.wait = c->refit_mode == 0 ? 1 : c->refit_mode == 3 ? 2 : 0;
             r.direct = c->refit_mode == 2;
-            auto go = [&](const RefitArgs& ra) -> int {
+            // waves per workgroup: the node and slot roles' own launch takes kRefitWaves (a
+            // slot's or node's list in one step), a launch with the one-wave roles one
+            auto go = [&](const RefitArgs& ra, int waves) -> int {
                 const int grid = ra.na + ra.nd + ra.nb + ra.n_dirty;
                 if (grid == 0) return RT_OK;
-                hipLaunchKernelGGL(k_refit, dim3(grid), dim3(64), 0, c->stream, c->anim, out, ra);
+                hipLaunchKernelGGL(k_refit, dim3(grid), dim3(64 * waves), 0, c->stream, c->anim, out, ra);
                 HIP_TRY(hipGetLastError());
-                c->ctr_tickets += static_cast<unsigned>(grid);
+                if (ra.wait == 1) c->ctr_tickets += static_cast<unsigned>(grid);
                 if (ra.wait) c->ctr_done += static_cast<unsigned>(ra.na);
                 return RT_OK;
             };
@@ -3570,9 +3679,8 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                 RefitArgs r1 = r, r2 = r;
                 r1.nb = r1.n_dirty = 0;
                 r2.na = r2.nd = 0;
-                r2.tbase = c->ctr_tickets + static_cast<unsigned>(r1.na + r1.nd);
-                if ((rc = go(r1)) != RT_OK || (rc = go(r2)) != RT_OK) return rc;
-            } else if ((rc = go(r)) != RT_OK) {
+                if ((rc = go(r1, 1)) != RT_OK || (rc = go(r2, kRefitWaves)) != RT_OK) return rc;
+            } else if ((rc = go(r, waves)) != RT_OK) {
                 return rc;
             }
             // the slot may be refilled once its event (recorded behind the next dispatch) is done
@@ -3694,6 +3802,11 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->latency_mode = c->latency_mode;
     b->schedule = c->schedule;
     b->sched_period = c->sched_period;
+    b->cost_dilate = c->cost_dilate;
+    b->moving_period = c->moving_period;
+    b->moving_dilate = c->moving_dilate;
+    b->moving_split = c->moving_split;
+    b->refit_mode = c->refit_mode;
     b->tail_from = c->tail_from;
     b->tail_max_lanes = c->tail_max_lanes;
     b->shadow_walk_override = c->shadow_walk_override;
@@ -3846,14 +3959,23 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                            c->nodes, kp);
     } else if (kind == RT_KERNEL_ACCEL) {
         KParams k2 = kp;
-        c->moving = c->have_sched_cam && std::memcmp(&c->sched_cam, &c->cam, sizeof c->cam) != 0 &&
+        k2.tiles_x = (kp.width + 7) / 8;
+        k2.tiles = k2.tiles_x * ((kp.out_rows + 7) / 8);
+        // rt_set_latency_mode applies to frames of at most kLatencyMaxSlots tiles per wave
+        // slot: a bigger frame keeps the chip busy on its own, and the split-walk instance's
+        // throughput cost then outweighs the shorter chains (waited frame, latency mode on
+        // against off: car 1080p 0.216 against 0.262 ms; car 3840x2160 0.706 against 0.626;
+        // config 5 3.364 against 3.332; profiles/r04zz2_latency_sweep_*.json)
+        const bool latency = c->latency_mode && k2.tiles <= kLatencyMaxSlots * c->cu_count * 16;
+        // a moved camera's cost order (moving_period): waited frames only -- with frames in
+        // flight a cost frame after every move cost the car's orbit 0.194 -> 0.238 ms per
+        // frame (r05j), and the order matters less there
+        c->moving = latency && c->have_sched_cam && std::memcmp(&c->sched_cam, &c->cam, sizeof c->cam) != 0 &&
                     c->moving_period > 0;
         c->sched_cam = c->cam;
         c->have_sched_cam = true;
         const int period = c->moving ? c->moving_period : c->sched_period;
         const int dilate = c->moving ? c->moving_dilate : c->cost_dilate;
-        k2.tiles_x = (kp.width + 7) / 8;
-        k2.tiles = k2.tiles_x * ((kp.out_rows + 7) / 8);
         k2.tile_counter = c->tile_counter;
         k2.tile_times = c->tile_times;
         if (c->tile_times)
@@ -3944,12 +4066,6 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const size_t lds = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces || k2.lane_k > 0
                                ? static_cast<size_t>(k2.lane_stack) * 64 * wpb * 6
                                : 0;
-        // rt_set_latency_mode applies to frames of at most kLatencyMaxSlots tiles per wave
-        // slot: a bigger frame keeps the chip busy on its own, and the split-walk instance's
-        // throughput cost then outweighs the shorter chains (waited frame, latency mode on
-        // against off: car 1080p 0.216 against 0.262 ms; car 3840x2160 0.706 against 0.626;
-        // config 5 3.364 against 3.332; profiles/r04zz2_latency_sweep_*.json)
-        const bool latency = c->latency_mode && k2.tiles <= kLatencyMaxSlots * c->cu_count * 16;
         if (k2.tile_order && k2.tile_order == c->sched_order) {
             // heavy tiles: explicit (rt_debug_heavy) or auto. A frame of at most
             // kHeavyAutoSlots waves per wave slot whose walks are all packets (config 2:
@@ -4719,8 +4835,20 @@ extern "C" int rt_debug_refits(rt_ctx* c) { return c ? c->updates_flushed : -1; 
 // Diagnostics: how flush_updates launches the refit (RefitArgs: 0 one launch whose box
 // roles wait for the record role, 1 two launches, 2 one launch deriving every box from
 // the records). Same device state either way.
+// out: dirty slots, their largest and total prim range, reference nodes listing an
+// entry, refit entries
+extern "C" int rt_debug_refit_stats(rt_ctx* c, long long* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    out[0] = c->n_dirty;
+    out[1] = c->dirty_max;
+    out[2] = c->dirty_sum;
+    out[3] = c->anim.nodes;
+    out[4] = static_cast<long long>(c->refit_ids.size());
+    return RT_OK;
+}
+
 extern "C" int rt_debug_refit(rt_ctx* c, int mode) {
-    if (!c || mode < 0 || mode > 2) return RT_ERR_INVALID;
+    if (!c || mode < 0 || mode > 3) return RT_ERR_INVALID;
     c->refit_mode = mode;
     return RT_OK;
 }

@@ -751,7 +751,8 @@ class ComputeShader:
         return int(fn(self._h))
 
     def debug_refit(self, mode):
-        """rt_debug_refit: 0 one launch (box roles wait), 1 two launches, 2 one launch (direct)."""
+        """rt_debug_refit: 0 one launch (box roles wait, by tickets), 1 two launches, 2 one launch
+        (direct), 3 one launch (box roles wait, in start order; the default)."""
         fn = self._lib.rt_debug_refit
         fn.argtypes = [_P, _I]
         fn.restype = _I
@@ -791,6 +792,14 @@ class ComputeShader:
         if k < 0:
             raise RTError("rt_debug_sched_order", k)
         return buf[:k].copy()
+
+    def debug_refit_stats(self):
+        """The refit's shape: dirty slots, largest / total prim range, nodes, entries."""
+        fn = self._lib.rt_debug_refit_stats
+        fn.argtypes = [_P, C.c_void_p]
+        out = np.zeros(5, np.int64)
+        self._chk(fn(self._h, out.ctypes.data), "rt_debug_refit_stats")
+        return dict(zip(["dirty_slots", "max_range", "sum_range", "nodes", "entries"], out.tolist()))
 
     def debug_moving(self, period, dilate, split):
         """Cost order of dispatches whose camera moved: re-derived every `period` frames

@@ -260,10 +260,10 @@ def test_kernel_timing_off_reports_nothing(ctx):
 def test_animated_mt_and_brute_frames_refit(ctx, fresh, mode):
     """Moller-Trumbore and brute-force frames of an animated scene: the sub-contexts
     (the MT accelerator, the one-leaf brute tree) follow rt_animate / rt_update_shapes
-    by the same device refit (MT: boxes, cones and per-ray padding constants merged
-    grow-only, the axis slab dropped) instead of the literal scan or a rebuild. Every
-    frame equals a fresh upload of the same scene (the accelerator built from scratch)
-    bit for bit, and the oracle at the end."""
+    by the same device refit (MT: boxes, grazing cones, per-ray padding constants and
+    axis slabs recomputed from the current records) instead of the literal scan or a
+    rebuild. Every frame equals a fresh upload of the same scene (the accelerator built
+    from scratch) bit for bit, and the oracle at the end."""
     W, H = 192, 108
     fs = rtamd.generate(3, 0, W, H)
     ids, frames = bench.wheel_frames(fs, 8)
@@ -292,3 +292,36 @@ def test_animated_mt_and_brute_frames_refit(ctx, fresh, mode):
         ru.upload(ctx, frames[(k + 3) % 8])
         fresh.upload(ru.scene(host))
         same(ctx.render(W, H), fresh.render(W, H), f"{mode} reference upload {k}")
+
+
+@pytest.mark.parametrize("refit", [0, 1, 2, 3])
+def test_refit_launch_modes_equal_fresh_upload(ctx, fresh, refit):
+    """Every launch shape of k_refit (rt_debug_refit: 0 one launch ordered by tickets,
+    1 two launches, 2 one launch reading the records itself, 3 one launch in start
+    order -- the default) refits the car's turning wheels to the frames of a fresh
+    upload, bit for bit, barycentric (back-face cones recomputed) and Moller-Trumbore."""
+    W, H = 192, 108
+    fs = rtamd.generate(3, 0, W, H)
+    ids, frames = bench.wheel_frames(fs, 6)
+    try:
+        for mt in (False, True):
+            host = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+            ctx.upload(fs)
+            ctx.debug_refit(refit)
+            ctx.set_params(W, H, 3, True, False, mt)
+            ctx.set_kernel(rtamd.KERNEL_AUTO)
+            ctx.set_animated(ids)
+            ctx.render(W, H)
+            r0 = ctx.debug_anim_rebuilds()
+            for k in range(6):
+                ctx.animate(frames[k])
+                host.shapes[ids] = frames[k]
+                oracle.update_bvh(host, ids)
+                fresh.upload(host)
+                fresh.set_params(W, H, 3, True, False, mt)
+                fresh.set_kernel(rtamd.KERNEL_AUTO)
+                same(ctx.render(W, H), fresh.render(W, H), f"refit {refit} mt {mt} frame {k}")
+            assert ctx.debug_anim_rebuilds() == r0
+    finally:
+        ctx.debug_refit(3)
+        ctx.set_animated(np.zeros(0, np.int32))

@@ -54,7 +54,8 @@ def main():
     print(json.dumps({"config": a.config, "upload": a.upload, "frames": a.frames, "latency_mode": a.latency, "refit_mode": a.refit,
                       "median_ms": float(np.median(ms)), "p10_ms": float(np.percentile(ms, 10)),
                       "p90_ms": float(np.percentile(ms, 90)), "warm_median_ms": float(np.median(warm)),
-                      "rebuilds": ctx.debug_anim_rebuilds(), "refits": ctx.debug_refits()}), flush=True)
+                      "rebuilds": ctx.debug_anim_rebuilds(), "refits": ctx.debug_refits(),
+                      **ctx.debug_refit_stats()}), flush=True)
     ctx.close()
 
 
