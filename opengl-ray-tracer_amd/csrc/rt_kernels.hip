@@ -1551,7 +1551,10 @@ constexpr int kMtWalkFrom = 1 << 16;      // auto walk policy of Moller-Trumbore
 constexpr int kMtPacketMaxNodes = 1024;  // ... over reference trees of fewer nodes (walk_from)
 // the heaviest tiles of the cost order as several waves (rt_debug_heavy)
 constexpr int kHeavyTiles = -1, kHeavyParts = 4, kHeavyAutoSlots = 2;  // -1: auto
-constexpr int kLatencyMaxSlots = 16;  // latency mode: frames of at most this many tiles per wave slot
+// latency mode: frames of at most this many tiles per wave slot (16 per CU). 12: the car's
+// 3840x2160 half share (64,800 tiles) waited 0.360 ms with it against 0.318 without, its
+// quarter share (32,640) 0.19 against 0.27 (profiles/r05r_share_sweep.json)
+constexpr int kLatencyMaxSlots = 12;
 constexpr unsigned kXcds = 8;  // MI355X: 8 XCDs, workgroups dealt round-robin
 
 __device__ __forceinline__ int work_bucket(unsigned c) {
@@ -2141,6 +2144,7 @@ __device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
 // result); sh: LDS scratch of the workgroup, free again on return.
 constexpr int kRefitWaves = 4;
 constexpr int kRefitFlag0 = 16, kRefitFlags = 16;  // k_refit's all-done flags: ctr[16 + 16 k]
+constexpr long long kDirectReads = 2048;           // rt_ctx::refit_mode auto
 __device__ __forceinline__ void block_minmax(float lo[3], float hi[3], float (*sh)[6]) {
     wave_minmax(lo, hi);
     const int nw = blockDim.x >> 6;
@@ -2589,12 +2593,14 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
 //   [na + nd, ...)      a workgroup each: node role (grow_node) for the first nb, then
 //                       slot role (refit_slot); both read what the record role wrote.
 // Modes (rt_debug_refit), on the car's wheels (640 entries, 650 dirty slots):
-//   1 two launches, records and node sets in one-wave workgroups, then nodes and slots
-//     in kRefitWaves-wave ones: the kernel boundary orders them (11.4 + 8.4 us, r05n);
-//   3 default: ONE launch of kRefitWaves-wave workgroups whose node / slot workgroups
-//     wait (wait 2) until every record workgroup has released its writes. Workgroups
-//     start in index order, record workgroups first, and every one of them runs to its
-//     end without waiting, so the waits end;
+//   1 default: two launches, records and node sets in one-wave workgroups, then nodes
+//     and slots in kRefitWaves-wave ones: the kernel boundary orders them (11.4 + 8.4
+//     us, no gap between them; r05n);
+//   3 ONE launch of kRefitWaves-wave workgroups whose node / slot workgroups wait (wait
+//     2) until every record workgroup has released its writes. Workgroups start in
+//     index order, record workgroups first, and every one of them runs to its end
+//     without waiting, so the waits end. Measured 42 us polling the done counter, 52
+//     us polling kRefitFlags copies of a flag (r05o, r05p): slower than two launches;
 //   0 as 3 with the start order made explicit by a ticket per workgroup (wait 1): the
 //     ticket counter serialises the launch (35 us when measured with one-wave slots);
 //   2 one launch whose node / slot roles derive each entry's boxes from its record over
@@ -2606,7 +2612,7 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
 __global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut o, RefitArgs r) {
     __shared__ float sh[kRefitWaves][6];
     const int tid = threadIdx.x, nt = blockDim.x;
-    unsigned t = blockIdx.x;
+    unsigned t = blockIdx.x;  // without waits the start order does not matter
     if (r.wait == 1) {
         __shared__ unsigned ticket;
         if (tid == 0) ticket = __hip_atomic_fetch_add(r.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.tbase;
@@ -2798,7 +2804,15 @@ struct rt_ctx {
     // rt_debug_refit: 0 one launch (box roles wait on tickets), 1 two launches (default:
     // the car's waited animated frame 0.262 ms against 0.268 and 0.299, r05d), 2 one
     // launch (box roles read the records over the host link themselves)
-    int refit_mode = 3;
+    // rt_debug_refit; -1 auto: one direct launch (mode 2) while the records its readers
+    // fetch over the host link are few (direct_reads <= kDirectReads), else two launches
+    // (mode 1). Waited animated frames, mode 1 against 2: config 2's three spheres (~50
+    // reads) 0.1062 against 0.1024 ms; the car's wheels (~7,500 reads) 0.2449 against
+    // 0.2777 (r05q)
+    int refit_mode = -1;
+    long long direct_reads = 0, n_direct_slot_reads = 0;
+    char* refit_dev = nullptr;  // refit mode 4: the pinned slot's records copied to the device
+    size_t refit_dev_cap = 0;
     long long dirty_sum = 0;  // rt_debug_refit_stats: the slot refit's prim ranges (largest, total)
     int dirty_max = 0;
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
@@ -3193,6 +3207,7 @@ int open_inf_slots(rt_ctx* c) {
 int prepare_animation(rt_ctx* c) {
     const int n = static_cast<int>(c->refit_ids.size());
     c->anim = AnimMaps{};
+    c->n_direct_slot_reads = 0;
     c->refit_of.assign(c->S, -1);
     for (int i = 0; i < n; ++i) c->refit_of[c->refit_ids[i]] = i;
     if (n == 0) return RT_OK;
@@ -3393,6 +3408,7 @@ int prepare_animation(rt_ctx* c) {
                                c->stream));
         HIP_TRY(hipMemcpyAsync(c->refit_list, dl.data(), dl.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
         c->n_dirty = nw;
+        c->n_direct_slot_reads = static_cast<long long>(work.back().w);  // the slots' refit prims
         const int rc = open_inf_slots(c);
         if (rc != RT_OK) return rc;
     }
@@ -3444,6 +3460,8 @@ int prepare_animation(rt_ctx* c) {
     append(prims_of, o[2], o[3]);
     append(wpos_of, o[4], o[5]);
     append(lists_of, o[6], o[7]);
+    c->direct_reads = n + c->n_direct_slot_reads;
+    for (const auto& l : lists_of) c->direct_reads += static_cast<long long>(l.size());
     append(wn_of, o[8], o[9]);
     append(items_of, o[10], o[11]);
     const size_t o_ids = buf.size();
@@ -3640,8 +3658,22 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                 HIP_TRY(hipMemsetAsync(c->refit_ctr, 0, words * sizeof(unsigned), c->stream));
                 c->ctr_tickets = c->ctr_done = 0;
             }
+            // mode 4: the records copied to the device first, then read there by every role
+            // (direct, one launch): one crossing of the host link instead of one per reader
             const char* src = pin_dev;
-            const int waves = c->refit_mode == 2 ? 1 : kRefitWaves;  // per workgroup of a single launch
+            const int mode = c->refit_mode >= 0 ? c->refit_mode : c->direct_reads <= kDirectReads ? 2 : 1;
+            if (mode == 4) {
+                if (c->refit_dev_cap < bytes) {
+                    hipFree(c->refit_dev);
+                    c->refit_dev = nullptr;
+                    c->refit_dev_cap = 0;
+                    if (hipMalloc(&c->refit_dev, bytes) != hipSuccess) return RT_ERR_NO_MEMORY;
+                    c->refit_dev_cap = bytes;
+                }
+                HIP_TRY(hipMemcpyAsync(c->refit_dev, pin, bytes, hipMemcpyHostToDevice, c->stream));
+                src = c->refit_dev;
+            }
+            const int waves = mode == 2 ? 1 : kRefitWaves;  // per workgroup of a single launch
             RefitArgs r{};
             r.fresh = reinterpret_cast<const FlatShape*>(src);
             r.flags = reinterpret_cast<const int*>(src + n * sizeof(FlatShape));
@@ -3650,7 +3682,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             r.ctr = c->refit_ctr;
             r.tbase = c->ctr_tickets;
             r.abase = c->ctr_done;
-            const int per = 64 * (c->refit_mode == 1 ? 1 : waves);  // record / node-set lanes per workgroup
+            const int per = 64 * (mode == 1 ? 1 : waves);  // record / node-set lanes per workgroup
             r.na = (n + per - 1) / per;
             r.N = c->N;
             r.n_items = nodes && acc ? c->n_titems : 0;
@@ -3662,8 +3694,8 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             r.dlist = c->refit_list;
             r.n_dirty = n > 0 && acc ? c->n_dirty : 0;
             r.rec = c->accel.mt ? kWideRecMt : kWideRec;
-            r.wait = c->refit_mode == 0 ? 1 : c->refit_mode == 3 ? 2 : 0;
-            r.direct = c->refit_mode == 2;
+            r.wait = mode == 0 ? 1 : mode == 3 ? 2 : 0;
+            r.direct = mode == 2 || mode == 4;
             // waves per workgroup: the node and slot roles' own launch takes kRefitWaves (a
             // slot's or node's list in one step), a launch with the one-wave roles one
             auto go = [&](const RefitArgs& ra, int waves) -> int {
@@ -3675,7 +3707,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                 if (ra.wait) c->ctr_done += static_cast<unsigned>(ra.na);
                 return RT_OK;
             };
-            if (c->refit_mode == 1) {  // records and node sets, then (a kernel boundary later) the boxes
+            if (mode == 1) {  // records and node sets, then (a kernel boundary later) the boxes
                 RefitArgs r1 = r, r2 = r;
                 r1.nb = r1.n_dirty = 0;
                 r2.na = r2.nd = 0;
@@ -4086,9 +4118,16 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                     // 4 waves: k = 95 0.2362 ms, 126 0.2161, 159 0.2184, 191 0.2203, 255 0.2260;
                     // as 2 waves: 63 0.2371, 127-511 0.224, 1023 0.229; 126 as 8: 0.2275. Some
                     // tiles ranked ~96-126 by whole time gain most from the split, so k sits
-                    // well above that edge (162 of the car's 32,400 tiles)
-                    hk = std::max(16, k2.tiles / 200);
-                    hp = 4;
+                    // well above that edge (162 of the car's 32,400 tiles).
+                    // A frame of few tiles per CU (a rank's stripe share of a strong frame) has
+                    // idle CUs to spread its heaviest chains over: the car's 1/8 share (4,080
+                    // tiles, 16 per CU) waited 0.175 ms by the whole-frame rule, 0.135-0.144 with
+                    // its heaviest 1/25 as 16 waves; the 1/4 share (8,160) 0.175-0.192 against
+                    // 0.156-0.160 with 1/25-1/50 as 8 waves; the 1/2 share mixed (C++ host loop,
+                    // tools/share_sweep.py, profiles/r05s/r05t_share_sweep*.json)
+                    const int per_cu = k2.tiles / std::max(1, c->cu_count);
+                    hk = std::max(16, k2.tiles / (per_cu <= 40 ? 25 : 200));
+                    hp = per_cu <= 20 ? 16 : per_cu <= 40 ? 8 : 4;
                 }
             }
             const bool stamps_fit =  // timed frames split only with a record per part
@@ -4381,6 +4420,7 @@ int rt_destroy(rt_ctx* c) {
     hipFree(c->anim_maps);
     hipFree(c->anim_sbox);
     hipFree(c->refit_ctr);
+    hipFree(c->refit_dev);
     for (int k = 0; k < rt_ctx::kAnimRing; ++k) {
         if (c->anim_pinned[k]) hipHostFree(c->anim_pinned[k]);
         if (c->anim_copied[k]) hipEventDestroy(c->anim_copied[k]);
@@ -4848,7 +4888,7 @@ extern "C" int rt_debug_refit_stats(rt_ctx* c, long long* out) {
 }
 
 extern "C" int rt_debug_refit(rt_ctx* c, int mode) {
-    if (!c || mode < 0 || mode > 3) return RT_ERR_INVALID;
+    if (!c || mode < -1 || mode > 4) return RT_ERR_INVALID;
     c->refit_mode = mode;
     return RT_OK;
 }
@@ -4979,7 +5019,7 @@ extern "C" int rt_debug_sched_order(rt_ctx* c, int* out, int n) {
 // waves (1, 2, 4 or 8), one band of 64 / parts pixels per wave; parts = 1: off;
 // k = -1: the default policy (kHeavyAutoSlots).
 extern "C" int rt_debug_heavy(rt_ctx* c, int k, int parts) {
-    if (!c || k < -1 || (parts != 1 && parts != 2 && parts != 4 && parts != 8)) return RT_ERR_INVALID;
+    if (!c || k < -1 || parts < 1 || parts > 32 || (parts & (parts - 1)) != 0) return RT_ERR_INVALID;
     c->heavy_k = k;
     c->heavy_parts = parts;
     return RT_OK;

@@ -752,7 +752,8 @@ class ComputeShader:
 
     def debug_refit(self, mode):
         """rt_debug_refit: 0 one launch (box roles wait, by tickets), 1 two launches, 2 one launch
-        (direct), 3 one launch (box roles wait, in start order; the default)."""
+        (direct), 3 one launch (box roles wait, in start order), 4 as 2 from a device copy;
+        -1 (the default) 2 for few records, else 1."""
         fn = self._lib.rt_debug_refit
         fn.argtypes = [_P, _I]
         fn.restype = _I

@@ -294,11 +294,12 @@ def test_animated_mt_and_brute_frames_refit(ctx, fresh, mode):
         same(ctx.render(W, H), fresh.render(W, H), f"{mode} reference upload {k}")
 
 
-@pytest.mark.parametrize("refit", [0, 1, 2, 3])
+@pytest.mark.parametrize("refit", [-1, 0, 1, 2, 3, 4])
 def test_refit_launch_modes_equal_fresh_upload(ctx, fresh, refit):
     """Every launch shape of k_refit (rt_debug_refit: 0 one launch ordered by tickets,
     1 two launches, 2 one launch reading the records itself, 3 one launch in start
-    order -- the default) refits the car's turning wheels to the frames of a fresh
+    order, 4 as 2 from a device copy of the records; -1, the default, picks 1 or 2)
+    refits the car's turning wheels to the frames of a fresh
     upload, bit for bit, barycentric (back-face cones recomputed) and Moller-Trumbore."""
     W, H = 192, 108
     fs = rtamd.generate(3, 0, W, H)
@@ -323,5 +324,5 @@ def test_refit_launch_modes_equal_fresh_upload(ctx, fresh, refit):
                 same(ctx.render(W, H), fresh.render(W, H), f"refit {refit} mt {mt} frame {k}")
             assert ctx.debug_anim_rebuilds() == r0
     finally:
-        ctx.debug_refit(3)
+        ctx.debug_refit(-1)
         ctx.set_animated(np.zeros(0, np.int32))

@@ -42,7 +42,9 @@ def main():
     ap.add_argument("--waited", type=int, default=150)
     ap.add_argument("--inflight", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=400)
-    ap.add_argument("--sweep", type=int, default=1, help="latency-mode heavy-split sweep (1080p, P > 1)")
+    ap.add_argument("--sweep", type=int, default=1, help="latency-mode heavy-split sweep (1080p)")
+    ap.add_argument("--sweep-parts", default="2,4", help="waves per split tile in the sweep")
+    ap.add_argument("--sweep-div", default="800,400,200,100,50", help="split k = tiles / each")
     a = ap.parse_args()
     out = {"GPU_MAX_HW_QUEUES": os.environ.get("GPU_MAX_HW_QUEUES"), "shares": []}
     for Hs in [int(x) for x in a.sizes.split(",")]:
@@ -71,10 +73,10 @@ def main():
                 rec["waited_ms"] = waited()
                 ctx.set_latency_mode(1)
                 rec["waited_latency_mode_ms"] = waited()
-                if a.sweep and H == 1080 and P > 1:
+                if a.sweep and H == 1080:
                     sw = {}
-                    for k in sorted({max(16, tiles // d) for d in (800, 400, 200, 100, 50)}):
-                        for parts in (2, 4):
+                    for k in sorted({max(16, tiles // int(d)) for d in a.sweep_div.split(",")}):
+                        for parts in [int(x) for x in a.sweep_parts.split(",")]:
                             ctx.debug_heavy(k, parts)
                             sw[f"{k}x{parts}"] = waited(100)
                     ctx.debug_heavy(-1, 1)
