@@ -2869,6 +2869,8 @@ struct rt_ctx {
 
 namespace {
 
+hipError_t sync_stream(rt_ctx* c);  // hipStreamSynchronize + the refit slots retired (below)
+
 #pragma clang diagnostic ignored "-Wunused-result"
 #define HIP_TRY(x)                                  \
     do {                                            \
@@ -3152,7 +3154,7 @@ int build_upload_accel(rt_ctx* c) {
         hipLaunchKernelGGL(k_pack_prims, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->geo_lin, c->prim_idx_dev,
                            c->prim_idx_dev + P, static_cast<int>(P), c->prims);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));  // the host vectors die here
+    HIP_TRY(sync_stream(c));  // the host vectors die here
     c->st_root = use_st ? static_cast<int>(kLocal | static_cast<unsigned>(nw + T.wroot)) : kNoChild;
     c->accel_ok = true;
     c->record_bytes = (an.size() + ln.size() + wn.size() + tl.size() + ti.size() + 4 * P + 2 * static_cast<size_t>(c->S)) *
@@ -3165,7 +3167,7 @@ int sync_host_nodes(rt_ctx* c) {
     if (!c->nodes_on_device_newer) return RT_OK;
     HIP_TRY(hipMemcpyAsync(c->host_nodes.data(), c->staging_nodes, c->N * sizeof(FlatNode), hipMemcpyDeviceToHost,
                            c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     c->nodes_on_device_newer = false;
     return RT_OK;
 }
@@ -3473,7 +3475,7 @@ int prepare_animation(rt_ctx* c) {
     int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
     if (rc != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     const int* d = c->anim_maps;
     c->anim = AnimMaps{d,        d + o[0], d + o[1],  d + o[2],  d + o[3], d + o[4], d + o[5], d + o_ids,
                        d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], d + o_cls, d + o_pe,
@@ -3534,6 +3536,16 @@ bool host_nodes_nest(const rt_ctx* c) {
 void stream_drained(rt_ctx* c) {
     c->mark_slot = -1;
     for (bool& b : c->slot_busy) b = false;
+}
+
+// hipStreamSynchronize of the context's stream, which also retires its refit slots
+// (and its sub-contexts', which run on the same stream).
+hipError_t sync_stream(rt_ctx* c) {
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess)
+        for (rt_ctx* x : {c, c->brute, c->mtc})
+            if (x) stream_drained(x);
+    return e;
 }
 
 // Records the anim_copied event of the last k_refit's slot if it is still pending.
@@ -4396,7 +4408,7 @@ extern "C" {
 int rt_destroy(rt_ctx* c) {
     if (!c) return RT_ERR_INVALID;
     hipSetDevice(c->device);
-    if (c->stream) hipStreamSynchronize(c->stream);
+    if (c->stream) sync_stream(c);
     if (c->brute) rt_destroy(c->brute);  // it runs on this context's stream
     c->brute = nullptr;
     if (c->mtc) rt_destroy(c->mtc);
@@ -4439,7 +4451,7 @@ int rt_set_stream(rt_ctx* c, void* s) {
     if (!c) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     if (const int rc = record_mark(c)) return rc;  // on the stream the k_refit ran on
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     if (c->own_stream) hipStreamDestroy(c->stream);
     if (s) {
         c->stream = static_cast<hipStream_t>(s);
@@ -4463,7 +4475,7 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     int rc = check_tree(nodes, N, idx, I, S, &ms);
     if (rc != RT_OK) return rc;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     free_scene(c);
     const size_t sS = S > 0 ? S : 1, sI = I > 0 ? I : 1, sN = N > 0 ? N : 1;
     if (hipMalloc(&c->geo_lin, sS * 5 * sizeof(float4)) != hipSuccess ||
@@ -4486,7 +4498,7 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
         hipLaunchKernelGGL(k_pack_nodes, dim3((N + 255) / 256), dim3(256), 0, c->stream, c->staging_nodes, N,
                            c->nodes);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     c->S = S;
     c->N = N;
     c->I = I;
@@ -4625,7 +4637,7 @@ int rt_build_lbvh(rt_ctx* c, float* device_ms) {
         if (rc == RT_OK &&
             (hipMemcpyAsync(nodes.data(), dn, N * sizeof(FlatNode), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
              hipMemcpyAsync(idx.data(), di, S * sizeof(int), hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-             hipStreamSynchronize(c->stream) != hipSuccess))
+             sync_stream(c) != hipSuccess))
             rc = RT_ERR_DEVICE;
         (void)hipFree(dn);
         (void)hipFree(di);
@@ -4658,7 +4670,7 @@ int rt_read_nodes(rt_ctx* c, FlatNode* nodes, int N) {
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     if (const int rc = flush_updates(c)) return rc;
     HIP_TRY(hipMemcpyAsync(nodes, c->staging_nodes, N * sizeof(FlatNode), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     return RT_OK;
 }
 
@@ -4719,7 +4731,7 @@ int rt_dispatch(rt_ctx* c, int width, int height, int y0, int y1) {
     if (!c || width <= 0 || height <= 0 || y0 < 0 || y1 > height || y0 > y1) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     if (width != c->img_w || height != c->img_h || !c->img) {
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        HIP_TRY(sync_stream(c));
         hipFree(c->img);
         c->img = nullptr;
         c->img_w = c->img_h = 0;
@@ -4769,7 +4781,7 @@ int rt_read_image(rt_ctx* c, float* dst, size_t pitch, int width, int height) {
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     HIP_TRY(hipMemcpy2DAsync(dst, pitch, c->img, c->img_pitch, static_cast<size_t>(c->img_w) * 16, c->img_h,
                              hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     return RT_OK;
 }
 
@@ -4802,7 +4814,7 @@ int rt_collect_stats_ex(rt_ctx* c, int width, int height, int y0, int stripe, in
         if (rc == RT_OK) rc = launch(c, kp, true);
         unsigned long long h[ST_COUNT];
         if (rc == RT_OK && (hipMemcpyAsync(h, c->stats_dev, sizeof h, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-                            hipStreamSynchronize(c->stream) != hipSuccess))
+                            sync_stream(c) != hipSuccess))
             rc = RT_ERR_DEVICE;
         if (rc == RT_OK) {
             out->pixels = h[ST_PIXELS];
@@ -4817,7 +4829,7 @@ int rt_collect_stats_ex(rt_ctx* c, int width, int height, int y0, int stripe, in
             out->hits = h[ST_HITS];
         }
     }
-    hipStreamSynchronize(c->stream);
+    sync_stream(c);
     hipFree(scratch);
     return rc;
 }
@@ -5008,7 +5020,7 @@ extern "C" int rt_debug_tile_order(rt_ctx* c, const int* order, int n) {
 extern "C" int rt_debug_sched_order(rt_ctx* c, int* out, int n) {
     if (!c || n < 0 || (n > 0 && !out)) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     const int k = std::min(n, c->sched_valid);
     if (k > 0 && c->sched_order)
         HIP_TRY(hipMemcpy(out, c->sched_order, static_cast<size_t>(k) * sizeof(int), hipMemcpyDeviceToHost));
@@ -5073,7 +5085,7 @@ extern "C" int rt_set_launch(rt_ctx* c, int waves_per_block, int persistent) {
 extern "C" int rt_debug_tile_times(rt_ctx* c, int cap, unsigned long long* out) {
     if (!c || cap < 0) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(sync_stream(c));
     if (out && c->tile_times && cap > 0) {
         const size_t n = std::min(static_cast<size_t>(cap), c->tile_times_cap);
         HIP_TRY(hipMemcpy(out, c->tile_times, n * kTileRec * sizeof(unsigned long long), hipMemcpyDeviceToHost));
