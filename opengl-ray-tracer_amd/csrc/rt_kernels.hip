@@ -2606,7 +2606,10 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
 //   2 one launch whose node / slot roles derive each entry's boxes from its record over
 //     the host link themselves (direct; 72 us).
 // Copying the records to the device before the launches instead of reading them over
-// the host link measured no faster (r05k: waited car frame 0.259 against 0.252 ms).
+// the host link measured no faster (r05k: waited car frame 0.259 against 0.252 ms). The
+// record role's 11 us are not its stores: with every store skipped in turn (timing builds,
+// r05x) it took 10.0-12.2 us, and moved beside the slot roles (its boxes alone in the first
+// launch, r05y) the first launch still took 10.3 us while the second grew to 23.
 // The node-set role never runs with AF_GROW entries in the same flush (flush_updates
 // applies host node records first), so no two roles write the same box.
 __global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut o, RefitArgs r) {
