@@ -2765,7 +2765,8 @@ struct rt_ctx {
     // held still (median ratio over 8 cameras, tools/camera_probe.py, r05h / r05i):
     // the still policy (every 16th frame, undilated) 1.53 / 1.46; every frame undilated
     // 1.26; every 4th dilated by 2 1.16; every frame dilated by 1 1.09 / 1.06, with split
-    // tiles on those frames 1.15 / 1.14.
+    // tiles on those frames 1.15 / 1.14 (a split tile ranked by its parts' sum), 1.15-1.19 by
+    // half or a quarter of it, 1.18 / 1.13 by its longest part (r05z, r05z2).
     int moving_period = 1, moving_dilate = 1, moving_split = 0;
     FlatCamera sched_cam{};
     bool have_sched_cam = false;
