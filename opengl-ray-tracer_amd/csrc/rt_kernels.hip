@@ -4141,9 +4141,14 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                     // its heaviest 1/25 as 16 waves; the 1/4 share (8,160) 0.175-0.192 against
                     // 0.156-0.160 with 1/25-1/50 as 8 waves; the 1/2 share mixed (C++ host loop,
                     // tools/share_sweep.py, profiles/r05s/r05t_share_sweep*.json)
+                    // Off the tuned view the 4-wave split lost: four still cameras along
+                    // bench.py's orbit waited 0.213 / 0.279 / 0.277 / 0.294 ms with it, 0.216 /
+                    // 0.268 / 0.268 / 0.284 as 2 waves (geometric mean over the views 1.034
+                    // against 1.011 of each view's best of a 4 x 3 grid; tools/view_sweep.py,
+                    // profiles/r05za_view_sweep.json): whole frames take 2 waves
                     const int per_cu = k2.tiles / std::max(1, c->cu_count);
                     hk = std::max(16, k2.tiles / (per_cu <= 40 ? 25 : 200));
-                    hp = per_cu <= 20 ? 16 : per_cu <= 40 ? 8 : 4;
+                    hp = per_cu <= 20 ? 16 : per_cu <= 40 ? 8 : 2;
                 }
             }
             const bool stamps_fit =  // timed frames split only with a record per part
