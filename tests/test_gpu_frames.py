@@ -717,3 +717,46 @@ def test_group_refuses_members_changed_behind_its_back(ctx):
         assert np.array_equal(g.read_image(W, H), want)
     finally:
         g.close()
+
+
+def test_moving_camera_cost_order_exact(ctx):
+    """Latency mode with a camera that moves every frame: each dispatch re-derives the
+    cost order from its tiles' whole wall times dilated by one tile (k_cost_dilate, then
+    k_tile_order) for the next. Every frame equals the row-major frame of its own camera,
+    and a still camera after the moves (the still policy again) too."""
+    import bench
+    W, H = 320, 180
+    cfg, _, _, mb, _, target = bench.WORKLOADS[3]
+    sc = rtamd.Scene().generate(cfg, 0, W / H)
+    fs = sc.serializeScene()
+    cams = bench.camera_path(rtamd, sc, fs, "orbit", target)[:48:6]  # 8 cameras, 3 degrees apart
+    ctx.upload(fs)
+    ctx.set_params(W, H, mb, True)
+    ctx.set_kernel(rtamd.KERNEL_ACCEL)
+    refs = []
+    try:
+        ctx.set_schedule(rtamd.SCHED_ROWS)
+        for cam in cams:
+            ctx.set_camera(cam)
+            refs.append(ctx.render(W, H))
+        ctx.set_schedule(rtamd.SCHED_COST)
+        ctx.set_latency_mode(1)
+        full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        for rnd in range(3):
+            for i, cam in enumerate(cams):
+                ctx.set_camera(cam)
+                full.fill_(float("nan"))
+                torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
+                ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
+                ctx.sync()
+                img = full.cpu().numpy()
+                assert np.array_equal(img, refs[i]), f"round {rnd} camera {i}: {int((img != refs[i]).any(axis=-1).sum())} px"
+        for _ in range(20):  # held still: the still policy's split frames
+            ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
+            ctx.sync()
+            assert np.array_equal(full.cpu().numpy(), refs[-1])
+    finally:
+        ctx.set_latency_mode(0)
+        ctx.set_schedule(rtamd.SCHED_COST)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+        ctx.set_camera(fs.camera)

@@ -582,7 +582,7 @@ def test_cost_measures_exact(ctx, cfg, W, H, mb):
 @pytest.mark.gpu
 @pytest.mark.parametrize("cfg,W,H,mb", [(2, 400, 300, 1), (3, 320, 180, 3), (5, 320, 180, 3)])
 def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
-    """rt_debug_heavy: the heaviest tiles of the cost order run as 2/4/8 waves, one
+    """rt_debug_heavy: the heaviest tiles of the cost order run as 2/4/8/16/32 waves, one
     band of pixels each. Frame after frame (cost-recording dispatches included),
     every pixel is written (NaN-poisoned surface) with the row-major frame's value,
     also on a stripe set (a rank's rows) and with compaction (config 5 queues rays
@@ -596,7 +596,7 @@ def test_heavy_tiles_as_several_waves_exact(ctx, cfg, W, H, mb):
         ref = ctx.render(W, H)
         ctx.set_schedule(rtamd.SCHED_COST)
         full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
-        for k, parts in [(-1, 4), (16, 8), (64, 4), (10 ** 6, 2), (7, 8)]:
+        for k, parts in [(-1, 4), (16, 8), (64, 4), (10 ** 6, 2), (7, 8), (40, 16), (12, 32)]:
             ctx.debug_heavy(k, parts)
             for _ in range(10):
                 full.fill_(float("nan"))
