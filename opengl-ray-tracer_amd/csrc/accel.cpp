@@ -4,6 +4,8 @@
 #include "accel_bound.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -800,9 +802,12 @@ struct SceneBuilder {
         };
         float best = INFINITY;
         int best_k = -1, best_axis = -1;
+        // per-thread bin counters, all zero between uses: the sparse sweep clears the bins
+        // it touched, the dense one clears every bin (not 2 KB zeroed per axis and node:
+        // config 5's scene tree has ~45k inner nodes)
+        thread_local int cnt[kMaxBins] = {0}, acnt[kMaxBins] = {0};
         for (int ax = 0; bounded && ax < 3; ++ax) {
             if (!(chi[ax] - clo[ax] > 0)) continue;
-            int cnt[kMaxBins] = {0}, acnt[kMaxBins] = {0};
             Box3 bb[kMaxBins];
             if (n < kBins) {
                 // Few atoms: only the bins they occupy are set up and swept. Growing by
@@ -849,6 +854,7 @@ struct SceneBuilder {
                         best_axis = ax;
                     }
                 }
+                for (int j = 0; j < nu; ++j) cnt[used[j]] = acnt[used[j]] = 0;
                 continue;
             }
             for (auto& x : bb) x = empty_box();
@@ -882,6 +888,8 @@ struct SceneBuilder {
                     best_axis = ax;
                 }
             }
+            std::fill(cnt, cnt + kBins, 0);
+            std::fill(acnt, acnt + kBins, 0);
         }
         int mid = b;
         if (best_k > 0) {
@@ -947,6 +955,15 @@ bool boxes_nest(const FlatNode& p, const FlatNode& ch) {
 // (out.st.wroot = -1 otherwise); st.max_stack <= cap sizes its LDS stack.
 // Binary height bound of the scene tree (median splits below it).
 constexpr int kSceneHeight = 40;
+
+static double prof_t0 = 0;
+static void prof(const char* what) {
+    static const bool on = std::getenv("RTA_BUILD_PROFILE") != nullptr;
+    if (!on) return;
+    const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "  %-28s %8.2f ms\n", what, t - prof_t0);
+    prof_t0 = t;
+}
 
 static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int N, const int* idx,
                              const std::vector<char>& reach, const std::vector<int>& seq_base,
@@ -1026,6 +1043,7 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
             add(unb, ub.data() + q, static_cast<int>(std::min(ub.size(), q + 4) - q), leaf_pad(nd));
     }
     const int nb = static_cast<int>(sb.atoms.size()), nu = static_cast<int>(unb.size());
+    prof("  scene: atoms");
     if (nb + nu == 0) return;
     sb.atoms.insert(sb.atoms.end(), unb.begin(), unb.end());
     // bounded atoms under one SAH tree, unbounded ones under another whose
@@ -1042,7 +1060,9 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
         if (nu > 0) unb_root = root;
     }
     st.height = sb.height;
+    prof("  scene: SAH build");
     build_cones(shapes, T);
+    prof("  scene: cones");
     if (unb_root >= 0) {  // the unbounded subtree is built last: its nodes are [unb_root, end)
         for (size_t j = static_cast<size_t>(unb_root); j < T.lbox.size(); ++j) T.lcone[4 * j + 3] = kNoPrune;
     }
@@ -1104,6 +1124,7 @@ static int build_wide(AccelHost& A, const std::vector<int>& ref_depth, int cap) 
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,
                  int leaf_threshold, int stack_cap, AccelHost& out, bool mt) {
     (void)I;
+    prof_t0 = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
     out = AccelHost();
     out.mt = mt;
     out.content.assign(N, empty_box());
@@ -1292,9 +1313,13 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
         const int swap = (std::isfinite(cl) && std::isfinite(crr) && cl > crr) ? 1 : 0;
         out.flags[k] = axis | (swap << 2) | (bounded ? 8 : 0);
     };
+    prof("leaves");
     visit(N - 1);
+    prof("content boxes");
     build_cones(shapes, out);
+    prof("cones");
     max_stack = std::max(max_stack, build_wide(out, depth, kLaneStack));
+    prof("wide");
     if (max_stack > stack_cap) return false;
     // MT: no scene tree. Its inner boxes bound hits, and an MT hit strays from its
     // triangle on grazing rays; the reference tree's exact boxes decide which leaves
@@ -1302,6 +1327,7 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     // grazing-cone local BVHs inside large leaves).
     if (!mt)
         build_scene_tree(shapes, nodes, N, idx, reach, seq_base, scls, sbox, std::min(stack_cap, kLaneStack), out);
+    prof("scene tree");
     if (out.st.wroot >= 0) max_stack = std::max(max_stack, out.st.max_stack);
     out.max_stack = max_stack;
     return max_stack <= stack_cap;
