@@ -2098,6 +2098,7 @@ struct RefitArgs {
     unsigned tbase, abase;     // their values before this launch
     int na, nd, nb;            // workgroups of the record, node-set and node roles
     const int4* dirty;         // slot refit work list (n_dirty entries after the nb node waves, + 1 end)
+    int n_big;                 // its first n_big slots take a workgroup each, the rest a wave each
     const float4* dstatic;     // per dirty slot: the box of its prims outside the refit set (lo, hi)
     const int* dlist;          // the refit set's prims of each dirty slot (dirty[j].w ..)
     int n_dirty, rec;          // its length; the wide record size (kWideRec / kWideRecMt)
@@ -2145,6 +2146,7 @@ __device__ __forceinline__ void wave_minmax(float lo[3], float hi[3]) {
 constexpr int kRefitWaves = 4;
 constexpr int kRefitFlag0 = 16, kRefitFlags = 16;  // k_refit's all-done flags: ctr[16 + 16 k]
 constexpr long long kDirectReads = 2048;           // rt_ctx::refit_mode auto
+constexpr int kBigList = 256;                      // a slot's refit list a wave unions in one step
 __device__ __forceinline__ void block_minmax(float lo[3], float hi[3], float (*sh)[6]) {
     wave_minmax(lo, hi);
     const int nw = blockDim.x >> 6;
@@ -2552,13 +2554,14 @@ __device__ void refit_slot_mt(const AnimMaps& m, const AnimOut& o, const RefitAr
 // LocalBuilder), the scene tree's top slots span every prim (the car: 4,020, against
 // 640 refit prims). dirty[j] = (4*w + s, first prim, end prim, first of its dlist
 // entries); dirty[j + 1].w ends them.
-__device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, float (*sh)[6]) {
-    const int tid = threadIdx.x, lane = tid & 63;
+__device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs& r, int j, float (*sh)[6],
+                           bool block) {
+    const int tid = block ? threadIdx.x : threadIdx.x & 63, lane = tid & 63;
     const int4 d = r.dirty[j];
     const float4* __restrict__ pbox = o.pbox;
     const float4 s0 = r.dstatic[2 * j], s1 = r.dstatic[2 * j + 1];
     float lo[3] = {s0.x, s0.y, s0.z}, hi[3] = {s1.x, s1.y, s1.z};
-    range4(d.w, r.dirty[j + 1].w, tid, blockDim.x,
+    range4(d.w, r.dirty[j + 1].w, tid, block ? static_cast<int>(blockDim.x) : 64,
         [&](int q) {
             const int p = r.dlist[q];
             const int e = r.direct ? m.prim_entry[p] : -1;
@@ -2574,7 +2577,10 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
             lo[0] = fminf(lo[0], a.x), lo[1] = fminf(lo[1], a.y), lo[2] = fminf(lo[2], a.z);
             hi[0] = fmaxf(hi[0], b.x), hi[1] = fmaxf(hi[1], b.y), hi[2] = fmaxf(hi[2], b.z);
         });
-    block_minmax(lo, hi, sh);
+    if (block)
+        block_minmax(lo, hi, sh);
+    else
+        wave_minmax(lo, hi);
     if (tid >= 64) return;  // the cones: one wave
     const int w = d.x >> 2, sl = d.x & 3;
     if (lane < 6) {  // rows 0-5 of the wide record: lo.xyz, hi.xyz
@@ -2654,11 +2660,18 @@ __global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut 
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    const int w = static_cast<int>(t);
-    if (w < r.nb)
-        grow_node(m, o, r, w, sh);
-    else if (w - r.nb < r.n_dirty)
-        refit_slot(m, o, r, w - r.nb, sh);
+    const int w = static_cast<int>(t) - r.nb;
+    if (w < 0) {
+        grow_node(m, o, r, w + r.nb, sh);
+        return;
+    }
+    const int nbig = min(r.n_big, r.n_dirty);
+    if (w < nbig) {
+        refit_slot(m, o, r, w, sh, true);  // a long list: the whole workgroup
+        return;
+    }
+    const int j = nbig + (w - nbig) * (nt >> 6) + (tid >> 6);  // a wave per slot
+    if (j < r.n_dirty) refit_slot(m, o, r, j, sh, false);
 }
 
 // Scene-tree wide slots of the unbounded subtree (kNoPrune): their boxes are the
@@ -2849,6 +2862,7 @@ struct rt_ctx {
     size_t anim_sbox_cap = 0;
     float4* pbox = nullptr;             // per prim conservative box (AnimOut::pbox)
     int4* refit_dirty = nullptr;        // k_refit's slot work list (RefitArgs::dirty)
+    int n_big = 0;                      // its first n_big slots have long refit lists (RefitArgs::n_big)
     float4* refit_static = nullptr;     // RefitArgs::dstatic
     int* refit_list = nullptr;          // RefitArgs::dlist
     int n_dirty = 0;
@@ -3370,6 +3384,22 @@ int prepare_animation(rt_ctx* c) {
         // per dirty slot: the box of its prims outside the refit set (they never move
         // while this set stands) and the list of those in it, which k_refit unions per frame
         c->dirty_max = c->dirty_sum = 0;
+        // slots whose refit list takes a wave more than one step (kBigList) first, one
+        // workgroup each; the rest kRefitWaves to a workgroup, one wave each (k_refit)
+        {
+            std::vector<char> big(work.size(), 0);
+            for (size_t q = 0; q < work.size(); ++q) {
+                int n_ref = 0;
+                for (int p = work[q].y; p < work[q].z; ++p) n_ref += which[A.prim_shape[p]] >= 0;
+                big[q] = n_ref > kBigList;
+            }
+            std::vector<int4> ord;
+            for (int pass = 1; pass >= 0; --pass)
+                for (size_t q = 0; q < work.size(); ++q)
+                    if (big[q] == pass) ord.push_back(work[q]);
+            c->n_big = static_cast<int>(std::count(big.begin(), big.end(), 1));
+            work.swap(ord);
+        }
         std::vector<float4> st(2 * (work.empty() ? 1 : work.size()));
         std::vector<int> dl;
         for (size_t q = 0; q < work.size(); ++q) {
@@ -3706,6 +3736,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             r.nd = nodes ? (c->N + r.n_items + per - 1) / per : 0;
             r.nb = n > 0 ? c->anim.nodes : 0;
             r.dirty = c->refit_dirty;
+            r.n_big = c->n_big;
             r.dstatic = c->refit_static;
             r.dlist = c->refit_list;
             r.n_dirty = n > 0 && acc ? c->n_dirty : 0;
@@ -3715,7 +3746,8 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             // waves per workgroup: the node and slot roles' own launch takes kRefitWaves (a
             // slot's or node's list in one step), a launch with the one-wave roles one
             auto go = [&](const RefitArgs& ra, int waves) -> int {
-                const int grid = ra.na + ra.nd + ra.nb + ra.n_dirty;
+                const int small = std::max(0, ra.n_dirty - ra.n_big);
+                const int grid = ra.na + ra.nd + ra.nb + std::min(ra.n_big, ra.n_dirty) + (small + waves - 1) / waves;
                 if (grid == 0) return RT_OK;
                 hipLaunchKernelGGL(k_refit, dim3(grid), dim3(64 * waves), 0, c->stream, c->anim, out, ra);
                 HIP_TRY(hipGetLastError());
