@@ -4177,10 +4177,13 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                     // bench.py's orbit waited 0.213 / 0.279 / 0.277 / 0.294 ms with it, 0.216 /
                     // 0.268 / 0.268 / 0.284 as 2 waves (geometric mean over the views 1.034
                     // against 1.011 of each view's best of a 4 x 3 grid; tools/view_sweep.py,
-                    // profiles/r05za_view_sweep.json): whole frames take 2 waves
+                    // profiles/r05za_view_sweep.json): whole frames that walk rays per lane take
+                    // 2 waves. All-packet frames keep 4: the MT car's waited frame took 2.68 ms
+                    // with 2 against 1.75 with 4 (r05zl)
                     const int per_cu = k2.tiles / std::max(1, c->cu_count);
+                    const bool lanes = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces;
                     hk = std::max(16, k2.tiles / (per_cu <= 40 ? 25 : 200));
-                    hp = per_cu <= 20 ? 16 : per_cu <= 40 ? 8 : 2;
+                    hp = per_cu <= 20 ? 16 : per_cu <= 40 ? 8 : lanes ? 2 : 4;
                 }
             }
             const bool stamps_fit =  // timed frames split only with a record per part
