@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--div", default="400,200,100,50")
     ap.add_argument("--parts", default="2,4,8")
     ap.add_argument("--frames", type=int, default=120)
+    ap.add_argument("--mt", action="store_true", help="useMollerTrumbore = 1")
     a = ap.parse_args()
     import torch
     import bench
@@ -36,7 +37,7 @@ def main():
     buf = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
     ctx = rtamd.ComputeShader(0)
     ctx.upload(fs)
-    ctx.set_params(W, H, mb, True)
+    ctx.set_params(W, H, mb, True, False, a.mt)
     ctx.set_kernel_timing(0)
     ctx.set_latency_mode(1)
     tiles = ((W + 7) // 8) * ((H + 7) // 8)
@@ -45,7 +46,7 @@ def main():
         rtamd.render_loop(ctx, cam, fs.light, W, H, buf.data_ptr(), W * 16, 48, True)  # the order settles
         return float(np.median(rtamd.render_loop(ctx, cam, fs.light, W, H, buf.data_ptr(), W * 16, a.frames, True)))
 
-    out = {"config": a.config, "tiles": tiles, "views": []}
+    out = {"config": a.config, "mt": a.mt, "tiles": tiles, "views": []}
     for k in range(a.samples):
         i = int(round(k * len(cams) / a.samples)) % len(cams)
         cam = cams[i:i + 1]
