@@ -4178,8 +4178,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                     // 0.268 / 0.268 / 0.284 as 2 waves (geometric mean over the views 1.034
                     // against 1.011 of each view's best of a 4 x 3 grid; tools/view_sweep.py,
                     // profiles/r05za_view_sweep.json): whole frames that walk rays per lane take
-                    // 2 waves. All-packet frames keep 4: the MT car's waited frame took 2.68 ms
-                    // with 2 against 1.75 with 4 (r05zl)
+                    // 2 waves. All-packet frames (the MT car) keep 4: 2.68 ms with 2 against 1.75
+                    // (r05zl); the heaviest 1/400 as 8, best over two orbit views (geometric mean
+                    // 1.782 against 1.864 ms, r05zn_view_sweep_mt.json), measured 1.770 against
+                    // 1.755 at the bench's view and 1.933 against 1.844 animated (r05zo): kept 4
                     const int per_cu = k2.tiles / std::max(1, c->cu_count);
                     const bool lanes = std::min(k2.lane_from_depth, k2.shadow_lane_from) < k2.maxBounces;
                     hk = std::max(16, k2.tiles / (per_cu <= 40 ? 25 : 200));
