@@ -117,6 +117,8 @@ def parse(argv=None):
                          "1 and 2, timed on every rank before the measured steps")
     ap.add_argument("--schedule", default="cost", choices=["cost", "xcd", "rows"],
                     help="tile dispatch order (rt_set_schedule): cost (default), cost dealt to XCDs as bands, rows")
+    ap.add_argument("--refit", type=int, default=-1,
+                    help="diagnostics: rt_debug_refit launch shape of the refit (-1: the library's choice)")
     ap.add_argument("--walk", type=int, default=-1,
                     help="walk policy (rt_set_walk): -1 auto, 0 all per lane, >= maxBounces all packets")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU-baseline sample time")
@@ -500,6 +502,7 @@ def main():
             c_.set_kernel(kernel_id)
             c_.set_schedule(SCHEDULES[a.schedule])
             c_.set_walk(a.walk)
+            c_.debug_refit(a.refit)
         ctxs = list(grp.contexts)
     else:
         streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(F - 1)]
@@ -511,6 +514,7 @@ def main():
             c_.set_kernel(kernel_id)
             c_.set_schedule(SCHEDULES[a.schedule])
             c_.set_walk(a.walk)
+            c_.debug_refit(a.refit)
             ctxs.append(c_)
             bufs.append(torch.empty((plan.rows_max, W, 4), dtype=torch.float32, device=dev))
     ctx = ctxs[0]
