@@ -259,11 +259,15 @@ int rt_set_schedule(struct rt_ctx* ctx, int mode);
  * reference's own loop, src/main.cpp:290-462) rather than keeping frames in
  * flight. 1: the accelerated kernel's instance with split walks in sparse
  * waves (idle lanes help a tile's few live rays) and, on frames not already
- * split, the heaviest 1/200 of the tiles as four waves each. Shortens one frame
- * (car: -19 %) and costs throughput when frames overlap. Frames of more than 16
- * tiles per wave slot (65,536 8x8 tiles on 256 CUs: 3840x2160 has 129,600)
- * render as in the default mode, which is faster for them. 0 (default): off.
- * Same image either way. */
+ * split, the heaviest tiles of the cost order as several waves each: 1/200 as
+ * two (four for all-packet frames such as Moller-Trumbore's), and on frames of
+ * few tiles per CU (a rank's share of a strong multi-GPU frame) 1/25 as eight or
+ * sixteen. A dispatch whose camera moved since the last one re-ranks the tiles
+ * after every frame (whole-tile wall times, each tile ranked by the largest
+ * within one tile). Shortens one frame (car: -18 %) and costs throughput when
+ * frames overlap. Frames of more than 12 tiles per wave slot (49,152 8x8 tiles
+ * on 256 CUs: 3840x2160 has 129,600) render as in the default mode, which is
+ * faster for them. 0 (default): off. Same image either way. */
 int rt_set_latency_mode(struct rt_ctx* ctx, int on);
 
 /* Ray compaction in the accelerated kernel: the rays still alive after bounce
