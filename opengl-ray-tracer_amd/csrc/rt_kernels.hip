@@ -1843,23 +1843,10 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
         const int cnt = b + lane < kp.tail_regions ? kp.tail_count[b + lane] : 0;
         total += wave_sum_int((cnt + 63) >> 6);
     }
-#ifndef RT_TAIL_XCD
-#define RT_TAIL_XCD 0  // experiment (A/B pending): chunks in XCD-contiguous eighths
-#endif
-    // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (workgroup b runs on XCD
-    // b % 8), so XCD x takes the x-th eighth of the chunks (region after region), its
-    // waves striding over them: each XCD's L2 holds what one band of regions' rays touch
-    const int wpb = static_cast<int>(blockDim.x >> 6), wave = static_cast<int>(threadIdx.x >> 6);
-    int chunk0 = static_cast<int>(blockIdx.x) * wpb + wave, limit = total, stride = waves;
-    if (RT_TAIL_XCD) {
-        const int G = static_cast<int>(gridDim.x), x = static_cast<int>(blockIdx.x % kXcds);
-        const int nx = G / static_cast<int>(kXcds) + (x < G % static_cast<int>(kXcds) ? 1 : 0);
-        const int c8 = (total + static_cast<int>(kXcds) - 1) / static_cast<int>(kXcds);
-        chunk0 = x * c8 + static_cast<int>(blockIdx.x / kXcds) * wpb + wave;
-        limit = min(total, (x + 1) * c8);
-        stride = nx * wpb;
-    }
-    for (int chunk = chunk0; chunk < limit; chunk += stride) {
+    // (r05: the chunks in XCD-contiguous eighths, each XCD's L2 on one band of regions,
+    // measured slower on config 5: 2.734 against 2.689 ms in flight, 3.419 against 3.292
+    // solo; profiles/r05zs_abf_tail_xcd_negative_*.json)
+    for (int chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); chunk < total; chunk += waves) {
         // the region holding chunk: running prefix of the regions' chunk counts
         int rid = 0, first = 0, n = 0, acc0 = 0;
         for (int b = 0; b < kp.tail_regions; b += 64) {
@@ -1904,7 +1891,7 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
                                             kp.lane_from_depth, kp.shadow_lane_from);
         }
         if (have) store_px(kp, r, x, make_float4(acc.x, acc.y, acc.z, 1.0f));
-        if (kTailOneShot && !RT_TAIL_XCD) break;  // one chunk per wave: no loop-carried state
+        if (kTailOneShot) break;  // one chunk per wave: no loop-carried state
     }
     if (blockIdx.x == 0)
         for (int b = threadIdx.x; b < kp.tail_counters; b += blockDim.x) kp.tail_count_next[b] = 0;
