@@ -2612,7 +2612,9 @@ __device__ void refit_slot(const AnimMaps& m, const AnimOut& o, const RefitArgs&
 //     2) until every record workgroup has released its writes. Workgroups start in
 //     index order, record workgroups first, and every one of them runs to its end
 //     without waiting, so the waits end. Measured 42 us polling the done counter, 52
-//     us polling kRefitFlags copies of a flag (r05o, r05p): slower than two launches;
+//     us polling kRefitFlags copies of a flag (r05o, r05p), 29 us with one agent-scope
+//     fence per workgroup instead of one per thread (each writes back or invalidates the
+//     XCD's L2; r05zv): slower than two launches;
 //   0 as 3 with the start order made explicit by a ticket per workgroup (wait 1): the
 //     ticket counter serialises the launch (35 us when measured with one-wave slots);
 //   2 one launch whose node / slot roles derive each entry's boxes from its record over
@@ -2637,9 +2639,11 @@ __global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut 
     if (t < static_cast<unsigned>(r.na)) {
         refit_record(m, o, r, static_cast<int>(t) * nt + tid);
         if (r.wait) {
-            __threadfence();  // this thread's writes, then the workgroup's release
+            // the workgroup's writes complete (barrier), then ONE agent-scope release: each
+            // fence writes the XCD's L2 back, and one per thread cost the launch ~30 us
             __syncthreads();
             if (tid == 0) {
+                __threadfence();
                 const unsigned done = __hip_atomic_fetch_add(r.ctr + 1, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
                 if (done - r.abase == static_cast<unsigned>(r.na) - 1u)  // the last one: raise the flags
                     for (int k = 0; k < kRefitFlags; ++k)
@@ -2659,12 +2663,13 @@ __global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut 
         // one of kRefitFlags copies of the all-done flag, a cache line each: ~650 waiting
         // workgroups polling the counter itself held its increments back (car: 42 us)
         const unsigned* flag = r.ctr + kRefitFlag0 + 16 * (blockIdx.x % kRefitFlags);
-        if (tid == 0)
+        if (tid == 0) {
             while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.abase <
                    static_cast<unsigned>(r.na))
                 __builtin_amdgcn_s_sleep(2);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one invalidation per workgroup
+        }
         __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     const int w = static_cast<int>(t) - r.nb;
     if (w < 0) {
