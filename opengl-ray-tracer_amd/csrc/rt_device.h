@@ -109,8 +109,8 @@ struct KParams {
                                              // waves each, one band of 64/heavy_parts pixels per wave
     unsigned* __restrict__ tile_cost;        // optional: each tile's work (rt_set_schedule)
     int cost_time;                           // tile_cost in wave wall-clock ticks, not lane work
-    unsigned* __restrict__ heavy_acc;        // with tile_cost and heavy_k: per split tile its parts' summed
-                                             // work, then per split tile the parts done (zeroed per dispatch)
+    unsigned long long* __restrict__ heavy_acc;  // with tile_cost and heavy_k: per split tile its parts done
+                                                 // (bits 56..63) and summed work (bits 0..55), zeroed per dispatch
     unsigned* __restrict__ sched_hist;       // with tile_cost: work-bucket histogram copies of this frame
     int lane_from_depth;                     // k_accel: bounces >= this walk per lane
     int shadow_lane_from;                    // k_accel: shadow walks of bounces >= this walk per lane
@@ -119,7 +119,8 @@ struct KParams {
     int lane_stack;                          // per-lane LDS stack entries
     // compaction (rt_set_tail): k_accel queues the rays alive after bounce tail_from - 1,
     // k_accel_tail runs their remaining bounces 64 to a wave; tail_queue == nullptr: off
-    float4* __restrict__ tail_queue;         // 4 float4 per ray: o|acc.x, d|acc.y, att|acc.z, row, x
+    float4* __restrict__ tail_queue;         // 3 float4 per ray: o|acc.x, d|acc.y, att|acc.z
+    int* __restrict__ tail_px;               // per queued ray its pixel, row * width + x (52 B a ray, was 64)
     int* __restrict__ tail_count;            // per region: rays queued by this dispatch
     int* __restrict__ tail_count_next;       // the next dispatch's counters (zeroed by k_accel_tail)
     int tail_from;

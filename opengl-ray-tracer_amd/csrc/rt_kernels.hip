@@ -1687,11 +1687,11 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
                     const int lane = threadIdx.x & 63;
                     const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
                     const PixelCoord pc = tile_pixel(kp, tile);
-                    float4* q = kp.tail_queue + 4 * static_cast<size_t>(pos);
+                    float4* q = kp.tail_queue + 3 * static_cast<size_t>(pos);
                     q[0] = make_float4(ray.o.x, ray.o.y, ray.o.z, acc.x);
                     q[1] = make_float4(ray.d.x, ray.d.y, ray.d.z, acc.y);
                     q[2] = make_float4(att.x, att.y, att.z, acc.z);
-                    q[3] = make_float4(__int_as_float(pc.r), __int_as_float(pc.x), 0.f, 0.f);
+                    kp.tail_px[pos] = pc.r * kp.width + pc.x;
                 }
             }
             deferred = alive;
@@ -1798,12 +1798,15 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel(AccelPtrs A, con
                 // heavy tile whose first band is sky then ranked low, ran whole and late,
                 // ranked high again, and so on (the latency-mode car waited frame 0.25 or
                 // 0.287 ms by the phase of that cycle, r04l)
+                // One 64-bit atomic carries both the count and the sum, so the last part reads
+                // the total from its own return value: no agent-scope fences (each writes back
+                // or invalidates the XCD's L2, the cost that sank the in-kernel dilation).
                 const int hk = slot / kp.heavy_parts;
-                atomicAdd(&kp.heavy_acc[hk], wk);
-                __threadfence();
-                if (atomicAdd(&kp.heavy_acc[kp.heavy_k + hk], 1u) == static_cast<unsigned>(kp.heavy_parts - 1)) {
-                    __threadfence();
-                    wk = atomicAdd(&kp.heavy_acc[hk], 0u);
+                const unsigned long long old =
+                    atomicAdd(&kp.heavy_acc[hk], (1ull << 56) | static_cast<unsigned long long>(wk));
+                if (static_cast<int>(old >> 56) == kp.heavy_parts - 1) {
+                    const unsigned long long sum = (old & ((1ull << 56) - 1)) + wk;
+                    wk = static_cast<unsigned>(sum < 0xffffffffull ? sum : 0xffffffffull);
                     rec = true;
                 }
             }
@@ -1874,13 +1877,14 @@ __global__ __launch_bounds__(kBlock) RT_ACCEL_ATTR void k_accel_tail(AccelPtrs A
         V acc = mk(0.f, 0.f, 0.f), att = mk(1.f, 1.f, 1.f);
         int r = 0, x = 0;
         if (alive) {
-            const float4* q = kp.tail_queue + 4 * static_cast<size_t>(i);
-            const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+            const float4* q = kp.tail_queue + 3 * static_cast<size_t>(i);
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+            const unsigned px = static_cast<unsigned>(kp.tail_px[i]);
             ray = Ray{mk(q0.x, q0.y, q0.z), mk(q1.x, q1.y, q1.z)};
             acc = mk(q0.w, q1.w, q2.w);
             att = mk(q2.x, q2.y, q2.z);
-            r = __float_as_int(q3.x);
-            x = __float_as_int(q3.y);
+            r = static_cast<int>(px / static_cast<unsigned>(kp.width));
+            x = static_cast<int>(px - static_cast<unsigned>(r) * static_cast<unsigned>(kp.width));
         }
         const bool have = alive;
         WalkCount wc{0u, 0u, 0u, 0u};
@@ -2771,7 +2775,7 @@ struct rt_ctx {
     // rt_set_schedule: per-tile durations of the last dispatch and the order derived from them
     int schedule = RT_SCHED_COST;
     unsigned* sched_cost = nullptr;
-    unsigned* heavy_acc = nullptr;  // split heavy tiles' part sums + counts (cost-recording dispatches)
+    unsigned long long* heavy_acc = nullptr;  // split heavy tiles' part counts + sums (cost-recording dispatches)
     size_t heavy_acc_cap = 0;
     int* sched_order = nullptr;
     unsigned* sched_sets = nullptr;      // 2 sets of per-group bucket histograms, alternating by frame
@@ -4221,15 +4225,15 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         k2.cost_time = c->cost_time != 0 ? 1 : 0;
         k2.heavy_acc = nullptr;
         if (k2.tile_cost && k2.heavy_k > 0) {  // the split tiles' part sums and counts (kernel comment)
-            const size_t need = 2 * static_cast<size_t>(k2.heavy_k);
+            const size_t need = static_cast<size_t>(k2.heavy_k);
             if (c->heavy_acc_cap < need) {
                 hipFree(c->heavy_acc);
                 c->heavy_acc = nullptr;
                 c->heavy_acc_cap = 0;
-                if (hipMalloc(&c->heavy_acc, need * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                if (hipMalloc(&c->heavy_acc, need * sizeof(unsigned long long)) != hipSuccess) return RT_ERR_NO_MEMORY;
                 c->heavy_acc_cap = need;
             }
-            HIP_TRY(hipMemsetAsync(c->heavy_acc, 0, need * sizeof(unsigned), c->stream));
+            HIP_TRY(hipMemsetAsync(c->heavy_acc, 0, need * sizeof(unsigned long long), c->stream));
             k2.heavy_acc = c->heavy_acc;
         }
         // Animated scenes keep the scene tree: rt_animate refits its boxes and items (prepare_animation).
@@ -4255,7 +4259,9 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 hipFree(c->tail_queue);
                 c->tail_queue = nullptr;
                 c->tail_cap = 0;
-                if (hipMalloc(&c->tail_queue, need * 4 * sizeof(float4)) != hipSuccess) return RT_ERR_NO_MEMORY;
+                // 3 float4 records, then the pixel words (rt_device.h, tail_queue)
+                if (hipMalloc(&c->tail_queue, need * (3 * sizeof(float4) + sizeof(int))) != hipSuccess)
+                    return RT_ERR_NO_MEMORY;
                 c->tail_cap = need;
             }
             if (regions > c->tail_regions_cap) {
@@ -4268,6 +4274,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                 c->tail_regions_cap = regions;
             }
             k2.tail_queue = c->tail_queue;
+            k2.tail_px = reinterpret_cast<int*>(c->tail_queue + 3 * c->tail_cap);
             k2.tail_count = c->tail_counts + c->tail_parity * c->tail_regions_cap;
             k2.tail_count_next = c->tail_counts + (1 - c->tail_parity) * c->tail_regions_cap;
             k2.tail_from = tail_from;
