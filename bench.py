@@ -547,24 +547,36 @@ def main():
     last_cam = [None for _ in range(max(F, 1))]  # per renderer: the camera of its last frame
     anim = None
     if a.animate:
-        if use_group or a.config not in (2, 3, 4):
-            raise SystemExit("--animate: configs 2/3/4 on one GPU or weak mode")
+        if a.config not in (2, 3, 4) or (strong and not use_group):
+            raise SystemExit("--animate: configs 2/3/4; with --gpus N > 1 over rt_group (--gather rt) or --mode weak")
         # the published scenes' animations (README.md:4): scene 1's bouncing spheres
         # (config 2), scene 2's turning wheels (configs 3/4)
         anim = sphere_frames(fs, 512) if a.config == 2 else wheel_frames(fs, 64)
-        for c_ in ctxs:
-            if a.upload == "device":
-                c_.set_animated(anim[0])
-    applied = [[] for _ in ctxs]  # per renderer: the animation frames it was given, in order
+        if a.upload == "device":
+            if use_group:  # every member and frame slot (rt_group_set_animated)
+                grp.set_animated(anim[0])
+            else:
+                for c_ in ctxs:
+                    c_.set_animated(anim[0])
+    # per renderer: the animation frames it was given, in order (over rt_group every slot
+    # context is given every frame: one list)
+    applied = [[] for _ in (ctxs if not use_group else [grp])]
     # --upload reference: each renderer's host keeps its own scene arrays, moved by the
-    # reference's own upload calls
-    ref_up = [rtamd.ReferenceUpload(fs, anim[0]) for _ in ctxs] if anim is not None and a.upload == "reference" \
-        else None
+    # reference's own upload calls (over rt_group: one host, its calls given to every slot)
+    ref_up = ([rtamd.ReferenceUpload(fs, anim[0]) for _ in (ctxs if not use_group else [grp])]
+              if anim is not None and a.upload == "reference" else None)
 
     def frame(i, inflight):
         if use_group:
             grp.set_camera(cams[i % len(cams)])    # SSBO 2 (src/main.cpp:328-330)
+            last_cam[0] = i % len(cams)
             grp.set_light(light)   # SSBO 1 (:332-334)
+            if ref_up is not None:  # the reference's upload calls, on every member and slot
+                ref_up[0].upload(grp, anim[1][i % len(anim[1])])
+                applied[0].append(i % len(anim[1]))
+            elif anim is not None:
+                grp.animate(anim[1][i % len(anim[1])])  # rt_group_animate: the device refit on every slot
+                applied[0].append(i % len(anim[1]))
             grp.dispatch(W, H, a.stripe)  # this rank's stripes + send/recv to rank 0 + unstripe there
             if inflight == 1:
                 group_sync()  # one frame at a time: the frame slots would otherwise overlap
@@ -640,19 +652,29 @@ def main():
     if use_group:
         verdict = torch.zeros(1, dtype=torch.int64, device="cpu" if gloo else dev)
         want = None
+        solo = None
         if rank == 0:
             solo = rtamd.ComputeShader(torch.cuda.current_device())
             solo.upload(fs)
             solo.set_params(W, H, mb, not a.brute, a.fresnel, a.mt)
             solo.set_kernel(kernel_id)
-            want = solo.render(W, H).view(np.uint32)
-            solo.close()
+            if anim is not None and a.upload == "device":
+                solo.set_animated(anim[0])
+            solo_up = rtamd.ReferenceUpload(fs, anim[0]) if ref_up is not None else None
         bad = []
         for j in range(F):
             frame(j, F)
             group_sync()
             if rank == 0:
+                solo.set_camera(cams[j % len(cams)])
+                if solo_up is not None:  # the same frame's animation, given to one context
+                    solo_up.upload(solo, anim[1][j % len(anim[1])])
+                elif anim is not None:
+                    solo.animate(anim[1][j % len(anim[1])])
+                want = solo.render(W, H).view(np.uint32)
                 bad.append(int((grp.read_image(W, H).view(np.uint32) != want).any(axis=-1).sum()))
+        if solo is not None:
+            solo.close()
         if rank == 0:
             verdict[0] = sum(bad)
             selfcheck = {"frames": F, "bad_pixels_per_slot": bad, "against": "rank 0's single-GPU frame (bit-exact)",
@@ -878,6 +900,23 @@ def main():
         if moving:
             out["camera_path"] = {"kind": a.camera_path, "cameras": len(cams),
                                   "last_camera_per_renderer": [x for x in last_cam if x is not None]}
+        if use_group and anim is not None:
+            # rank 0's last gathered frame against the oracle rendering the group's scene
+            # (every slot context was given every frame: the last records, and the node
+            # boxes grown by all of them); outside the timed region, whole frame
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle  # noqa: E402  (checker only)
+            group_sync()
+            img = grp.read_image(W, H)
+            fk = (ref_up[0].scene(fs) if ref_up is not None else animated_oracle_scene(fs, anim[0], anim[1], applied[0]))
+            fk.camera = cams[last_cam[0]:last_cam[0] + 1].copy()
+            ref, _ = oracle.render(fk, W, H, oracle.params(W, H, mb, not a.brute, a.fresnel, a.mt), threads=thr)
+            chk = parity_check([img], 0, ref, "")
+            out["parity"] = dict(chk, frames_checked=1, rows_checked=[0, H],
+                                 against=("oracle/rt_oracle.c (GLSL restated) on rank 0's last gathered frame: its "
+                                          "camera, the group's last records and node boxes grown over every frame "
+                                          "it was given"),
+                                 animation_frames_applied=[len(applied[0])])
         if mode == "frames" and (anim is not None or moving):
             # every renderer's last timed frame against the oracle rendering that
             # renderer's scene: its last frame's camera, and when animated its last

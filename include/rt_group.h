@@ -99,6 +99,23 @@ int rt_group_set_camera(struct rt_group* g, const FlatCamera* camera);
 int rt_group_set_light(struct rt_group* g, const FlatLight* light);
 int rt_group_set_params(struct rt_group* g, const rt_params* params);
 
+/* The reference's per-frame upload of an animated scene (src/main.cpp:336-346):
+ * rt_update_shapes (updateScene's glBufferSubData per record, :981-992),
+ * rt_update_nodes (updateBVH + serializeBVH + glBufferSubData, :340-345, :1068-1077),
+ * rt_set_animated / rt_animate (the same on the device) on EVERY local member and
+ * EVERY frame slot, in call order: each slot context renders every F-th frame from
+ * its own copy of the scene, so each is given every frame's update (grow-only node
+ * boxes need every position). Deferred or stream-ordered exactly as the
+ * single-context calls (rt_api.h): one device refit per slot at its next operation.
+ * The sky-row band (rt_group_set_sky_rows) follows the root box these calls leave:
+ * rt_group_update_nodes sets it from node N-1, rt_group_animate grows it as the
+ * device's refit grows it. Every rank must make the same calls with the same records
+ * before the same frame. */
+int rt_group_update_shapes(struct rt_group* g, int first, int count, const FlatShape* shapes);
+int rt_group_update_nodes(struct rt_group* g, const FlatNode* nodes, int num_nodes);
+int rt_group_set_animated(struct rt_group* g, const int* ids, int count);
+int rt_group_animate(struct rt_group* g, const FlatShape* shapes);
+
 /* Render the W x H frame split into `stripe`-row stripes over the ranks and
  * gather it into rank 0's surface. Stream-ordered and asynchronous; every rank
  * calls it for every frame, in the same order. */
@@ -112,8 +129,15 @@ int rt_group_dispatch(struct rt_group* g, int width, int height, int stripe);
  * same band of rows that may meet the box from the camera, parameters and tree
  * it was given; the peers send only their rows inside it and rank 0 writes the
  * others' background (1080p car: 283 of 1080 rows). Applies to the BVH branch
- * with at least one bounce. The image does not depend on it. */
+ * with at least one bounce. The image does not depend on it. A member whose camera
+ * or node boxes were changed through its own context (rt_group_member) instead of
+ * the group's calls makes its process refuse the frame (RT_ERR_INVALID); with one
+ * process per GPU the other ranks then time out in rt_group_sync and the group is
+ * aborted. */
 int rt_group_set_sky_rows(struct rt_group* g, int on);
+/* The band [*y0, *y1) of image rows the last rt_group_dispatch sent over the links
+ * ([0, height) when the band did not apply); RT_ERR_INVALID before any dispatch. */
+int rt_group_sky_band(struct rt_group* g, int* y0, int* y1);
 
 /* Rank 0's stripes per period (1 <= share <= 64; default 1). Rank 0's rows
  * never cross a link, so when rank 0's ingress bounds the frame (7 peers' rows

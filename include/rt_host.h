@@ -50,6 +50,14 @@ int rth_upload_animated(struct rt_ctx* ctx, FlatShape* shapes, int num_shapes, c
                         const FlatShape* recs, int count, FlatNode* nodes, int num_nodes, const int* indices,
                         int num_indices);
 
+/* rth_upload_animated over a multi-GPU group (include/rt_group.h): the same calls,
+ * rt_group_update_shapes per record and one rt_group_update_nodes, which give every
+ * local member and frame slot the update. */
+struct rt_group;
+int rth_group_upload_animated(struct rt_group* g, FlatShape* shapes, int num_shapes, const int* ids,
+                              const FlatShape* recs, int count, FlatNode* nodes, int num_nodes, const int* indices,
+                              int num_indices);
+
 /* rth_render_loop with that upload before each dispatch: frame i moves shapes
  * ids[0..count) to anim[(i % anim_frames) * count + j]. shapes / nodes are the
  * host's whole scene arrays, updated in place as the reference's are. */

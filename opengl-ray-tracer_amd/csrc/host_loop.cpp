@@ -11,27 +11,50 @@
 #include <cstddef>
 
 #include "../../include/rt_api.h"
+#include "../../include/rt_group.h"
 #include "../../include/rt_host.h"
 #include "../../include/rt_scene.h"
+
+namespace {
 
 // The reference's own upload of an animated frame, call for call (:336-346):
 // updateScene's glBufferSubData of each animated record (:981-992), updateBVH on
 // the host's node objects (:1068-1077), then serializeBVH and one glBufferSubData
-// of every node record (:340-345).
-extern "C" int rth_upload_animated(rt_ctx* ctx, FlatShape* shapes, int num_shapes, const int* ids,
-                                   const FlatShape* recs, int count, FlatNode* nodes, int num_nodes, const int* indices,
-                                   int num_indices) {
-    if (!ctx || !shapes || num_shapes < 0 || count < 0 || (count > 0 && (!ids || !recs)) || !nodes || num_nodes < 0)
+// of every node record (:340-345). T: a context (rt_update_*) or a group
+// (rt_group_update_*, every member and frame slot).
+template <class T, class Shapes, class Nodes>
+int upload_animated(T* dst, Shapes update_shapes, Nodes update_nodes, FlatShape* shapes, int num_shapes,
+                    const int* ids, const FlatShape* recs, int count, FlatNode* nodes, int num_nodes,
+                    const int* indices, int num_indices) {
+    if (!dst || !shapes || num_shapes < 0 || count < 0 || (count > 0 && (!ids || !recs)) || !nodes || num_nodes < 0)
         return RT_ERR_INVALID;
     for (int j = 0; j < count; ++j) {
         if (ids[j] < 0 || ids[j] >= num_shapes) return RT_ERR_INVALID;
         shapes[ids[j]] = recs[j];                                       // flatScene.shapes[i] = serializeShape(...)
-        const int rc = rt_update_shapes(ctx, ids[j], 1, &shapes[ids[j]]);  // glBufferSubData of that one record
+        const int rc = update_shapes(dst, ids[j], 1, &shapes[ids[j]]);  // glBufferSubData of that one record
         if (rc != RT_OK) return rc;
     }
     if (rts_update_bvh(shapes, num_shapes, nodes, num_nodes, indices, num_indices, ids, count) != 0)  // updateBVH
         return RT_ERR_INVALID;
-    return rt_update_nodes(ctx, nodes, num_nodes);  // serializeBVH + glBufferSubData of the nodes
+    return update_nodes(dst, nodes, num_nodes);  // serializeBVH + glBufferSubData of the nodes
+}
+
+}  // namespace
+
+extern "C" int rth_upload_animated(rt_ctx* ctx, FlatShape* shapes, int num_shapes, const int* ids,
+                                   const FlatShape* recs, int count, FlatNode* nodes, int num_nodes, const int* indices,
+                                   int num_indices) {
+    return upload_animated(ctx, rt_update_shapes, rt_update_nodes, shapes, num_shapes, ids, recs, count, nodes,
+                           num_nodes, indices, num_indices);
+}
+
+// The same over a multi-GPU group (include/rt_group.h): every local member and frame
+// slot is given each call.
+extern "C" int rth_group_upload_animated(rt_group* g, FlatShape* shapes, int num_shapes, const int* ids,
+                                         const FlatShape* recs, int count, FlatNode* nodes, int num_nodes,
+                                         const int* indices, int num_indices) {
+    return upload_animated(g, rt_group_update_shapes, rt_group_update_nodes, shapes, num_shapes, ids, recs, count,
+                           nodes, num_nodes, indices, num_indices);
 }
 
 namespace {

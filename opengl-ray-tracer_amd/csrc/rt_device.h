@@ -56,22 +56,22 @@ __device__ __forceinline__ int prim_type(const PrimRec& g) { return g.st & 3; }
 struct V {
     float x, y, z;
 };
-__device__ __forceinline__ V mk(float x, float y, float z) { return V{x, y, z}; }
-__device__ __forceinline__ V operator+(V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ V operator-(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
-__device__ __forceinline__ V operator-(V a) { return V{-a.x, -a.y, -a.z}; }
-__device__ __forceinline__ V operator*(V a, float s) { return V{a.x * s, a.y * s, a.z * s}; }
-__device__ __forceinline__ V operator*(float s, V a) { return V{s * a.x, s * a.y, s * a.z}; }
+__host__ __device__ __forceinline__ V mk(float x, float y, float z) { return V{x, y, z}; }
+__host__ __device__ __forceinline__ V operator+(V a, V b) { return V{a.x + b.x, a.y + b.y, a.z + b.z}; }
+__host__ __device__ __forceinline__ V operator-(V a, V b) { return V{a.x - b.x, a.y - b.y, a.z - b.z}; }
+__host__ __device__ __forceinline__ V operator-(V a) { return V{-a.x, -a.y, -a.z}; }
+__host__ __device__ __forceinline__ V operator*(V a, float s) { return V{a.x * s, a.y * s, a.z * s}; }
+__host__ __device__ __forceinline__ V operator*(float s, V a) { return V{s * a.x, s * a.y, s * a.z}; }
 __device__ __forceinline__ V mulv(V a, V b) { return V{a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ V divs(V a, float s) { return V{a.x / s, a.y / s, a.z / s}; }
-__device__ __forceinline__ float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-__device__ __forceinline__ V cross(V a, V b) {
+__host__ __device__ __forceinline__ float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__host__ __device__ __forceinline__ V cross(V a, V b) {
     return V{a.y * b.z - b.y * a.z, a.z * b.x - b.z * a.x, a.x * b.y - b.x * a.y};
 }
-__device__ __forceinline__ float len(V a) { return __builtin_sqrtf(dot(a, a)); }
-__device__ __forceinline__ V normalize(V a) { return a * (1.0f / __builtin_sqrtf(dot(a, a))); }
-__device__ __forceinline__ float dist(V a, V b) { return len(b - a); }
-__device__ __forceinline__ V reflect(V i, V n) { return i - (n * dot(n, i)) * 2.0f; }
+__host__ __device__ __forceinline__ float len(V a) { return __builtin_sqrtf(dot(a, a)); }
+__host__ __device__ __forceinline__ V normalize(V a) { return a * (1.0f / __builtin_sqrtf(dot(a, a))); }
+__host__ __device__ __forceinline__ float dist(V a, V b) { return len(b - a); }
+__host__ __device__ __forceinline__ V reflect(V i, V n) { return i - (n * dot(n, i)) * 2.0f; }
 __device__ __forceinline__ V mix(V x, V y, float a) { return x + a * (y - x); }
 __device__ __forceinline__ float gmax(float a, float b) { return (a < b) ? b : a; }  // GLSL/glm max
 __device__ __forceinline__ float gmin(float a, float b) { return (b < a) ? b : a; }  // GLSL/glm min

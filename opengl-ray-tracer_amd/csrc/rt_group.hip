@@ -150,6 +150,7 @@ struct rt_group {
     float root_lo[3] = {0, 0, 0}, root_hi[3] = {0, 0, 0};
     bool have_cam = false, have_params = false, have_root = false;
     bool sky_rows = true;       // rt_group_set_sky_rows
+    int band_y0 = 0, band_y1 = 0;  // the last dispatch's band (rt_group_sky_band)
     double timeout_ms = 60000;  // rt_group_set_timeout
     bool phase_timing = true;   // rt_group_set_phase_timing
     // phase times of member `tm` (rank 0 when local, else the first member)
@@ -335,6 +336,13 @@ void harvest(rt_group* g, PhaseRec& p) {
         g->sum[3] += ms;
         ++g->nsum[3];
     }
+}
+
+// Whether a frame's sky-row band is computed (rt_group_dispatch): rows that miss the
+// root box are background only on the BVH branch with at least one bounce.
+bool sky_applies(const rt_group* g) {
+    return g->sky_rows && g->nranks > 1 && g->have_cam && g->have_params && g->have_root && g->params.useBVH &&
+           g->params.maxBounces >= 1 && g->params.resY > 0;
 }
 
 // Every slot context of every local member.
@@ -536,6 +544,34 @@ int rt_group_set_params(rt_group* g, const rt_params* p) {
     return rc;
 }
 
+// The reference's per-frame upload of an animated scene (src/main.cpp:336-346) on
+// every local member x frame slot: each slot context holds its own copy of the scene
+// and renders every F-th frame, so each one is given every update, in order (a slot
+// that skipped a frame's rt_animate would miss that frame's updateBVH growth). The
+// calls are the single-context ones, deferred or stream-ordered alike.
+int rt_group_update_shapes(rt_group* g, int first, int count, const FlatShape* shapes) {
+    return each_ctx(g, [&](rt_ctx* c) { return rt_update_shapes(c, first, count, shapes); });
+}
+
+int rt_group_update_nodes(rt_group* g, const FlatNode* nodes, int num_nodes) {
+    const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_update_nodes(c, nodes, num_nodes); });
+    if (rc == RT_OK) g->have_root = rtx::view_root(g->m[0].slot[0].ctx, g->root_lo, g->root_hi);
+    return rc;
+}
+
+int rt_group_set_animated(rt_group* g, const int* ids, int count) {
+    return each_ctx(g, [&](rt_ctx* c) { return rt_set_animated(c, ids, count); });
+}
+
+int rt_group_animate(rt_group* g, const FlatShape* shapes) {
+    const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_animate(c, shapes); });
+    if (g) mark_all_dirty(g);  // k_refit is queued on every slot's stream (the bounded waits poll them)
+    // the grown root (the sky-row band follows it): the same host computation in every
+    // slot context and on every rank
+    if (rc == RT_OK) g->have_root = rtx::view_root(g->m[0].slot[0].ctx, g->root_lo, g->root_hi);
+    return rc;
+}
+
 int rt_group_set_sky_rows(rt_group* g, int on) {
     if (!g) return RT_ERR_INVALID;
     g->sky_rows = on != 0;
@@ -552,13 +588,18 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     // computes the same band [yb0, yb1) from the same camera, box and parameters; a
     // peer sends its compact rows inside it, rank 0 writes the rest as background.
     // Only where the reference draws the background for a ray missing the root:
-    // the BVH branch with at least one bounce and a root box. The band is the
-    // group's: a member whose camera or node boxes were changed through its own
-    // context (rt_group_member: rt_set_camera, rt_animate, rt_update_nodes) would
-    // draw geometry in rows the band calls sky, so such a frame is refused before
-    // anything is posted (RT_ERR_INVALID; rt_group_set_sky_rows(g, 0) lifts it).
-    const bool sky = g->sky_rows && g->nranks > 1 && g->have_cam && g->have_params && g->have_root &&
-                     g->params.useBVH && g->params.maxBounces >= 1 && g->params.resY > 0;
+    // the BVH branch with at least one bounce and a root box. The band follows the
+    // group's camera and the root box its update calls leave (rt_group_update_nodes
+    // sets it, rt_group_animate grows it as the device does), so it is recomputed
+    // every frame. A member whose camera or node boxes were changed through its own
+    // context instead (rt_group_member: rt_set_camera, rt_animate, rt_update_nodes)
+    // would draw geometry in rows the band calls sky, so such a frame is refused
+    // before this process posts anything (RT_ERR_INVALID; rt_group_set_sky_rows(g, 0)
+    // lifts it). In a group of one process per GPU only the rank holding that member
+    // refuses: the others post the frame and their fan-in runs into the timeout, which
+    // aborts the communicator. That is the documented misuse (rt_group.h); the group
+    // calls keep every rank's members equal.
+    const bool sky = sky_applies(g);
     if (sky)
         for (Member& b : g->m)
             if (!rtx::matches_view(b.slot[jj].ctx, g->cam, g->root_lo, g->root_hi)) return RT_ERR_INVALID;
@@ -614,6 +655,8 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     }
     int yb0 = 0, yb1 = height;  // the sky-row band (above)
     if (sky) rtg::sky_band(g->cam, g->root_lo, g->root_hi, height, g->params.resY, &yb0, &yb1);
+    g->band_y0 = yb0;
+    g->band_y1 = yb1;
     // the peers' compact row range inside the band (one contiguous run each)
     auto band_of = [&](int rank, int& c0, int& c1) {
         const Rows w = rank_rows(height, P, stripe, k, rank);
@@ -798,6 +841,13 @@ int rt_group_dispatch(rt_group* g, int width, int height, int stripe) {
     g->ring_pos = (g->ring_pos + 1) % kPhaseRing;
     g->last_slot = j;
     ++g->next;
+    return RT_OK;
+}
+
+int rt_group_sky_band(rt_group* g, int* y0, int* y1) {
+    if (!g || !y0 || !y1 || g->next == 0) return RT_ERR_INVALID;
+    *y0 = g->band_y0;
+    *y1 = g->band_y1;
     return RT_OK;
 }
 

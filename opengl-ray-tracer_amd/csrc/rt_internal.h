@@ -29,10 +29,16 @@ int create_ctx(rt_ctx** out, int device, hipStream_t stream);
 hipError_t make_stream(hipStream_t* s, bool own_queue);
 
 // Whether the context renders with camera `cam` and a root box equal to [lo, hi]:
-// its camera as last set, its node records current on the host (no rt_animate growth
-// on the device, whatever rt_update_nodes left pending included). rt_group computes
-// the sky-row band from the group's own camera and root box on every rank; a member
-// changed behind the group's back would get background rows where it draws geometry.
+// its camera as last set, and the root box its next render sees (the host's node
+// records, whatever rt_update_nodes left pending included, grown by every rt_animate
+// as k_refit grows it). rt_group computes the sky-row band from the group's own camera
+// and root box on every rank; a member changed behind the group's back would get
+// background rows where it draws geometry.
 bool matches_view(const rt_ctx* c, const FlatCamera& cam, const float lo[3], const float hi[3]);
+
+// The root box of matches_view (false without a scene or nodes). After rt_group's
+// update calls every slot context holds the same one, computed on the host by the
+// same operations on every rank.
+bool view_root(const rt_ctx* c, float lo[3], float hi[3]);
 
 }  // namespace rtx

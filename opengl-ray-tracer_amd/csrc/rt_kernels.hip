@@ -2021,7 +2021,7 @@ __global__ __launch_bounds__(kOrderThreads) void k_cost_dilate(const unsigned* _
 // Device animation (rt_animate): updateScene + updateBVH on the device.
 
 // Wall::end (src/shapes/wall.hpp:16-31), host glm operation order.
-__device__ V wall_end(const FlatShape& s) {
+__host__ __device__ V wall_end(const FlatShape& s) {
     const V n = mk(s.planeNormal.x, s.planeNormal.y, s.planeNormal.z);
     const V t1 = fabsf(n.x) > fabsf(n.y) ? normalize(mk(-n.z, 0.f, n.x)) : normalize(mk(0.f, -n.z, n.y));
     const V t2 = normalize(cross(n, t1));
@@ -2031,7 +2031,7 @@ __device__ V wall_end(const FlatShape& s) {
 // BoundingBox::growToInclude(shape) (BoundingBox.hpp:50-95) from an empty box:
 // the points it adds, as a (lo, hi) pair; a shape that adds nothing leaves
 // lo = +inf, hi = -inf.
-__device__ void reference_box(const FlatShape& s, float lo[3], float hi[3]) {
+__host__ __device__ void reference_box(const FlatShape& s, float lo[3], float hi[3]) {
     for (int a = 0; a < 3; ++a) {
         lo[a] = INFINITY;
         hi[a] = -INFINITY;
@@ -2883,6 +2883,12 @@ struct rt_ctx {
     int n_dirty = 0;
     int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
+    // The root node's box as the next render sees it, kept on the host without a
+    // readback: set from the records by rt_upload_scene / rt_update_nodes, grown by
+    // rt_animate as k_refit grows it (reference_box of every animated shape the root
+    // lists). rt_group computes its sky-row band from it (rtx::view_root).
+    float root_lo[3] = {0.f, 0.f, 0.f}, root_hi[3] = {0.f, 0.f, 0.f};
+    std::vector<char> entry_root;       // per refit entry: node N-1 lists it (k_refit grows the root by it)
     // The brute-force branch (useBVH = 0, gpu_shader.comp:523-620) tests every shape in
     // index order, keeps the strict-< first minimum and stops shadows at the first
     // occluder: exactly the BVH branch walking a tree of ONE leaf that lists shapes
@@ -3245,6 +3251,7 @@ int prepare_animation(rt_ctx* c) {
     c->n_direct_slot_reads = 0;
     c->refit_of.assign(c->S, -1);
     for (int i = 0; i < n; ++i) c->refit_of[c->refit_ids[i]] = i;
+    c->entry_root.clear();
     if (n == 0) return RT_OK;
     const int N = c->N;
     const std::vector<int>& which = c->refit_of;  // shape -> refit entry
@@ -3296,6 +3303,8 @@ int prepare_animation(rt_ctx* c) {
         }
         std::sort(L.begin(), L.end());
     }
+    c->entry_root.assign(n, 0);
+    for (int i = 0; i < n; ++i) c->entry_root[i] = std::binary_search(nodes_of[i].begin(), nodes_of[i].end(), N - 1);
     if (c->accel_ok) {
         const size_t P = A.prim_shape.size(), M = A.lbox.size();
         std::vector<int> lleaf(P, -1), lparent(M, -1), wpos(M, -1);
@@ -3533,6 +3542,15 @@ int prepare_animation(rt_ctx* c) {
     // the degraded-bound reports of earlier refits concern the accelerator this replaced
     for (bool& pend : c->report_pending) pend = false;
     return ensure_staging(c->anim_sbox, c->anim_sbox_cap, 4 * static_cast<size_t>(n));
+}
+
+// The root's box from the host's node records (rt_upload_scene, rt_update_nodes).
+void set_root(rt_ctx* c) {
+    if (c->N <= 0 || static_cast<int>(c->host_nodes.size()) != c->N) return;
+    const FlatNode& r = c->host_nodes[c->N - 1];
+    const float lo[3] = {r.boundsMin.x, r.boundsMin.y, r.boundsMin.z}, hi[3] = {r.boundsMax.x, r.boundsMax.y, r.boundsMax.z};
+    std::memcpy(c->root_lo, lo, sizeof lo);
+    std::memcpy(c->root_hi, hi, sizeof hi);
 }
 
 // (Re)builds the accelerator after the host copies changed, then the animation lists.
@@ -4461,10 +4479,14 @@ int rtx::create_ctx(rt_ctx** out, int device, hipStream_t stream) {
 bool rtx::matches_view(const rt_ctx* c, const FlatCamera& cam, const float lo[3], const float hi[3]) {
     if (!c || !c->have_cam || std::memcmp(&c->cam, &cam, sizeof cam) != 0) return false;
     if (c->N <= 0) return true;
-    if (c->nodes_on_device_newer || static_cast<int>(c->host_nodes.size()) != c->N) return false;
-    const FlatNode& r = c->host_nodes[c->N - 1];
-    const float rl[3] = {r.boundsMin.x, r.boundsMin.y, r.boundsMin.z}, rh[3] = {r.boundsMax.x, r.boundsMax.y, r.boundsMax.z};
-    return std::memcmp(rl, lo, sizeof rl) == 0 && std::memcmp(rh, hi, sizeof rh) == 0;
+    return std::memcmp(c->root_lo, lo, sizeof c->root_lo) == 0 && std::memcmp(c->root_hi, hi, sizeof c->root_hi) == 0;
+}
+
+bool rtx::view_root(const rt_ctx* c, float lo[3], float hi[3]) {
+    if (!c || !c->have_scene || c->N <= 0) return false;
+    std::memcpy(lo, c->root_lo, sizeof c->root_lo);
+    std::memcpy(hi, c->root_hi, sizeof c->root_hi);
+    return true;
 }
 
 extern "C" {
@@ -4572,6 +4594,7 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->host_shapes.assign(shapes, shapes + S);
     c->have_scene = true;
     c->nodes_on_device_newer = false;
+    set_root(c);
     c->anim_ids.clear();  // ids refer to the previous scene
     c->refit_ids.clear();
     c->anim_base.clear();
@@ -4621,6 +4644,7 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
     // every device copy of the boxes at the next device operation (flush_updates).
     c->host_nodes.assign(nodes, nodes + N);
     c->nodes_on_device_newer = false;  // these boxes replace any the device grew
+    set_root(c);
     c->nodes_dirty = true;
     c->boxes_finite = 1;
     for (int k = 0; k < N; ++k)
@@ -4670,6 +4694,18 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (c->nodes_dirty && (rc = flush_updates(c)) != RT_OK) return rc;
     const int n = static_cast<int>(c->anim_ids.size());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
+    // the root's box as k_refit grows it (grow_node: glm::min / max of the listed
+    // shapes' growToInclude boxes), for rtx::view_root
+    for (int i = 0; i < n; ++i) {
+        const int e = c->refit_of[c->anim_ids[i]];
+        if (e < 0 || e >= static_cast<int>(c->entry_root.size()) || !c->entry_root[e]) continue;
+        float lo[3], hi[3];
+        reference_box(shapes[i], lo, hi);
+        for (int a = 0; a < 3; ++a) {
+            c->root_lo[a] = lo[a] < c->root_lo[a] ? lo[a] : c->root_lo[a];
+            c->root_hi[a] = c->root_hi[a] < hi[a] ? hi[a] : c->root_hi[a];
+        }
+    }
     if (c->brute && !c->brute_stale)  // the brute-force context: the same records, no nodes to grow
         for (int i = 0; i < n && !c->brute_stale; ++i)
             if (rt_update_shapes(c->brute, c->anim_ids[i], 1, &shapes[i]) != RT_OK) c->brute_stale = true;

@@ -182,6 +182,7 @@ HOST_SYMBOLS = {
     "rth_render_loop": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P]),
     "rth_render_loop_anim": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _I, _P]),
     "rth_upload_animated": (_I, [_P, _P, _I, _P, _P, _I, _P, _I, _P, _I]),
+    "rth_group_upload_animated": (_I, [_P, _P, _I, _P, _P, _I, _P, _I, _P, _I]),
     "rth_render_rows_loop": (_I, [_P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I, _I, _P]),
     "rth_render_loop_ref": (_I, [_P, _P, _I, _P, _I, _I, _P, C.c_size_t, _I, _I, _P, _I, _P, _I, _P, _I, _P, _I,
                                  _P, _I, _P]),
@@ -234,11 +235,15 @@ GROUP_SYMBOLS = {
     "rt_group_set_timeout": (_I, [_P, C.c_double]),
     "rt_group_set_phase_timing": (_I, [_P, _I]),
     "rt_group_set_sky_rows": (_I, [_P, _I]),
+    "rt_group_sky_band": (_I, [_P, _P, _P]),
     "rt_group_check": (_I, [_P]),
     "rt_group_phase_times": (_I, [_P, _P]),
     "rt_group_upload_scene": (_I, [_P, _P, _I, _P, _I, _P, _I]),
     "rt_group_set_camera": (_I, [_P, _P]), "rt_group_set_light": (_I, [_P, _P]),
     "rt_group_set_params": (_I, [_P, _P]),
+    "rt_group_update_shapes": (_I, [_P, _I, _I, _P]),
+    "rt_group_update_nodes": (_I, [_P, _P, _I]),
+    "rt_group_set_animated": (_I, [_P, _P, _I]), "rt_group_animate": (_I, [_P, _P]),
     "rt_group_dispatch": (_I, [_P, _I, _I, _I]),
     "rt_group_set_root_share": (_I, [_P, _I]),
     "rt_group_collect_stats": (_I, [_P, _I, _I, _I, _P]),
@@ -314,12 +319,14 @@ class ReferenceUpload:
         self.ids = np.ascontiguousarray(ids, np.int32)
 
     def upload(self, ctx, recs):
+        """ctx: a ComputeShader (rth_upload_animated) or a Group (rth_group_upload_animated:
+        every member and frame slot is given the calls)."""
         recs = as_records(np.asarray(recs).reshape(-1), SHAPE_DTYPE)
-        rc = host_lib().rth_upload_animated(ctx._h, _ptr(self.shapes), len(self.shapes), _ptr(self.ids), _ptr(recs),
-                                            len(self.ids), _ptr(self.nodes), len(self.nodes), _ptr(self.indices),
-                                            len(self.indices))
+        fn = host_lib().rth_group_upload_animated if isinstance(ctx, Group) else host_lib().rth_upload_animated
+        rc = fn(ctx._h, _ptr(self.shapes), len(self.shapes), _ptr(self.ids), _ptr(recs), len(self.ids),
+                _ptr(self.nodes), len(self.nodes), _ptr(self.indices), len(self.indices))
         if rc != 0:
-            raise RTError("rth_upload_animated", rc)
+            raise RTError("rth_group_upload_animated" if isinstance(ctx, Group) else "rth_upload_animated", rc)
 
     def scene(self, fs):
         """The scene this host has uploaded (for the oracle)."""
@@ -966,6 +973,30 @@ class Group:
     def dispatch(self, width, height, stripe=8):
         self._chk(self._lib.rt_group_dispatch(self._h, width, height, stripe), "rt_group_dispatch")
 
+    # the reference's animated-frame upload on every member and frame slot (rt_group.h)
+    def update_shapes(self, first, shapes):
+        shapes = as_records(shapes, SHAPE_DTYPE)
+        self._chk(self._lib.rt_group_update_shapes(self._h, first, len(shapes), _ptr(shapes)),
+                  "rt_group_update_shapes")
+
+    def update_nodes(self, nodes):
+        nodes = as_records(nodes, NODE_DTYPE)
+        self._chk(self._lib.rt_group_update_nodes(self._h, _ptr(nodes), len(nodes)), "rt_group_update_nodes")
+
+    def set_animated(self, ids):
+        """animatedIndices (src/main.cpp:120,706-708) on every member and frame slot."""
+        ids = np.ascontiguousarray(ids, np.int32)
+        self._n_animated = len(ids)
+        self._chk(self._lib.rt_group_set_animated(self._h, _ptr(ids), len(ids)), "rt_group_set_animated")
+
+    def animate(self, shapes):
+        """The animated shapes' new records, in set_animated order: updateScene +
+        updateBVH + upload (src/main.cpp:336-346) on the device of every member and slot."""
+        shapes = as_records(shapes, SHAPE_DTYPE)
+        if len(shapes) != getattr(self, "_n_animated", -1):
+            raise ValueError("animate: one record per animated shape")
+        self._chk(self._lib.rt_group_animate(self._h, _ptr(shapes)), "rt_group_animate")
+
     def set_root_share(self, share):
         """Rank 0's stripes per period of share + P - 1 (rt_group_set_root_share)."""
         self._chk(self._lib.rt_group_set_root_share(self._h, int(share)), "rt_group_set_root_share")
@@ -991,6 +1022,19 @@ class Group:
     def set_sky_rows(self, on):
         """rt_group_set_sky_rows: keep background-only rows off the links (default on)."""
         self._chk(self._lib.rt_group_set_sky_rows(self._h, int(bool(on))), "rt_group_set_sky_rows")
+
+    def sky_band(self):
+        """The image rows [y0, y1) the last dispatch sent over the links (rt_group_sky_band)."""
+        y0, y1 = C.c_int(), C.c_int()
+        self._chk(self._lib.rt_group_sky_band(self._h, C.byref(y0), C.byref(y1)), "rt_group_sky_band")
+        return y0.value, y1.value
+
+    def device_image(self):
+        """(pointer, pitch) of rank 0's surface of the last dispatched frame (rt_group_device_image):
+        the frame after sync(), until `frames` more dispatches reuse the slot."""
+        p, pitch = C.c_void_p(), C.c_size_t()
+        self._chk(self._lib.rt_group_device_image(self._h, C.byref(p), C.byref(pitch)), "rt_group_device_image")
+        return p.value, pitch.value
 
     def set_phase_timing(self, on):
         """rt_group_set_phase_timing: record the render / fan-in / unstripe events (default on)."""

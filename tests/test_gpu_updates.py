@@ -326,3 +326,88 @@ def test_refit_launch_modes_equal_fresh_upload(ctx, fresh, refit):
     finally:
         ctx.debug_refit(-1)
         ctx.set_animated(np.zeros(0, np.int32))
+
+
+# --------------------------------------------------------------------------
+# The animated frame on the multi-GPU group (rt_group_update_shapes / _nodes,
+# rt_group_set_animated / rt_group_animate; include/rt_group.h)
+
+def _copy_surface(ptr, pitch, W, H):
+    """rank 0's pitched RGBA32F surface (rt_group_device_image) to the host."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    out = np.empty((H, W, 4), np.float32)
+    rc = hip.hipMemcpy2D(ctypes.c_void_p(out.ctypes.data), ctypes.c_size_t(W * 16), ctypes.c_void_p(ptr),
+                         ctypes.c_size_t(pitch), ctypes.c_size_t(W * 16), ctypes.c_size_t(H), 2)  # DeviceToHost
+    assert rc == 0, f"hipMemcpy2D {rc}"
+    return out
+
+
+@pytest.mark.parametrize("upload", ["device", "reference"])
+@pytest.mark.parametrize("cfg", [3, 2])
+@pytest.mark.parametrize("kind", ["copy8_3840x2160", "rccl1_1920x1080"])
+def test_group_animated_frames(ctx, kind, cfg, upload):
+    """16 animated frames through the group, 3 frames in flight: the car's wheels turn
+    (config 3) or scene 1's spheres bounce (config 2), uploaded by rt_group_animate (the
+    device's updateBVH) or by the reference's own calls on the group (one
+    rt_group_update_shapes per animated record, updateBVH on the host, one
+    rt_group_update_nodes: rth_group_upload_animated). Cases: 8 copy-transport members
+    on one GPU at 3840x2160 (sky rows on: the band follows the grown root box every
+    frame) and a 1-rank RCCL group (ncclCommInitRank) at 1920x1080. Every gathered
+    frame equals a single context given the same calls, bit for bit; the last frame
+    equals the oracle of the animated scene (4K: a band of rows through the scene);
+    no slot context rebuilds its accelerator (src/main.cpp:336-346, 981-992, 1068-1077)."""
+    W, H = (3840, 2160) if kind.startswith("copy8") else (1920, 1080)
+    mb = 3 if cfg == 3 else 1
+    F, n_frames = 3, 16
+    fs = rtamd.generate(cfg, 0, W, H)
+    ids, frames = bench.wheel_frames(fs, n_frames) if cfg == 3 else bench.sphere_frames(fs, 4 * n_frames)
+    if cfg == 2:
+        frames = frames[::4]  # 1/15 s apart: the spheres move visibly from frame to frame
+    g = (rtamd.Group([0] * 8, rtamd.GATHER_COPY, frames=F) if kind.startswith("copy8") else
+         rtamd.Group(uid=rtamd.group_unique_id(), nranks=1, rank=0, device=0, frames=F))
+    try:
+        g.set_timeout(60000)
+        g.upload(fs)
+        g.set_params(W, H, mb, True)
+        ctx.upload(fs)
+        ctx.set_params(W, H, mb, True)
+        ctx.set_kernel(rtamd.KERNEL_AUTO)
+        if upload == "device":
+            g.set_animated(ids)
+            ctx.set_animated(ids)
+        else:
+            ru_g, ru_c = rtamd.ReferenceUpload(fs, ids), rtamd.ReferenceUpload(fs, ids)
+        rebuilds0 = [c.debug_anim_rebuilds() for c in g.contexts]
+        k = 0
+        bands = []
+        while k < n_frames:
+            burst = []
+            for _ in range(min(F, n_frames - k)):  # F frames in flight, nothing waited between them
+                if upload == "device":
+                    g.animate(frames[k])
+                else:
+                    ru_g.upload(g, frames[k])
+                g.dispatch(W, H, 8)
+                burst.append((k, g.device_image()))
+                bands.append(g.sky_band())
+                k += 1
+            g.sync()
+            for j, (ptr, pitch) in burst:
+                if upload == "device":
+                    ctx.animate(frames[j])
+                else:
+                    ru_c.upload(ctx, frames[j])
+                same(_copy_surface(ptr, pitch, W, H), ctx.render(W, H), f"{kind} config {cfg} {upload} frame {j}")
+        assert [c.debug_anim_rebuilds() for c in g.contexts] == rebuilds0, "an accelerator was rebuilt"
+        if g.nranks > 1 and cfg == 3:
+            assert all(0 < y0 < y1 <= H for y0, y1 in bands), f"sky rows off: {bands}"  # the car's sky is on top
+        last = _copy_surface(*g.device_image(), W, H)
+        fk = (bench.animated_oracle_scene(fs, ids, frames, list(range(n_frames))) if upload == "device" else
+              ru_g.scene(fs))
+        p = oracle.params(W, H, mb)
+        y0, rows = (H // 2 - 32, 64) if H > 1080 else (0, H)
+        want, _ = oracle.render(fk, W, H, p, y0=y0, out_rows=rows, threads=16)
+        check(last[y0:y0 + rows], want, f"{kind} config {cfg} {upload}: last frame against the oracle")
+    finally:
+        g.close()
