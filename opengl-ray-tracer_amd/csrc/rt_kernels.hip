@@ -1691,7 +1691,9 @@ __device__ void accel_tile(const AccelPtrs& A, const float4* __restrict__ mat, c
                     q[0] = make_float4(ray.o.x, ray.o.y, ray.o.z, acc.x);
                     q[1] = make_float4(ray.d.x, ray.d.y, ray.d.z, acc.y);
                     q[2] = make_float4(att.x, att.y, att.z, acc.z);
-                    kp.tail_px[pos] = pc.r * kp.width + pc.x;
+                    // unsigned, as k_accel_tail decodes it (launch() keeps width * rows < 2^32)
+                    kp.tail_px[pos] = static_cast<int>(static_cast<unsigned>(pc.r) * static_cast<unsigned>(kp.width) +
+                                                       static_cast<unsigned>(pc.x));
                 }
             }
             deferred = alive;
@@ -2668,9 +2670,19 @@ __global__ __launch_bounds__(64 * kRefitWaves) void k_refit(AnimMaps m, AnimOut 
         // workgroups polling the counter itself held its increments back (car: 42 us)
         const unsigned* flag = r.ctr + kRefitFlag0 + 16 * (blockIdx.x % kRefitFlags);
         if (tid == 0) {
+            // Bounded (diagnostic modes only): these waits rely on the record
+            // workgroups having started, which HIP does not promise. Past ~1 s of the
+            // constant-rate clock (100 MHz) the wait gives up and reports, so a scheduling
+            // change shows up as a rebuild (check_reports), not as a GPU hang.
+            const unsigned long long t0 = wall_clock64();
             while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - r.abase <
-                   static_cast<unsigned>(r.na))
+                   static_cast<unsigned>(r.na)) {
                 __builtin_amdgcn_s_sleep(2);
+                if (wall_clock64() - t0 > 100000000ull) {
+                    __hip_atomic_store(r.report, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    break;
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one invalidation per workgroup
         }
         __syncthreads();
@@ -2846,6 +2858,8 @@ struct rt_ctx {
     char* refit_dev = nullptr;  // refit mode 4: the pinned slot's records copied to the device
     size_t refit_dev_cap = 0;
     long long dirty_sum = 0;  // rt_debug_refit_stats: the slot refit's prim ranges (largest, total)
+    long long last_flush_bytes = 0;  // rt_debug_refit_stats: the pinned records of the last flush
+    int refit_compactions = 0;       // rt_debug_refit_stats: stale entries dropped (compact_refit_set)
     int dirty_max = 0;
     int* anim_maps = nullptr;           // AnimMaps lists, one allocation
     size_t anim_maps_cap = 0;
@@ -3539,8 +3553,6 @@ int prepare_animation(rt_ctx* c) {
                        d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], d + o_cls, d + o_pe,
                        n,
                        static_cast<int>(node_ids.size())};
-    // the degraded-bound reports of earlier refits concern the accelerator this replaced
-    for (bool& pend : c->report_pending) pend = false;
     return ensure_staging(c->anim_sbox, c->anim_sbox_cap, 4 * static_cast<size_t>(n));
 }
 
@@ -3558,6 +3570,9 @@ int upload_accel(rt_ctx* c) {
     int rc = sync_host_nodes(c);
     if (rc != RT_OK) return rc;
     rc = build_upload_accel(c);
+    // the degraded-bound reports of earlier refits concern the accelerator this replaced
+    // (prepare_animation alone, when the refit set changes, keeps them: same accelerator)
+    for (bool& pend : c->report_pending) pend = false;
     // the refit set stays (its shapes tend to move again), with the records just built from
     c->anim_base.resize(c->refit_ids.size());
     for (size_t i = 0; i < c->refit_ids.size(); ++i) c->anim_base[i] = c->host_shapes[c->refit_ids[i]];
@@ -3678,6 +3693,42 @@ int pinned_slot(rt_ctx* c, size_t bytes, char** host, const char** dev) {
     return slot;
 }
 
+// The refit set only grows while shapes join it (rt_update_shapes of a shape not in
+// it), and every flush copies and refits all of it. A host that writes a different
+// few shapes each frame would make that every shape it ever touched. So once the
+// entries that are neither animated nor written since the last flush ("stale")
+// outnumber kRefitSlack, S / 16 and the live ones, they leave the set: their device
+// records are current (the last flush that listed them wrote them), and
+// prepare_animation folds their current boxes into the slots' fixed parts, which it
+// recomputes from the host records. An entry whose bound changed kind since the build
+// stays (the fixed part has no box for it; its report rebuilds the accelerator).
+// Per-flush entries stay below about 2 x live + max(kRefitSlack, S / 16).
+constexpr size_t kRefitSlack = 4096;
+void compact_refit_set(rt_ctx* c) {
+    const size_t n = c->refit_ids.size(), live = c->anim_ids.size() + c->upd_ids.size();
+    if (n <= live || n - live <= std::max({kRefitSlack, static_cast<size_t>(c->S) / 16, live})) return;
+    std::vector<char> keep_shape(c->S, 0);
+    for (int id : c->anim_ids) keep_shape[id] = 1;
+    for (int id : c->upd_ids) keep_shape[id] = 1;
+    std::vector<int> ids;
+    std::vector<FlatShape> base;
+    for (size_t i = 0; i < n; ++i) {
+        const int id = c->refit_ids[i];
+        bool keep = keep_shape[id] != 0;
+        if (!keep && i < c->anim_cls.size()) {
+            rta::Box3 b;
+            keep = rta::classify(c->host_shapes[id], b, c->accel.origin_lim, c->accel.mt) != c->anim_cls[i];
+        }
+        if (keep) {
+            ids.push_back(id);
+            base.push_back(c->anim_base[i]);
+        }
+    }
+    c->refit_ids.swap(ids);
+    c->anim_base.swap(base);
+    ++c->refit_compactions;
+}
+
 // Applies what rt_update_shapes / rt_update_nodes left on the host, and an
 // rt_animate frame (grow: the animated entries grow the nodes listing them, as
 // updateBVH does), to every device copy with one launch of k_refit on the stream:
@@ -3705,11 +3756,13 @@ int flush_updates(rt_ctx* c, bool grow = false) {
                 c->anim_base.push_back(ub.second);
                 added = true;
             }
+        if (added) compact_refit_set(c);
         if (added && (rc = prepare_animation(c)) != RT_OK) return rc;
         const int n = static_cast<int>(c->refit_ids.size());
         const bool nodes = c->nodes_dirty && c->N > 0;
         const size_t rec_bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
         const size_t bytes = rec_bytes + (nodes ? static_cast<size_t>(c->N) * sizeof(FlatNode) : 0);
+        c->last_flush_bytes = static_cast<long long>(bytes);
         if (bytes > 0) {
             char* pin = nullptr;
             const char* pin_dev = nullptr;
@@ -4269,7 +4322,10 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         const int tail_from = c->tail_from != RT_TAIL_AUTO
                                   ? c->tail_from
                                   : (c->accel.st.item_ref.size() >= kTailAutoItems ? 2 : 0);
-        const bool tail = tail_from > 0 && tail_from < k2.maxBounces && !c->persistent;
+        // the queue's pixel word is row * width + x in 32 bits (rt_device.h): larger
+        // frames render without compaction
+        const bool tail = tail_from > 0 && tail_from < k2.maxBounces && !c->persistent &&
+                          static_cast<unsigned long long>(k2.width) * k2.out_rows < (1ull << 32);
         const int rx = (k2.tiles_x + 7) / 8, regions = rx * ((k2.tiles / k2.tiles_x + 7) / 8);
         if (tail) {
             const size_t need = static_cast<size_t>(regions) * kTailRegion;
@@ -4652,7 +4708,9 @@ int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
                         nodes[k].boundsMax.y, nodes[k].boundsMax.z})
             if (std::isnan(v)) c->boxes_finite = 0;
     // the scene tree holds only while the boxes nest (accel.h SceneTree)
-    if (c->accel_ok && c->accel.st.wroot >= 0 && !host_nodes_nest(c)) c->nodes_rebuild = true;
+    // (recomputed per call: a later write that restores nesting before the flush
+    // cancels the rebuild an earlier one asked for)
+    c->nodes_rebuild = c->accel_ok && c->accel.st.wroot >= 0 && !host_nodes_nest(c);
     if (c->mtc && !c->mtc_stale && rt_update_nodes(c->mtc, nodes, N) != RT_OK) c->mtc_stale = true;
     return RT_OK;
 }
@@ -4960,6 +5018,11 @@ int rt_last_kernel_ms(rt_ctx* c, float* ms) {
 
 extern "C" int rt_accel_info_get(rt_ctx* c, rt_accel_info* out) {
     if (!c || !out) return RT_ERR_INVALID;
+    // the accelerator the next dispatch uses: pending updates applied first (a flush may rebuild it)
+    if (c->have_scene) {
+        if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+        if (const int rc = flush_updates(c)) return rc;
+    }
     out->built = c->accel_ok ? 1 : 0;
     out->local_nodes = static_cast<int>(c->accel.lbox.size());
     out->local_leaves = c->accel.local_leaves;
@@ -4987,8 +5050,8 @@ extern "C" int rt_debug_refits(rt_ctx* c) { return c ? c->updates_flushed : -1; 
 // Diagnostics: how flush_updates launches the refit (RefitArgs: 0 one launch whose box
 // roles wait for the record role, 1 two launches, 2 one launch deriving every box from
 // the records). Same device state either way.
-// out: dirty slots, their largest and total prim range, reference nodes listing an
-// entry, refit entries
+// out[7]: dirty slots, their largest and total prim range, reference nodes listing an
+// entry, refit entries, bytes of the last flush's pinned records, compactions
 extern "C" int rt_debug_refit_stats(rt_ctx* c, long long* out) {
     if (!c || !out) return RT_ERR_INVALID;
     out[0] = c->n_dirty;
@@ -4996,6 +5059,8 @@ extern "C" int rt_debug_refit_stats(rt_ctx* c, long long* out) {
     out[2] = c->dirty_sum;
     out[3] = c->anim.nodes;
     out[4] = static_cast<long long>(c->refit_ids.size());
+    out[5] = c->last_flush_bytes;
+    out[6] = c->refit_compactions;
     return RT_OK;
 }
 

@@ -805,9 +805,10 @@ class ComputeShader:
         """The refit's shape: dirty slots, largest / total prim range, nodes, entries."""
         fn = self._lib.rt_debug_refit_stats
         fn.argtypes = [_P, C.c_void_p]
-        out = np.zeros(5, np.int64)
+        out = np.zeros(7, np.int64)
         self._chk(fn(self._h, out.ctypes.data), "rt_debug_refit_stats")
-        return dict(zip(["dirty_slots", "max_range", "sum_range", "nodes", "entries"], out.tolist()))
+        return dict(zip(["dirty_slots", "max_range", "sum_range", "nodes", "entries", "flush_bytes", "compactions"],
+                        out.tolist()))
 
     def debug_moving(self, period, dilate, split):
         """Cost order of dispatches whose camera moved: re-derived every `period` frames

@@ -411,3 +411,39 @@ def test_group_animated_frames(ctx, kind, cfg, upload):
         check(last[y0:y0 + rows], want, f"{kind} config {cfg} {upload}: last frame against the oracle")
     finally:
         g.close()
+
+
+def test_refit_set_stays_bounded(ctx, fresh):
+    """A host that writes a different 1 % of config 5's 100,000 triangles every frame
+    (rt_update_shapes, src/main.cpp:981-992) for 50 frames: the refit set drops the
+    shapes written in earlier frames once they outnumber max(4096, S / 16) and the live
+    ones (compact_refit_set), so a flush's pinned records stay bounded
+    (rt_debug_refit_stats) instead of growing to every shape touched, and every frame
+    equals a fresh upload of the same arrays, bit for bit."""
+    W, H = 256, 144
+    fs = rtamd.generate(5, 0, W, H)
+    S = len(fs.shapes)
+    rng = np.random.default_rng(11)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3, True)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    fresh.set_params(W, H, 3, True)
+    shapes = fs.shapes.copy()
+    order = rng.permutation(S)
+    per = S // 100
+    worst = {"entries": 0, "flush_bytes": 0}
+    for k in range(50):
+        ids = np.sort(order[k * per:(k + 1) * per])
+        moved = _moved(shapes, ids, rng, k)
+        shapes[ids] = moved[ids]
+        for i in ids:  # one record per call, as updateScene writes them
+            ctx.update_shapes(int(i), shapes[i:i + 1])
+        got = ctx.render(W, H)
+        st = ctx.debug_refit_stats()
+        worst = {key: max(worst[key], st[key]) for key in worst}
+        fresh.upload(rtamd.FlatScene(shapes, fs.nodes, fs.indices, fs.camera, fs.light))
+        same(got, fresh.render(W, H), f"frame {k}")
+    bound = 2 * per + max(4096, S // 16)
+    assert ctx.debug_refit_stats()["compactions"] >= 1
+    assert worst["entries"] <= bound, worst
+    assert worst["flush_bytes"] <= bound * (rtamd.SHAPE_DTYPE.itemsize + 4), worst
