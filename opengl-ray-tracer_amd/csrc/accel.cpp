@@ -595,8 +595,9 @@ int make_wide(AccelHost& A, int j, int budget, std::vector<int>& memo, int& pend
         for (int b : sl) m = std::max(m, inner_height(A, b, memo));
         return static_cast<int>(sl.size()) - 1 + m;
     };
+    const int max_kids = A.mt ? kWide : kWideKids;
     for (;;) {
-        if (static_cast<int>(slots.size()) >= kWide) break;
+        if (static_cast<int>(slots.size()) >= max_kids) break;
         int pick = -1;
         float best = -1.f;
         for (int s2 = 0; s2 < static_cast<int>(slots.size()); ++s2)
@@ -612,9 +613,13 @@ int make_wide(AccelHost& A, int j, int budget, std::vector<int>& memo, int& pend
         if (need(next) > budget) break;  // deeper expansion would exceed the stack budget
         slots = next;
     }
+    // one record of kWide children, or two consecutive ones (a pair: up to 2 kWide)
     const int w = static_cast<int>(A.wchild.size()) / kWide;
-    A.wchild.resize(A.wchild.size() + kWide, -1);
-    A.wsub.resize(A.wsub.size() + kWide, -1);
+    const int recs = static_cast<int>(slots.size()) > kWide ? 2 : 1;
+    A.wchild.resize(A.wchild.size() + recs * kWide, -1);
+    A.wsub.resize(A.wsub.size() + recs * kWide, -1);
+    A.wpair.resize(A.wpair.size() + recs, 0);
+    A.wpair[w] = recs == 2;
     const int own = static_cast<int>(slots.size()) - 1;
     int below = 0;
     for (int s2 = 0; s2 < static_cast<int>(slots.size()); ++s2) {
@@ -1077,6 +1082,7 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
         st.wroot = 0;
         T.wchild.assign(kWide, -1);
         T.wsub.assign(kWide, -1);
+        T.wpair.assign(1, 0);
         T.wchild[0] = root;
     }
     st.max_stack = std::min(pend + 2, cap);
@@ -1099,6 +1105,7 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
     }
     st.wchild = T.wchild;
     st.wsub = T.wsub;
+    st.wpair = T.wpair;
     out.st_cone = T.lcone;
 }
 
@@ -1107,6 +1114,7 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
 static int build_wide(AccelHost& A, const std::vector<int>& ref_depth, int cap) {
     A.wchild.clear();
     A.wsub.clear();
+    A.wpair.clear();
     A.wroot.assign(A.local_root.size(), -1);
     std::vector<int> memo(A.lbox.size(), -1);
     int need = 0;

@@ -53,6 +53,7 @@ struct SceneTree {
     std::vector<int> item_ref;  // per item: its reference leaf
     std::vector<int> item_start, item_count;  // per item: prim range (AccelHost prims)
     std::vector<int> wchild, wsub;            // wide collapse (as AccelHost)
+    std::vector<char> wpair;                  // per record (as AccelHost)
     int wroot = -1;             // wide root, -1: no scene tree for this scene
     int max_stack = 0;          // the lane walk's stack bound over it
     int height = 0;             // binary height
@@ -81,6 +82,10 @@ struct AccelHost {
     // wchild = binary node index or -1, wsub = wide node of an inner child or -1.
     // wroot = wide node of each reference leaf's local root (-1: none, or a leaf).
     std::vector<int> wchild, wsub, wroot;
+    // Per record of kWide children: 1 if it and the next record are ONE node of up to
+    // 2 kWide children (kWideKids = 8, barycentric accelerators): the walk tests both
+    // records' children at one step (rt_kernels.hip, the kPair bit of the node's code).
+    std::vector<char> wpair;
     int max_stack = 0;            // worst-case wave stack entries
     // Largest |coordinate| of any bounded shape box, and the largest |coordinate|
     // of a ray origin the bounds are built for (kOriginRel * (scene_mag + 1)).
@@ -115,7 +120,14 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 // Back-face cones of the local nodes (fills A.lcone; grazing cones when A.mt).
 void build_cones(const FlatShape* shapes, AccelHost& A);
 
-constexpr int kWide = 4;
+constexpr int kWide = 4;  // children per wide record (one 128-byte record of the barycentric accelerator)
+// Children per wide node of the barycentric accelerators: 8 = two consecutive records
+// tested at one step (half as many... log8 instead of log4 dependent node steps per
+// descent), or 4. Moller-Trumbore accelerators stay at kWide.
+#ifndef RT_WIDE8
+#define RT_WIDE8 0
+#endif
+constexpr int kWideKids = RT_WIDE8 ? 2 * kWide : kWide;
 // Cone threshold of a scene-tree node without a distance bound (SceneTree).
 constexpr float kNoPrune = -8.0f;
 // Stack entries the lane walk keeps per lane in LDS (6 B each: code + bf16

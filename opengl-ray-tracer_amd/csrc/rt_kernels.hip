@@ -580,7 +580,11 @@ struct AccelPtrs {
 
 // Child codes of the walks' stacks and of lnodes / wnodes entries.
 constexpr unsigned kLocal = 0x80000000u, kLeaf = 0x40000000u, kTopLeaf = 0x20000000u, kItem = 0x10000000u;
+// A wide-node code (kLocal without kLeaf) with kPair names a node of two consecutive
+// records (accel.h kWideKids, AccelHost::wpair): both are tested at one step.
+constexpr unsigned kPair = 0x08000000u, kRecMask = 0x07ffffffu;
 constexpr int kNoChild = 0x7fffffff;
+constexpr bool kWide8 = RT_WIDE8 != 0;
 
 // The closest hit so far: distance, rank in the reference walk, ray parameter and
 // record slot. The hit point is o + t d, recomputed from t after the walk: the same
@@ -912,7 +916,7 @@ __host__ __device__ __forceinline__ float* wide_box_f(float4* lnodes, int rec, i
 
 template <bool MT = false>
 __device__ __forceinline__ Kids4 wide_kids(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
-    const float4* q = A.lnodes + (MT ? kWideRecMt : kWideRec) * static_cast<size_t>(uc & 0x3fffffffu);
+    const float4* q = A.lnodes + (MT ? kWideRecMt : kWideRec) * static_cast<size_t>(uc & kRecMask);
     float t[4];
     bool h[4];
     int cc[4];
@@ -983,6 +987,56 @@ __device__ __forceinline__ void sort4(Kids4& k) {
     cas(k, 0, 2);
     cas(k, 1, 3);
     cas(k, 1, 2);
+}
+
+// The second record of a kPair node (its children 4-7), or none: every child a miss.
+template <bool MT = false>
+__device__ __forceinline__ Kids4 wide_kids_hi(const AccelPtrs& A, unsigned uc, const rta::RayC& c, float tl, bool in) {
+    Kids4 k;
+    if (!MT && kWide8 && (uc & kPair)) return wide_kids<MT>(A, uc + 1u, c, tl, in);
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+        k.t[s2] = INFINITY;
+        k.code[s2] = kNoChild;
+    }
+    return k;
+}
+
+// Both records' children as one list sorted by entry parameter (19-comparator
+// network), for the split walk's shared prologue.
+struct Kids8 {
+    float t[8];
+    int code[8];
+};
+__device__ __forceinline__ Kids8 sort8(const Kids4& a, const Kids4& b) {
+    Kids8 k;
+#pragma unroll
+    for (int s2 = 0; s2 < 4; ++s2) {
+        k.t[s2] = a.t[s2], k.code[s2] = a.code[s2];
+        k.t[4 + s2] = b.t[s2], k.code[4 + s2] = b.code[s2];
+    }
+    auto cx = [&](int i, int j) {
+        const bool sw = k.t[j] < k.t[i];
+        const float ti = k.t[i], tj = k.t[j];
+        const int ci = k.code[i], cj = k.code[j];
+        k.t[i] = sw ? tj : ti, k.t[j] = sw ? ti : tj;
+        k.code[i] = sw ? cj : ci, k.code[j] = sw ? ci : cj;
+    };
+    cx(0, 1), cx(2, 3), cx(4, 5), cx(6, 7), cx(0, 2), cx(1, 3), cx(4, 6), cx(5, 7), cx(1, 2), cx(5, 6);
+    cx(0, 4), cx(1, 5), cx(2, 6), cx(3, 7), cx(2, 4), cx(3, 5), cx(1, 2), cx(3, 4), cx(5, 6);
+    return k;
+}
+__device__ __forceinline__ int pick_code8(const Kids8& k, int i) {
+    int r = k.code[0];
+#pragma unroll
+    for (int s2 = 1; s2 < 8; ++s2) r = i == s2 ? k.code[s2] : r;
+    return r;
+}
+__device__ __forceinline__ float pick_t8(const Kids8& k, int i) {
+    float r = k.t[0];
+#pragma unroll
+    for (int s2 = 1; s2 < 8; ++s2) r = i == s2 ? k.t[s2] : r;
+    return r;
 }
 
 // k.code[i] / k.t[i] for a lane-varying i (selects, no indexed registers)
@@ -1077,28 +1131,56 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                 have = lf.z != kNoChild;
                 cur = lf.z;
             } else if (uc & kLocal) {
-                Kids4 w = wide_kids<MT>(A, uc, c, tl0, true);
-                sort4(w);
-                const int h = (w.t[0] < INFINITY) + (w.t[1] < INFINITY) + (w.t[2] < INFINITY) + (w.t[3] < INFINITY);
-                if (h == 0) {
-                    have = false;
-                } else if (h >= ss) {  // positions si and si + ss (ss >= 2, h <= 4) are this lane's
-                    if (si + ss < h) {
-                        if (sp < pcap) {
-                            stk[sp] = pick_code(w, si + ss);
-                            stt[sp] = f_bf16_down(pick_t(w, si + ss));
-                            sp += stride;
-                        } else {
-                            ovf = true;
+                if constexpr (!MT && kWide8) {
+                    // a kPair node: both records' children, sorted as one list of up to 8
+                    const Kids8 w = sort8(wide_kids<MT>(A, uc, c, tl0, true), wide_kids_hi<MT>(A, uc, c, tl0, true));
+                    int h = 0;
+#pragma unroll
+                    for (int s2 = 0; s2 < 8; ++s2) h += w.t[s2] < INFINITY;
+                    if (h == 0) {
+                        have = false;
+                    } else if (h >= ss) {  // positions si, si + ss, ... (ss >= 2, h <= 8) are this lane's
+                        for (int q = si + ss; q < h; q += ss) {
+                            if (sp < pcap) {
+                                stk[sp] = pick_code8(w, q);
+                                stt[sp] = f_bf16_down(pick_t8(w, q));
+                                sp += stride;
+                            } else {
+                                ovf = true;
+                            }
                         }
+                        cur = pick_code8(w, si);
+                        ss = 1;
+                    } else {  // child p, shared by the lanes [lo, hi) of this share
+                        const int p = si * h / ss, lo = (p * ss + h - 1) / h, hi = ((p + 1) * ss + h - 1) / h;
+                        cur = pick_code8(w, p);
+                        si -= lo;
+                        ss = hi - lo;
                     }
-                    cur = pick_code(w, si);
-                    ss = 1;
-                } else {  // child p, shared by the lanes [lo, hi) of this share
-                    const int p = si * h / ss, lo = (p * ss + h - 1) / h, hi = ((p + 1) * ss + h - 1) / h;
-                    cur = pick_code(w, p);
-                    si -= lo;
-                    ss = hi - lo;
+                } else {
+                    Kids4 w = wide_kids<MT>(A, uc, c, tl0, true);
+                    sort4(w);
+                    const int h = (w.t[0] < INFINITY) + (w.t[1] < INFINITY) + (w.t[2] < INFINITY) + (w.t[3] < INFINITY);
+                    if (h == 0) {
+                        have = false;
+                    } else if (h >= ss) {  // positions si and si + ss (ss >= 2, h <= 4) are this lane's
+                        if (si + ss < h) {
+                            if (sp < pcap) {
+                                stk[sp] = pick_code(w, si + ss);
+                                stt[sp] = f_bf16_down(pick_t(w, si + ss));
+                                sp += stride;
+                            } else {
+                                ovf = true;
+                            }
+                        }
+                        cur = pick_code(w, si);
+                        ss = 1;
+                    } else {  // child p, shared by the lanes [lo, hi) of this share
+                        const int p = si * h / ss, lo = (p * ss + h - 1) / h, hi = ((p + 1) * ss + h - 1) / h;
+                        cur = pick_code(w, p);
+                        si -= lo;
+                        ss = hi - lo;
+                    }
                 }
             } else {
                 const Kids k = ref_kids(A, uc, r, inv, c, tl0, true, fast);
@@ -1188,19 +1270,41 @@ __device__ void lane_walk(const AccelPtrs& A, const Ray& r, bool active, float l
                         count = static_cast<int>(uc & 0x3fu);
                         if (uc & kItem) count = ((fm >> (count >> 3)) & 1u) ? (count & 7) : 0;  // few-leaf item
                     } else {
-                        Kids4 w = wide_kids<MT>(A, uc, c, tl, true);
-                        sort4(w);
-#pragma unroll
-                        for (int s2 = 3; s2 >= 1; --s2) {
-                            if (w.t[s2] < INFINITY) {
+                        auto push = [&](float t, int code) {
+                            if (t < INFINITY) {
                                 if (sp < pcap) {
-                                    stk[sp] = w.code[s2];
-                                    stt[sp] = f_bf16_down(w.t[s2]);
+                                    stk[sp] = code;
+                                    stt[sp] = f_bf16_down(t);
                                     sp += stride;
                                 } else {
                                     ovf = true;  // scene tree only: local trees fit their bound
                                 }
                             }
+                        };
+                        // a node of two records (kPair): the second record's children first,
+                        // sorted, its 2nd-4th stacked; then the first record's; the nearer of
+                        // the two records' nearest is walked, the other stacked last. One
+                        // record's values live at a time (the walk is at the VGPR cap).
+                        const bool pair = !MT && kWide8 && (uc & kPair);
+                        float vt = INFINITY;
+                        int vc = kNoChild;
+                        if (pair) {
+                            Kids4 v = wide_kids<MT>(A, uc + 1u, c, tl, true);
+                            sort4(v);
+#pragma unroll
+                            for (int s2 = 3; s2 >= 1; --s2) push(v.t[s2], v.code[s2]);
+                            vt = v.t[0];
+                            vc = v.code[0];
+                        }
+                        Kids4 w = wide_kids<MT>(A, uc, c, tl, true);
+                        sort4(w);
+#pragma unroll
+                        for (int s2 = 3; s2 >= 1; --s2) push(w.t[s2], w.code[s2]);
+                        if (pair) {
+                            const bool vf = vt < w.t[0];
+                            push(vf ? w.t[0] : vt, vf ? w.code[0] : vc);
+                            w.t[0] = vf ? vt : w.t[0];
+                            w.code[0] = vf ? vc : w.code[0];
                         }
                         if (w.t[0] < INFINITY) cur = w.code[0];
                     }
@@ -1424,21 +1528,26 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
         } else if (uc & kLocal) {
             // wide node: children ordered by the entry parameters of the first lane
             // that enters any of them; the rest pushed far to near
-            const Kids4 w = wide_kids<MT>(A, uc, c, tl, lane_in(m));
-            unsigned long long wm[4];
-            float key[4];
-            int code[4];
+            // a kPair node (uniform): both records' children, up to 8
+            constexpr int NK = !MT && kWide8 ? 8 : 4;
+            Kids4 wk[2];
+            wk[0] = wide_kids<MT>(A, uc, c, tl, lane_in(m));
+            if (NK == 8) wk[1] = wide_kids_hi<MT>(A, uc, c, tl, lane_in(m));
+            unsigned long long wm[NK];
+            float key[NK];
+            int code[NK];
             unsigned long long any = 0;
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                wm[s2] = __ballot(w.t[s2] < INFINITY);
+            for (int s2 = 0; s2 < NK; ++s2) {
+                wm[s2] = __ballot(wk[s2 >> 2].t[s2 & 3] < INFINITY);
                 any |= wm[s2];
             }
             const int rep = any ? __builtin_ctzll(any) : 0;
 #pragma unroll
-            for (int s2 = 0; s2 < 4; ++s2) {
-                key[s2] = wm[s2] ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.t[s2]), rep)) : INFINITY;
-                code[s2] = uni(w.code[s2]);
+            for (int s2 = 0; s2 < NK; ++s2) {
+                const Kids4& w = wk[s2 >> 2];
+                key[s2] = wm[s2] ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w.t[s2 & 3]), rep)) : INFINITY;
+                code[s2] = uni(w.code[s2 & 3]);
                 if (wm[s2] && !(key[s2] < INFINITY)) key[s2] = 3.0e38f;  // the representative lane misses it
             }
 #define RT_CAS3(i, j)                                                                   \
@@ -1447,10 +1556,16 @@ __device__ void packet_walk(const AccelPtrs& A, const Ray& r, bool active, float
         const int c_ = code[i]; code[i] = code[j]; code[j] = c_;                        \
         const unsigned long long m_ = wm[i]; wm[i] = wm[j]; wm[j] = m_;                 \
     }
-            RT_CAS3(0, 1) RT_CAS3(2, 3) RT_CAS3(0, 2) RT_CAS3(1, 3) RT_CAS3(1, 2)
+            if (NK == 8) {
+                RT_CAS3(0, 1) RT_CAS3(2, 3) RT_CAS3(4, 5) RT_CAS3(6, 7) RT_CAS3(0, 2) RT_CAS3(1, 3) RT_CAS3(4, 6)
+                RT_CAS3(5, 7) RT_CAS3(1, 2) RT_CAS3(5, 6) RT_CAS3(0, 4) RT_CAS3(1, 5) RT_CAS3(2, 6) RT_CAS3(3, 7)
+                RT_CAS3(2, 4) RT_CAS3(3, 5) RT_CAS3(1, 2) RT_CAS3(3, 4) RT_CAS3(5, 6)
+            } else {
+                RT_CAS3(0, 1) RT_CAS3(2, 3) RT_CAS3(0, 2) RT_CAS3(1, 3) RT_CAS3(1, 2)
+            }
 #undef RT_CAS3
 #pragma unroll
-            for (int s2 = 3; s2 >= 1; --s2)
+            for (int s2 = NK - 1; s2 >= 1; --s2)
                 if (wm[s2]) {
                     if (st.sp < pcap) st.push(code[s2], wm[s2]);
                     else ovf |= wm[s2];  // scene tree only: local trees fit their bound
@@ -3074,11 +3189,16 @@ int build_upload_accel(rt_ctx* c) {
     const bool use_st = T.wroot >= 0;
     const size_t nw = A.wchild.size() / rta::kWide;
     const size_t nws = use_st ? T.wchild.size() / rta::kWide : 0;
-    if (nw + nws >= (1u << 28) || T.item_ref.size() >= (1u << 28)) return RT_OK;
+    if (nw + nws >= (1u << 27) || T.item_ref.size() >= (1u << 28)) return RT_OK;  // kRecMask, kItem
+    // the code of the node whose first record is r (+ base): kPair when it spans two
+    auto wide_code = [](const std::vector<char>& pair, int r, size_t base) {
+        return static_cast<int>(kLocal | static_cast<unsigned>(base + r) |
+                                (r < static_cast<int>(pair.size()) && pair[r] ? kPair : 0u));
+    };
     std::vector<float4> ln(rec * (nw + nws ? nw + nws : 1));
     auto emit_wide = [&](size_t w, size_t at, const std::vector<int>& wchild, const std::vector<int>& wsub,
-                         const std::vector<rta::Box3>& boxes, const std::vector<float>& cones,
-                         const std::function<int(int)>& leaf_of, size_t sub_base) {
+                         const std::vector<char>& wpair, const std::vector<rta::Box3>& boxes,
+                         const std::vector<float>& cones, const std::function<int(int)>& leaf_of, size_t sub_base) {
         float v[kWideRecMt][4];
         for (int s2 = 0; s2 < 4; ++s2) {
             const int j = wchild[rta::kWide * w + s2];
@@ -3095,7 +3215,7 @@ int build_upload_accel(rt_ctx* c) {
                 if (A.mt && boxes.data() == A.lbox.data())
                     for (int a = 0; a < rta::kMtPadF; ++a) mtc[a] = A.lmt[rta::kMtPadF * j + a];
                 const int sub = wsub[rta::kWide * w + s2];
-                code = sub < 0 ? leaf_of(j) : static_cast<int>(kLocal | static_cast<unsigned>(sub_base + sub));
+                code = sub < 0 ? leaf_of(j) : wide_code(wpair, sub, sub_base);
             }
             if (A.mt) {  // per child 16 floats: box, cone, the per-ray padding constants
                 float* blk = &v[0][0] + 16 * s2;
@@ -3111,8 +3231,8 @@ int build_upload_accel(rt_ctx* c) {
         for (int r = 0; r < rec; ++r) ln[rec * at + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
     };
     for (size_t w = 0; w < nw; ++w)
-        emit_wide(w, w, A.wchild, A.wsub, A.lbox, A.lcone, [&](int j) { return leaf_code(static_cast<size_t>(j)); },
-                  0);
+        emit_wide(w, w, A.wchild, A.wsub, A.wpair, A.lbox, A.lcone,
+                  [&](int j) { return leaf_code(static_cast<size_t>(j)); }, 0);
     // Items: with <= 8 distinct reference leaves (few-leaf mode, few_mask) a
     // local-leaf code kLocal|kLeaf|kItem|start<<6|leaf<<3|count and titems =
     // the leaves' exact boxes; otherwise kTopLeaf|kItem|item and titems = per
@@ -3138,7 +3258,8 @@ int build_upload_accel(rt_ctx* c) {
     };
     std::vector<float4> ti(2 * (use_st ? std::max<size_t>(T.item_ref.size(), 1) : 1));
     if (use_st) {
-        for (size_t w = 0; w < nws; ++w) emit_wide(w, nw + w, T.wchild, T.wsub, T.box, A.st_cone, item_code, nw);
+        for (size_t w = 0; w < nws; ++w)
+            emit_wide(w, nw + w, T.wchild, T.wsub, T.wpair, T.box, A.st_cone, item_code, nw);
         auto put = [&](size_t i, int ref, int start, int count) {
             const FlatNode& n = c->host_nodes[ref];
             ti[2 * i] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(start));
@@ -3165,7 +3286,7 @@ int build_upload_accel(rt_ctx* c) {
         const FlatNode& n = c->host_nodes[k];
         if (n.leftChild == -1) {
             const int r = A.local_root[k];
-            const int lr = A.wroot[k] >= 0 ? static_cast<int>(kLocal | static_cast<unsigned>(A.wroot[k]))
+            const int lr = A.wroot[k] >= 0 ? wide_code(A.wpair, A.wroot[k], 0)
                                            : (r >= 0 ? leaf_code(static_cast<size_t>(r)) : kNoChild);
             tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr, 0);
             continue;
@@ -3208,7 +3329,7 @@ int build_upload_accel(rt_ctx* c) {
                            c->prim_idx_dev + P, static_cast<int>(P), c->prims);
     HIP_TRY(hipGetLastError());
     HIP_TRY(sync_stream(c));  // the host vectors die here
-    c->st_root = use_st ? static_cast<int>(kLocal | static_cast<unsigned>(nw + T.wroot)) : kNoChild;
+    c->st_root = use_st ? wide_code(T.wpair, T.wroot, nw) : kNoChild;
     c->accel_ok = true;
     c->record_bytes = (an.size() + ln.size() + wn.size() + tl.size() + ti.size() + 4 * P + 2 * static_cast<size_t>(c->S)) *
                       sizeof(float4);

@@ -22,7 +22,9 @@ from dataclasses import dataclass
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIBDIR = os.path.join(HERE, "lib")
+# RTAMD_LIBDIR: another build's directory (librtamd.so, librtscene.so, librthost.so), for
+# A/B profiling of build variants (tools/build_var.sh); the default is the in-tree lib/
+LIBDIR = os.environ.get("RTAMD_LIBDIR") or os.path.join(HERE, "lib")
 
 # ---------------------------------------------------------------------------
 # Record layouts (include/rt_flat.h; sizes pinned by static asserts there).

@@ -122,11 +122,11 @@ unsigned long long accel_hash(const FlatShape* shapes, int S, const FlatNode* no
     };
     auto sc = [&](const auto& x) { bytes(&x, sizeof x); };
     v(A.prim_shape); v(A.prim_seq); v(A.content); v(A.flags); v(A.plain_start); v(A.plain_count);
-    v(A.local_root); v(A.lbox); v(A.la); v(A.lb); v(A.lcone); v(A.wchild); v(A.wsub); v(A.wroot);
+    v(A.local_root); v(A.lbox); v(A.la); v(A.lb); v(A.lcone); v(A.wchild); v(A.wsub); v(A.wroot); v(A.wpair);
     sc(A.max_stack); sc(A.scene_mag); sc(A.origin_lim); sc(A.always_prims); sc(A.bounded_prims);
     sc(A.local_leaves);
     v(A.st.box); v(A.st.a); v(A.st.b); v(A.st.item_of); v(A.st.item_ref); v(A.st.item_start);
-    v(A.st.item_count); v(A.st.wchild); v(A.st.wsub); sc(A.st.wroot); sc(A.st.max_stack); sc(A.st.height);
+    v(A.st.item_count); v(A.st.wchild); v(A.st.wsub); v(A.st.wpair); sc(A.st.wroot); sc(A.st.max_stack); sc(A.st.height);
     sc(A.st.nested); v(A.st_cone); v(A.lmt); sc(A.mt_z);
     return h;
 }
@@ -155,9 +155,13 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
             if (std::isnan(v)) boxes_finite = false;
     constexpr int kSceneBase = 1 << 29;
     // ACSTAT: wide-node visits per depth below the local roots
+    // children of the node whose first record is w: kWide, or 2 kWide for a pair (accel.h wpair)
+    auto kids = [](const std::vector<char>& pair, int w) {
+        return rta::kWide * (w < static_cast<int>(pair.size()) && pair[w] ? 2 : 1);
+    };
     std::vector<int> wdepth(A.wchild.size() / rta::kWide, 0);
     for (size_t w = 0; w < wdepth.size(); ++w)
-        for (int s2 = 0; s2 < rta::kWide; ++s2)
+        for (int s2 = 0; s2 < kids(A.wpair, static_cast<int>(w)); ++s2)
             if (A.wsub[rta::kWide * w + s2] >= 0) wdepth[A.wsub[rta::kWide * w + s2]] = wdepth[w] + 1;
     long long per_depth[64] = {0}, forced_depth[64] = {0};
     long long tests = 0, scene_rays = 0, pops = 0, forced = 0;
@@ -208,7 +212,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     // scene-tree wide node: padded boxes and cones; an item tests its
                     // reference leaf's exact box before its shapes
                     const int w = -(code + kSceneBase) - 1;
-                    for (int s2 = 0; s2 < rta::kWide; ++s2) {
+                    for (int s2 = 0; s2 < kids(A.st.wpair, w); ++s2) {
                         const int j = A.st.wchild[rta::kWide * w + s2];
                         if (j < 0) continue;
                         const float* k = &A.st_cone[4 * j];
@@ -242,7 +246,7 @@ int accel_check(const FlatShape* shapes, int S, const FlatNode* nodes, int N, co
                     // box and back-face cone, tested at the wide node
                     const int w = -code - 1;
                     ++per_depth[std::min(63, wdepth[w])];
-                    for (int s2 = 0; s2 < rta::kWide; ++s2) {
+                    for (int s2 = 0; s2 < kids(A.wpair, w); ++s2) {
                         const int j = A.wchild[rta::kWide * w + s2];
                         if (j < 0) continue;
                         const float* k = &A.lcone[4 * j];
