@@ -12,7 +12,7 @@ the rows rank r renders when P GPUs split the frame into interleaved 8-row strip
     as `parts` waves), since the auto setting (tiles / 200 as 4 waves) was swept on
     whole frames only.
 
-    GPU_MAX_HW_QUEUES=16 python tools/share_sweep.py [--sizes 1080,2160] [--parts 1,2,4,8]
+    [RT_HW_QUEUES=16] python tools/share_sweep.py [--sizes 1080,2160] [--parts 1,2,4,8]
 Prints one JSON object.
 """
 import argparse
@@ -21,7 +21,10 @@ import os
 import sys
 import time
 
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")  # before the HIP runtime starts
+# before the HIP runtime starts; set, not defaulted: the GPU box exports 4, and with 4
+# queues F = 8 contexts share them and run in order (r05's in-flight share figures were
+# taken that way: 1/8 share 0.050 ms at F = 8, 0.031 with 8 or 16 queues, r06f)
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("RT_HW_QUEUES", "16")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
