@@ -4366,6 +4366,16 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
                                    std::min(k2.lane_from_depth, k2.shadow_lane_from) >= k2.maxBounces;
                 hk = small ? std::max(16, k2.tiles / 256) : 0;
                 hp = small ? 8 : 1;
+                if (small && latency) {
+                    // Waited, such a frame ends on its heaviest packet chains: split into 32
+                    // waves of 2 rays, a tile's parts walk little more than their own rays'
+                    // nodes. Config 2 waited (Python loop, tools/latency_sweep.py, r06k-r06m):
+                    // 29 x 8 (the in-flight rule) 0.0957 ms, 40 x 16 0.0907, 40 x 32 0.0793,
+                    // 60 / 120 x 32 0.0798, 20 x 32 0.0819, 40 x 64 0.0855. In flight the
+                    // in-flight rule stays best (4 frames: 0.0314 against 0.0416 with 40 x 32).
+                    hk = std::max(16, k2.tiles / 128);
+                    hp = 32;
+                }
                 if (!small && latency) {
                     // rt_set_latency_mode: the heaviest 1/200 as 4 waves. Car waited frame with the
                     // wall-time cost order and whole-tile cost frames (Python loop,
@@ -5317,7 +5327,7 @@ extern "C" int rt_debug_sched_order(rt_ctx* c, int* out, int n) {
 // waves (1, 2, 4 or 8), one band of 64 / parts pixels per wave; parts = 1: off;
 // k = -1: the default policy (kHeavyAutoSlots).
 extern "C" int rt_debug_heavy(rt_ctx* c, int k, int parts) {
-    if (!c || k < -1 || parts < 1 || parts > 32 || (parts & (parts - 1)) != 0) return RT_ERR_INVALID;
+    if (!c || k < -1 || parts < 1 || parts > 64 || (parts & (parts - 1)) != 0) return RT_ERR_INVALID;
     c->heavy_k = k;
     c->heavy_parts = parts;
     return RT_OK;

@@ -42,7 +42,11 @@ if a.child is None:
         for name in ("current", "lib2"):
             out = subprocess.run([sys.executable, __file__, "--lib2", a.lib2, "--config", str(a.config),
                                   "--inflight", str(a.inflight), "--frames", str(a.frames), "--bounces", str(a.bounces)] + (["--mt"] if a.mt else []) + ["--walk2", str(a.walk2), "--set2", a.set2, "--set", a.set, "--child", name],
-                                 capture_output=True, text=True, check=True).stdout.strip().splitlines()[-1]
+                                 capture_output=True, text=True, check=True,
+                                 # 2F hardware queues, as bench.plan_inflight sets (the box exports 4,
+                                 # and F contexts on 4 shared queues run partly in order)
+                                 env=dict(os.environ, GPU_MAX_HW_QUEUES=str(max(6, 2 * a.inflight)))
+                                 ).stdout.strip().splitlines()[-1]
             r = json.loads(out)
             res[name].append(r["ms"])
             img = np.load(r["img"])

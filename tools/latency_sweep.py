@@ -44,6 +44,35 @@ SETTINGS = {
     "split16x32": {"split": (16, 32)},
     "split32x16": {"split": (32, 16)},
     "split4x8": {"split": (4, 8)},
+    # Sweep 10 (r06): config 2's waited frame (the monkey scene, all-packet: primary + shadow),
+    # whose slowest tiles are packet-step chains (profiles/r06h_tile_profile_latency_c2.txt)
+    "heavy_off": {"heavy": (0, 1)},
+    "heavy300x2": {"heavy": (300, 2)},
+    "heavy150x4": {"heavy": (150, 4)},
+    "heavy75x8": {"heavy": (75, 8)},
+    "heavy40x16": {"heavy": (40, 16)},
+    "lanek64x1": {"lane_k": (64, 1)},
+    "lanek64x3": {"lane_k": (64, 3)},
+    "lanek256x3": {"lane_k": (256, 3)},
+    "lanek1024x3": {"lane_k": (1024, 3)},
+    "latency0": {"latency": 0},
+    "lanek32x3": {"lane_k": (32, 3)},
+    "lanek128x3": {"lane_k": (128, 3)},
+    "lanek64x3_h40x16": {"lane_k": (64, 3), "heavy": (40, 16)},
+    "lanek64x3_h40x8": {"lane_k": (64, 3), "heavy": (40, 8)},
+    "lanek128x3_h40x16": {"lane_k": (128, 3), "heavy": (40, 16)},
+    "lanek64x3_h20x16": {"lane_k": (64, 3), "heavy": (20, 16)},
+    "lanek64x3_h80x16": {"lane_k": (64, 3), "heavy": (80, 16)},
+    "h20x16": {"heavy": (20, 16)},
+    "h40x32": {"heavy": (40, 32)},
+    "h20x32": {"heavy": (20, 32)},
+    "h60x32": {"heavy": (60, 32)},
+    "h80x32": {"heavy": (80, 32)},
+    "h120x32": {"heavy": (120, 32)},
+    "h20x64": {"heavy": (20, 64)},
+    "h40x64": {"heavy": (40, 64)},
+    "h80x64": {"heavy": (80, 64)},
+    "h160x16": {"heavy": (160, 16)},
 }
 
 
