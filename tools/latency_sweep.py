@@ -73,6 +73,15 @@ SETTINGS = {
     "h40x64": {"heavy": (40, 64)},
     "h80x64": {"heavy": (80, 64)},
     "h160x16": {"heavy": (160, 16)},
+    # the car (config 3): whole-frame rule 162 x 2
+    "h162x4": {"heavy": (162, 4)},
+    "h162x8": {"heavy": (162, 8)},
+    "h162x16": {"heavy": (162, 16)},
+    "h162x32": {"heavy": (162, 32)},
+    "h81x16": {"heavy": (81, 16)},
+    "h81x32": {"heavy": (81, 32)},
+    "h324x8": {"heavy": (324, 8)},
+    "h324x16": {"heavy": (324, 16)},
 }
 
 
