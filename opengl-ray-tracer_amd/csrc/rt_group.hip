@@ -564,8 +564,9 @@ int rt_group_set_animated(rt_group* g, const int* ids, int count) {
 }
 
 int rt_group_animate(rt_group* g, const FlatShape* shapes) {
-    const int rc = each_ctx(g, [&](rt_ctx* c) { return rt_animate(c, shapes); });
-    if (g) mark_all_dirty(g);  // k_refit is queued on every slot's stream (the bounded waits poll them)
+    // deferred per slot (rtx::animate_deferred): each slot context refits once, at the
+    // dispatch of the next frame it renders, with the growth of every frame since its last
+    const int rc = each_ctx(g, [&](rt_ctx* c) { return rtx::animate_deferred(c, shapes); });
     // the grown root (the sky-row band follows it): the same host computation in every
     // slot context and on every rank
     if (rc == RT_OK) g->have_root = rtx::view_root(g->m[0].slot[0].ctx, g->root_lo, g->root_hi);

@@ -41,4 +41,12 @@ bool matches_view(const rt_ctx* c, const FlatCamera& cam, const float lo[3], con
 // same operations on every rank.
 bool view_root(const rt_ctx* c, float lo[3], float hi[3]);
 
+// rt_animate without the device work: the animated shapes' records and this frame's
+// growth (the union of every deferred frame's growToInclude boxes, per shape) stay on the
+// host until the context's next device operation, whose one refit applies them all
+// (k_refit AF_BOX). rt_group's frame slots take every frame this way: a slot renders
+// every F-th frame, and its refit then runs once per frame it renders, not once per frame.
+// The nodes grow exactly as by one rt_animate per frame (min / max of the same boxes).
+int animate_deferred(rt_ctx* c, const FlatShape* shapes);
+
 }  // namespace rtx

@@ -2195,7 +2195,9 @@ struct AnimMaps {
 // the per-frame flag of a refit entry: the nodes listing it grow to hold it
 // (rt_animate: updateBVH on the device; rt_update_shapes leaves the node boxes to
 // rt_update_nodes, as a glBufferSubData of the shape records does)
-enum { AF_GROW = 4 };
+// AF_BOX (with AF_GROW): the growth is the box the host passed for the entry (the union of
+// several frames' growToInclude boxes: rtx::animate_deferred), not its current record's
+enum { AF_GROW = 4, AF_BOX = 8 };
 
 struct AnimOut {
     FlatShape* shapes;  // staging copy of the full shape array
@@ -2218,7 +2220,8 @@ struct AnimOut {
 // and how its workgroups split the work.
 struct RefitArgs {
     const FlatShape* fresh;    // per entry: its current record (pinned, mapped)
-    const int* flags;          // per entry: AF_GROW (pinned)
+    const int* flags;          // per entry: AF_GROW, AF_BOX (pinned)
+    const float4* gbox;        // per entry with AF_BOX: its growth box (lo, hi; pinned), or null
     const FlatNode* nsrc;      // rt_update_nodes: the host's node records (pinned), or null
     int* report;               // pinned: set to 1 when an entry's bound changed kind
     unsigned* ctr;             // [0] workgroup tickets, [1] finished record workgroups, then the flags
@@ -2334,7 +2337,12 @@ __device__ void refit_record(const AnimMaps& m, const AnimOut& o, const RefitArg
     if (s0 < s1) store_geo(o.geo_leaf + 5 * static_cast<size_t>(slot0), g);
     for (int q = s0 + 1; q < s1; ++q) store_geo(o.geo_leaf + 5 * static_cast<size_t>(m.slot_list[q]), g);
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    if (fl & AF_GROW) reference_box(s, lo, hi);  // else the nodes keep their boxes
+    if (fl & AF_BOX) {  // several frames' boxes, unioned on the host
+        const float4 a = r.gbox[2 * static_cast<size_t>(i)], b = r.gbox[2 * static_cast<size_t>(i) + 1];
+        lo[0] = a.x, lo[1] = a.y, lo[2] = a.z, hi[0] = b.x, hi[1] = b.y, hi[2] = b.z;
+    } else if (fl & AF_GROW) {
+        reference_box(s, lo, hi);  // else the nodes keep their boxes
+    }
     float4* sb = o.sbox + 4 * static_cast<size_t>(i);
     sb[0] = make_float4(lo[0], lo[1], lo[2], 0.f);
     sb[1] = make_float4(hi[0], hi[1], hi[2], 0.f);
@@ -2385,7 +2393,12 @@ __device__ void grow_node(const AnimMaps& m, const AnimOut& o, const RefitArgs& 
             if (r.direct) {  // from the record itself (no wait for the record role)
                 const FlatShape s = r.fresh[i];
                 float rl[3] = {INFINITY, INFINITY, INFINITY}, rh[3] = {-INFINITY, -INFINITY, -INFINITY};
-                if (r.flags[i] & AF_GROW) reference_box(s, rl, rh);
+                if (r.flags[i] & AF_BOX) {
+                    const float4 a = r.gbox[2 * static_cast<size_t>(i)], b = r.gbox[2 * static_cast<size_t>(i) + 1];
+                    rl[0] = a.x, rl[1] = a.y, rl[2] = a.z, rh[0] = b.x, rh[1] = b.y, rh[2] = b.z;
+                } else if (r.flags[i] & AF_GROW) {
+                    reference_box(s, rl, rh);
+                }
                 rta::Box3 cb;
                 if (o.anodes) entry_cbox(o, s, m.ecls[i], cb);
                 else cb = rta::Box3{{INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
@@ -3018,6 +3031,11 @@ struct rt_ctx {
     // lists). rt_group computes its sky-row band from it (rtx::view_root).
     float root_lo[3] = {0.f, 0.f, 0.f}, root_hi[3] = {0.f, 0.f, 0.f};
     std::vector<char> entry_root;       // per refit entry: node N-1 lists it (k_refit grows the root by it)
+    // rtx::animate_deferred (rt_group's frame slots): per animated shape (anim_ids order)
+    // the union of the growToInclude boxes of every frame given since the last flush
+    // (lo xyz, hi xyz), applied by the next flush as that shape's growth (AF_BOX)
+    std::vector<float> grow_box;
+    bool grow_pending = false;
     // The brute-force branch (useBVH = 0, gpu_shader.comp:523-620) tests every shape in
     // index order, keeps the strict-< first minimum and stops shadows at the first
     // occluder: exactly the BVH branch walking a tree of ONE leaf that lists shapes
@@ -3865,7 +3883,8 @@ int flush_updates(rt_ctx* c, bool grow = false) {
     if (!c->have_scene) return RT_OK;
     int rc = check_reports(c);
     if (rc != RT_OK) return rc;
-    const bool work = !c->upd_ids.empty() || c->nodes_dirty || grow;
+    const bool gbox = c->grow_pending && !c->anim_ids.empty();
+    const bool work = !c->upd_ids.empty() || c->nodes_dirty || grow || gbox;
     if (!work && !c->bounds_rebuild) return RT_OK;
     if (work) {
         // shapes new to the refit set join it with their build-time records
@@ -3882,7 +3901,9 @@ int flush_updates(rt_ctx* c, bool grow = false) {
         const int n = static_cast<int>(c->refit_ids.size());
         const bool nodes = c->nodes_dirty && c->N > 0;
         const size_t rec_bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
-        const size_t bytes = rec_bytes + (nodes ? static_cast<size_t>(c->N) * sizeof(FlatNode) : 0);
+        const size_t node_bytes = nodes ? static_cast<size_t>(c->N) * sizeof(FlatNode) : 0;
+        const size_t box_at = (rec_bytes + node_bytes + 15) / 16 * 16;  // growth boxes (AF_BOX), 2 float4 per entry
+        const size_t bytes = gbox ? box_at + static_cast<size_t>(n) * 2 * sizeof(float4) : rec_bytes + node_bytes;
         c->last_flush_bytes = static_cast<long long>(bytes);
         if (bytes > 0) {
             char* pin = nullptr;
@@ -3895,6 +3916,16 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             std::memset(flags, 0, n * sizeof(int));
             if (grow)
                 for (int id : c->anim_ids) flags[c->refit_of[id]] = AF_GROW;
+            if (gbox) {
+                float4* gb = reinterpret_cast<float4*>(pin + box_at);
+                for (size_t k = 0; k < c->anim_ids.size(); ++k) {
+                    const int e = c->refit_of[c->anim_ids[k]];
+                    const float* b = &c->grow_box[6 * k];
+                    flags[e] = AF_GROW | AF_BOX;
+                    gb[2 * e] = make_float4(b[0], b[1], b[2], 0.f);
+                    gb[2 * e + 1] = make_float4(b[3], b[4], b[5], 0.f);
+                }
+            }
             if (nodes) std::memcpy(pin + rec_bytes, c->host_nodes.data(), c->N * sizeof(FlatNode));
             const bool acc = c->accel_ok;
             const size_t P = c->accel.prim_shape.size();
@@ -3930,6 +3961,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             RefitArgs r{};
             r.fresh = reinterpret_cast<const FlatShape*>(src);
             r.flags = reinterpret_cast<const int*>(src + n * sizeof(FlatShape));
+            r.gbox = gbox ? reinterpret_cast<const float4*>(src + box_at) : nullptr;
             r.nsrc = nodes ? reinterpret_cast<const FlatNode*>(src + rec_bytes) : nullptr;
             r.report = reinterpret_cast<int*>(const_cast<char*>(pin_dev) + c->report_at[slot]);
             r.ctr = c->refit_ctr;
@@ -3977,7 +4009,15 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             c->report_pending[slot] = n > 0 && acc;
             if (nodes && (rc = open_inf_slots(c)) != RT_OK) return rc;
         }
-        if (grow) c->nodes_on_device_newer = true;  // the device grew the nodes past host_nodes
+        if (grow || gbox) c->nodes_on_device_newer = true;  // the device grew the nodes past host_nodes
+        if (gbox) {
+            c->grow_pending = false;
+            for (size_t k = 0; k < c->anim_ids.size(); ++k)
+                for (int a = 0; a < 3; ++a) {
+                    c->grow_box[6 * k + a] = INFINITY;
+                    c->grow_box[6 * k + 3 + a] = -INFINITY;
+                }
+        }
         c->nodes_dirty = false;
         for (int id : c->upd_ids) c->upd_mark[id] = 0;
         c->upd_ids.clear();
@@ -4669,6 +4709,46 @@ bool rtx::matches_view(const rt_ctx* c, const FlatCamera& cam, const float lo[3]
     return std::memcmp(c->root_lo, lo, sizeof c->root_lo) == 0 && std::memcmp(c->root_hi, hi, sizeof c->root_hi) == 0;
 }
 
+int rtx::animate_deferred(rt_ctx* c, const FlatShape* shapes) {
+    if (!c || !c->have_scene || c->anim_ids.empty() || !shapes) return RT_ERR_INVALID;
+    const int n = static_cast<int>(c->anim_ids.size());
+    // node records the host wrote before this frame apply first (as rt_animate): a refit
+    // never carries both the host's node records and growth (k_refit's roles would both
+    // write the grown boxes)
+    if (c->nodes_dirty) {
+        if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+        if (const int rc = flush_updates(c)) return rc;
+    }
+    if (c->grow_box.size() != 6 * static_cast<size_t>(n)) return RT_ERR_INVALID;
+    for (int i = 0; i < n; ++i) {
+        const int id = c->anim_ids[i];
+        c->host_shapes[id] = shapes[i];
+        // the growth of this frame, on the host with the device's operations
+        // (reference_box: BoundingBox::growToInclude), unioned with the pending frames'
+        float lo[3], hi[3];
+        reference_box(shapes[i], lo, hi);
+        float* b = &c->grow_box[6 * static_cast<size_t>(i)];
+        for (int a = 0; a < 3; ++a) {
+            b[a] = lo[a] < b[a] ? lo[a] : b[a];
+            b[3 + a] = b[3 + a] < hi[a] ? hi[a] : b[3 + a];
+        }
+        const int e = c->refit_of[id];
+        if (e >= 0 && e < static_cast<int>(c->entry_root.size()) && c->entry_root[e])
+            for (int a = 0; a < 3; ++a) {
+                c->root_lo[a] = lo[a] < c->root_lo[a] ? lo[a] : c->root_lo[a];
+                c->root_hi[a] = c->root_hi[a] < hi[a] ? hi[a] : c->root_hi[a];
+            }
+    }
+    c->grow_pending = true;
+    // the sub-contexts follow as rt_animate makes them: brute force the records (no nodes),
+    // Moller-Trumbore the same deferred frame
+    if (c->brute && !c->brute_stale)
+        for (int i = 0; i < n && !c->brute_stale; ++i)
+            if (rt_update_shapes(c->brute, c->anim_ids[i], 1, &shapes[i]) != RT_OK) c->brute_stale = true;
+    if (c->mtc && !c->mtc_stale && rtx::animate_deferred(c->mtc, shapes) != RT_OK) c->mtc_stale = true;
+    return RT_OK;
+}
+
 bool rtx::view_root(const rt_ctx* c, float lo[3], float hi[3]) {
     if (!c || !c->have_scene || c->N <= 0) return false;
     std::memcpy(lo, c->root_lo, sizeof c->root_lo);
@@ -4820,6 +4900,10 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
 
 int rt_update_nodes(rt_ctx* c, const FlatNode* nodes, int N) {
     if (!c || !c->have_scene || N != c->N || (N > 0 && !nodes)) return RT_ERR_INVALID;
+    if (c->grow_pending) {  // deferred growth (rtx::animate_deferred) applies before these records
+        if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+        if (const int rc = flush_updates(c)) return rc;
+    }
     for (int k = 0; k < N; ++k) {
         const FlatNode &a = nodes[k], &b = c->host_nodes[k];
         if (a.leftChild != b.leftChild || a.rightChild != b.rightChild ||
@@ -4854,7 +4938,17 @@ int rt_set_animated(rt_ctx* c, const int* ids, int count) {
         seen[ids[i]] = 1;
     }
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    if (c->grow_pending) {  // deferred frames of the old set first (rtx::animate_deferred)
+        const int rc = flush_updates(c);
+        if (rc != RT_OK) return rc;
+    }
     c->anim_ids.assign(ids, ids + count);
+    c->grow_box.assign(6 * static_cast<size_t>(count), 0.f);
+    for (int i = 0; i < count; ++i)
+        for (int a = 0; a < 3; ++a) {
+            c->grow_box[6 * i + a] = INFINITY;
+            c->grow_box[6 * i + 3 + a] = -INFINITY;
+        }
     // The refit set takes the new ids with the records the accelerator was built from
     // (a shape rewritten since: its record before the first rewrite); shapes already in
     // it keep their base, and shapes that stop being animated stay in it.
@@ -4879,6 +4973,10 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (!c || !c->have_scene || c->anim_ids.empty() || !shapes) return RT_ERR_INVALID;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     int rc = RT_OK;
+    if (c->grow_pending) {  // deferred frames pending (rtx::animate_deferred): this one joins them
+        if ((rc = rtx::animate_deferred(c, shapes)) != RT_OK) return rc;
+        return flush_updates(c);
+    }
     // node records the host wrote before this frame apply first, then this frame's growth
     if (c->nodes_dirty && (rc = flush_updates(c)) != RT_OK) return rc;
     const int n = static_cast<int>(c->anim_ids.size());
