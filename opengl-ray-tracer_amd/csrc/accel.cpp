@@ -961,7 +961,7 @@ bool boxes_nest(const FlatNode& p, const FlatNode& ch) {
 // Binary height bound of the scene tree (median splits below it).
 constexpr int kSceneHeight = 40;
 
-static double prof_t0 = 0;
+static thread_local double prof_t0 = 0;  // a rebuild thread may build beside another context
 static void prof(const char* what) {
     static const bool on = std::getenv("RTA_BUILD_PROFILE") != nullptr;
     if (!on) return;
@@ -1160,6 +1160,8 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     parallel_chunks(S, 4096, [&](int i0, int i1, int) {
         for (int i = i0; i < i1; ++i) scls[i] = classify(shapes[i], sbox[i], out.origin_lim, mt);
     });
+    out.shape_cls = scls;
+    out.shape_box = sbox;
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -31,7 +32,10 @@
 #include <cstring>
 #include <functional>
 #include <limits>
+#include <atomic>
+#include <memory>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/rt_api.h"
@@ -3024,6 +3028,25 @@ struct rt_ctx {
     int* refit_list = nullptr;          // RefitArgs::dlist
     int n_dirty = 0;
     int anim_rebuilds = 0;              // host rebuilds rt_animate fell back to (diagnostics)
+    // A refit that asks for a rebuild (a bound changed kind, or the node boxes stopped
+    // nesting) starts it on a host thread over a snapshot of the records (AsyncBuild) and
+    // the frames go on meanwhile, exact: a changed-kind shape is entered through every box
+    // above it (k_refit), and while the boxes do not nest the rays walk the reference tree
+    // (st_suspended). The first device operation after the build finishes swaps the new
+    // accelerator in and refits it to the records written since the snapshot. rt_debug_
+    // async_rebuild(0): the rebuild runs in the flush that asked for it, as before round 6.
+    struct AsyncBuild {
+        std::thread th;
+        std::atomic<bool> done{false};
+        bool ok = false;
+        rta::AccelHost A;
+        std::vector<FlatShape> shapes;  // the snapshot the accelerator is built from
+        std::vector<FlatNode> nodes;
+    };
+    std::unique_ptr<AsyncBuild> rebuild;
+    int async_rebuild = 1;
+    bool st_suspended = false;          // the scene tree is off until the rebuild lands
+    int async_swaps = 0;                // rebuilt accelerators swapped in (diagnostics)
     bool nodes_on_device_newer = false; // staging_nodes grew past host_nodes
     // The root node's box as the next render sees it, kept on the host without a
     // readback: set from the records by rt_upload_scene / rt_update_nodes, grown by
@@ -3036,6 +3059,9 @@ struct rt_ctx {
     // (lo xyz, hi xyz), applied by the next flush as that shape's growth (AF_BOX)
     std::vector<float> grow_box;
     bool grow_pending = false;
+    // per shape: its host record may differ from the one the accelerator was built from
+    // (prepare_animation then classifies it again instead of reusing AccelHost::shape_box)
+    std::vector<char> shape_moved;
     // The brute-force branch (useBVH = 0, gpu_shader.comp:523-620) tests every shape in
     // index order, keeps the strict-< first minimum and stops shadows at the first
     // occluder: exactly the BVH branch walking a tree of ONE leaf that lists shapes
@@ -3113,7 +3139,9 @@ void free_accel(rt_ctx* c) {
     c->accel_ok = false;
 }
 
+void discard_rebuild(rt_ctx* c);
 void free_scene(rt_ctx* c) {
+    discard_rebuild(c);
     hipFree(c->geo_lin);
     hipFree(c->geo_leaf);
     hipFree(c->mat);
@@ -3166,14 +3194,22 @@ inline float bits_f(int v) {
 // Builds the accelerator from the host copies of the scene and uploads it;
 // expects geo_lin to be packed (k_pack_prims copies from it). On failure the
 // context keeps rendering with k_packet.
+int upload_built_accel(rt_ctx* c);
 int build_upload_accel(rt_ctx* c) {
     free_accel(c);
     const int N = c->N;
     if (N == 0) return RT_OK;
-    rta::AccelHost& A = c->accel;
     if (!rta::build_accel(c->host_shapes.data(), c->S, c->host_nodes.data(), N, c->host_idx.data(), c->I,
-                          kLeafScan, kMaxStack, A, c->build_mt))
+                          kLeafScan, kMaxStack, c->accel, c->build_mt))
         return RT_OK;
+    return upload_built_accel(c);
+}
+
+// The device half of build_upload_accel: c->accel (built) to the device, with the
+// current host node records' exact boxes and the device's current shape records.
+int upload_built_accel(rt_ctx* c) {
+    const int N = c->N;
+    rta::AccelHost& A = c->accel;
     if (N >= (1 << 28)) return RT_OK;  // codes carry the node index in 28 bits
     c->boxes_finite = 1;
     for (int k = 0; k < N; ++k) {
@@ -3399,6 +3435,14 @@ int open_inf_slots(rt_ctx* c) {
 // anim_base holds, per entry, the record the accelerator's bounds and cones were
 // built from.
 int prepare_animation(rt_ctx* c) {
+    static const bool prof = std::getenv("RT_REBUILD_PROFILE") != nullptr;  // diagnostics: phase times
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char* what) {
+        if (!prof) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "  prepare %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
     const int n = static_cast<int>(c->refit_ids.size());
     c->anim = AnimMaps{};
     c->n_direct_slot_reads = 0;
@@ -3415,12 +3459,25 @@ int prepare_animation(rt_ctx* c) {
         c->anim_cls[i] = rta::classify(c->anim_base[i], b, A.origin_lim, A.mt);
     }
     // reference nodes listing each shape: the leaves that list it and every node above
-    std::vector<std::vector<int>> parents(N);
+    // (CSR: a vector per node took ~6 ms of a config-5 setup)
+    std::vector<int> poff(static_cast<size_t>(N) + 1, 0), plist;
     for (int k = 0; k < N; ++k) {
         const FlatNode& nd = c->host_nodes[k];
         if (nd.leftChild != -1) {
-            parents[nd.leftChild].push_back(k);
-            if (nd.rightChild != nd.leftChild) parents[nd.rightChild].push_back(k);
+            ++poff[nd.leftChild + 1];
+            if (nd.rightChild != nd.leftChild) ++poff[nd.rightChild + 1];
+        }
+    }
+    for (int k = 0; k < N; ++k) poff[k + 1] += poff[k];
+    plist.resize(poff[N]);
+    {
+        std::vector<int> fill(poff.begin(), poff.end() - 1);
+        for (int k = 0; k < N; ++k) {
+            const FlatNode& nd = c->host_nodes[k];
+            if (nd.leftChild != -1) {
+                plist[fill[nd.leftChild]++] = k;
+                if (nd.rightChild != nd.leftChild) plist[fill[nd.rightChild]++] = k;
+            }
         }
     }
     std::vector<std::vector<int>> nodes_of(n), slots_of(n), prims_of(n), wpos_of(n);
@@ -3448,14 +3505,15 @@ int prepare_animation(rt_ctx* c) {
             const int k = todo.back();
             todo.pop_back();
             L.push_back(k);
-            for (int p : parents[k])
-                if (stamp[p] != i) {
+            for (int q = poff[k]; q < poff[k + 1]; ++q)
+                if (const int p = plist[q]; stamp[p] != i) {
                     stamp[p] = i;
                     todo.push_back(p);
                 }
         }
         std::sort(L.begin(), L.end());
     }
+    lap("nodes_of");
     c->entry_root.assign(n, 0);
     for (int i = 0; i < n; ++i) c->entry_root[i] = std::binary_search(nodes_of[i].begin(), nodes_of[i].end(), N - 1);
     if (c->accel_ok) {
@@ -3485,6 +3543,7 @@ int prepare_animation(rt_ctx* c) {
                     dirty[j] = 1;
                 }
         }
+    lap("local maps");
         // prim range of every local subtree (contiguous: LocalBuilder emits a subtree's prims together)
         std::vector<int> first(M, 0), end(M, 0);
         for (size_t j = M; j-- > 0;) {  // children have larger indices than their parent
@@ -3506,6 +3565,7 @@ int prepare_animation(rt_ctx* c) {
         // prims are contiguous. Its unbounded part (kNoPrune: boxes are the padded
         // reference-leaf boxes, which grow) goes infinite while the set is animated;
         // the items' exact boxes follow the grown leaves (k_refit).
+    lap("local ranges");
         const rta::SceneTree& T = A.st;
         if (T.wroot >= 0) {
             const size_t nw = A.wchild.size() / rta::kWide, Ms = T.box.size();
@@ -3548,16 +3608,27 @@ int prepare_animation(rt_ctx* c) {
             for (size_t j = 0; j < Ms; ++j)
                 if (sdirty[j]) work.push_back(make_int4(swpos[j], sfirst[j], send[j], 0));
         }
+    lap("scene tree maps");
         std::vector<float4> pb(2 * (P ? P : 1), make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+        const bool cached = A.shape_cls.size() == static_cast<size_t>(c->S) && c->shape_moved.size() == A.shape_cls.size();
         for (size_t p = 0; p < P; ++p) {
             rta::Box3 b;
-            if (rta::classify(c->host_shapes[A.prim_shape[p]], b, A.origin_lim, A.mt) != rta::BOUNDED) {
+            const int sh = A.prim_shape[p];
+            int cls;
+            if (cached && !c->shape_moved[sh]) {
+                cls = A.shape_cls[sh];
+                b = A.shape_box[sh];
+            } else {
+                cls = rta::classify(c->host_shapes[sh], b, A.origin_lim, A.mt);
+            }
+            if (cls != rta::BOUNDED) {
                 pb[2 * p + 1] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
                 continue;
             }
             pb[2 * p] = make_float4(b.lo[0], b.lo[1], b.lo[2], 0.f);
             pb[2 * p + 1] = make_float4(b.hi[0], b.hi[1], b.hi[2], 0.f);
         }
+    lap("prim boxes (classify)");
         // per dirty slot: the box of its prims outside the refit set (they never move
         // while this set stands) and the list of those in it, which k_refit unions per frame
         c->dirty_max = c->dirty_sum = 0;
@@ -3597,6 +3668,7 @@ int prepare_animation(rt_ctx* c) {
             st[2 * q] = make_float4(lo[0], lo[1], lo[2], 0.f);
             st[2 * q + 1] = make_float4(hi[0], hi[1], hi[2], 0.f);
         }
+    lap("slot static boxes");
         const int nw = static_cast<int>(work.size());
         work.push_back(make_int4(0, 0, 0, static_cast<int>(dl.size())));  // the end of the last list
         if (dl.empty()) dl.push_back(0);
@@ -3625,6 +3697,7 @@ int prepare_animation(rt_ctx* c) {
         const int rc = open_inf_slots(c);
         if (rc != RT_OK) return rc;
     }
+    lap("slot uploads");
     // one int allocation: ids, then (offsets, list) x 4
     std::vector<int> buf(c->refit_ids);
     auto append = [&](const std::vector<std::vector<int>>& lists, size_t& off_at, size_t& list_at) {
@@ -3683,10 +3756,12 @@ int prepare_animation(rt_ctx* c) {
     buf.insert(buf.end(), c->anim_cls.begin(), c->anim_cls.end());
     const size_t o_pe = buf.size();   // per accelerator prim: its shape's refit entry (-1: none)
     for (size_t p = 0; p < (c->accel_ok ? A.prim_shape.size() : 0); ++p) buf.push_back(which[A.prim_shape[p]]);
+    lap("node lists");
     int rc = ensure_staging(c->anim_maps, c->anim_maps_cap, buf.size());
     if (rc != RT_OK) return rc;
     HIP_TRY(hipMemcpyAsync(c->anim_maps, buf.data(), buf.size() * sizeof(int), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(sync_stream(c));
+    lap("maps upload + sync");
     const int* d = c->anim_maps;
     c->anim = AnimMaps{d,        d + o[0], d + o[1],  d + o[2],  d + o[3], d + o[4], d + o[5], d + o_ids,
                        d + o[6], d + o[7], d + o[8], d + o[9], d + o[10], d + o[11], d + o_cls, d + o_pe,
@@ -3706,9 +3781,12 @@ void set_root(rt_ctx* c) {
 
 // (Re)builds the accelerator after the host copies changed, then the animation lists.
 int upload_accel(rt_ctx* c) {
+    discard_rebuild(c);
+    c->st_suspended = false;
     int rc = sync_host_nodes(c);
     if (rc != RT_OK) return rc;
     rc = build_upload_accel(c);
+    c->shape_moved.assign(c->S, 0);  // built from the current host records
     // the degraded-bound reports of earlier refits concern the accelerator this replaced
     // (prepare_animation alone, when the refit set changes, keeps them: same accelerator)
     for (bool& pend : c->report_pending) pend = false;
@@ -3748,6 +3826,106 @@ bool host_nodes_nest(const rt_ctx* c) {
         st.push_back(nd.rightChild);
     }
     return true;
+}
+
+// Asynchronous rebuild (rt_ctx::AsyncBuild). A running build is joined and dropped
+// by anything that replaces the scene or rebuilds synchronously.
+void discard_rebuild(rt_ctx* c) {
+    if (!c->rebuild) return;
+    if (c->rebuild->th.joinable()) c->rebuild->th.join();
+    c->rebuild.reset();
+}
+
+// Starts the rebuild over a snapshot of the host records (device-grown node boxes
+// fetched first). A rebuild already running is left to finish: the refit that lands it
+// checks the kinds of bound and the nesting again.
+int start_rebuild(rt_ctx* c) {
+    if (c->rebuild) return RT_OK;
+    ++c->anim_rebuilds;
+    const int rc = sync_host_nodes(c);
+    if (rc != RT_OK) return rc;
+    if (c->nodes_rebuild) c->st_suspended = true;  // exact meanwhile: the reference tree only
+    c->nodes_rebuild = false;
+    auto b = std::make_unique<rt_ctx::AsyncBuild>();
+    b->shapes = c->host_shapes;
+    b->nodes = c->host_nodes;
+    rt_ctx::AsyncBuild* raw = b.get();
+    const std::vector<int>* idx = &c->host_idx;  // fixed while the build runs: an upload joins it first
+    const int S = c->S, N = c->N, I = c->I;
+    const bool mt = c->build_mt;
+    raw->th = std::thread([raw, idx, S, N, I, mt] {
+        raw->ok = rta::build_accel(raw->shapes.data(), S, raw->nodes.data(), N, idx->data(), I, kLeafScan, kMaxStack,
+                                   raw->A, mt);
+        raw->done.store(true, std::memory_order_release);
+    });
+    c->rebuild = std::move(b);
+    return RT_OK;
+}
+
+// Swaps a finished rebuild in: its accelerator to the device (the frames in flight end
+// first), then every shape whose record differs from the snapshot, and the animated
+// ones, form the refit set with their snapshot records as the build-time base, so the
+// next refit brings the new accelerator to the current records (the caller's flush).
+int finish_rebuild(rt_ctx* c, bool* refit) {
+    if (!c->rebuild || !c->rebuild->done.load(std::memory_order_acquire)) return RT_OK;
+    std::unique_ptr<rt_ctx::AsyncBuild> b = std::move(c->rebuild);
+    b->th.join();
+    static const bool prof = std::getenv("RT_REBUILD_PROFILE") != nullptr;  // diagnostics: phase times
+    using clk = std::chrono::steady_clock;
+    auto t0 = clk::now();
+    auto lap = [&](const char* what) {
+        if (!prof) return;
+        const auto t = clk::now();
+        std::fprintf(stderr, "finish_rebuild %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
+    int rc = sync_host_nodes(c);
+    if (rc != RT_OK) return rc;
+    HIP_TRY(sync_stream(c));
+    lap("sync");
+    free_accel(c);
+    c->st_suspended = false;
+    for (bool& pend : c->report_pending) pend = false;  // reports about the accelerator replaced
+    ++c->async_swaps;
+    if (!b->ok) {  // as a failed synchronous build: no accelerator (k_packet)
+        c->accel = rta::AccelHost();
+        c->refit_ids.clear();
+        c->anim_base.clear();
+        return prepare_animation(c);
+    }
+    c->accel = std::move(b->A);
+    lap("free");
+    if ((rc = upload_built_accel(c)) != RT_OK) return rc;
+    lap("upload");
+    std::vector<char> in(c->S, 0);
+    std::vector<int> ids;
+    std::vector<FlatShape> base;
+    auto add = [&](int id) {
+        if (in[id]) return;
+        in[id] = 1;
+        ids.push_back(id);
+        base.push_back(b->shapes[id]);
+    };
+    for (int id : c->anim_ids) add(id);
+    c->shape_moved.assign(c->S, 0);
+    for (int id = 0; id < c->S; ++id)
+        if (std::memcmp(&c->host_shapes[id], &b->shapes[id], sizeof(FlatShape)) != 0) {
+            add(id);
+            c->shape_moved[id] = 1;
+        }
+    c->refit_ids.swap(ids);
+    c->anim_base.swap(base);
+    // pending writes stay pending (upd_ids): their shapes are in the set with the snapshot base
+    for (auto& ub : c->upd_base) ub.second = b->shapes[ub.first];
+    // the node records since the snapshot are in every copy already (upload_built_accel read
+    // host_nodes; pending ones stay nodes_dirty); boxes that do not nest (any more) rebuild
+    // again, exact meanwhile
+    c->nodes_rebuild = c->accel_ok && c->accel.st.wroot >= 0 && !host_nodes_nest(c);
+    *refit = !c->refit_ids.empty();
+    lap("refit set");
+    rc = prepare_animation(c);
+    lap("prepare_animation");
+    return rc;
 }
 
 // Reads the report words of earlier refits whose k_refit has run (block: wait for
@@ -3881,10 +4059,13 @@ void compact_refit_set(rt_ctx* c) {
 // operation that reads the device scene.
 int flush_updates(rt_ctx* c, bool grow = false) {
     if (!c->have_scene) return RT_OK;
-    int rc = check_reports(c);
+    bool swapped = false;  // a rebuilt accelerator landed: its refit set is refit now
+    int rc = finish_rebuild(c, &swapped);
+    if (rc != RT_OK) return rc;
+    rc = check_reports(c);
     if (rc != RT_OK) return rc;
     const bool gbox = c->grow_pending && !c->anim_ids.empty();
-    const bool work = !c->upd_ids.empty() || c->nodes_dirty || grow || gbox;
+    const bool work = !c->upd_ids.empty() || c->nodes_dirty || grow || gbox || swapped;
     if (!work && !c->bounds_rebuild) return RT_OK;
     if (work) {
         // shapes new to the refit set join it with their build-time records
@@ -4028,9 +4209,11 @@ int flush_updates(rt_ctx* c, bool grow = false) {
         return RT_OK;
     }
     // a bound changed kind (reported by an earlier k_refit), or the node boxes stopped
-    // nesting: rebuild from the host copies (which the refit above brought to the device)
-    ++c->anim_rebuilds;
+    // nesting: rebuild from the host copies (which the refit above brought to the device),
+    // on a host thread while the frames go on (rt_ctx::AsyncBuild), or here
     c->bounds_rebuild = false;
+    if (c->async_rebuild) return start_rebuild(c);
+    ++c->anim_rebuilds;
     return upload_accel(c);
 }
 
@@ -4479,7 +4662,8 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             k2.heavy_acc = c->heavy_acc;
         }
         // Animated scenes keep the scene tree: rt_animate refits its boxes and items (prepare_animation).
-        const int troot = c->tree_mode == RT_TREE_SCENE ? c->st_root : kNoChild;
+        // (off while a rebuild for node boxes that stopped nesting runs: st_suspended)
+        const int troot = c->tree_mode == RT_TREE_SCENE && !c->st_suspended ? c->st_root : kNoChild;
         // production shape on a dispatch that records no tile work: the counter-free kernel
 
         const AccelPtrs A{c->anodes, c->prims, c->lnodes, c->wnodes, c->tleaf, c->titems, troot,
@@ -4723,6 +4907,7 @@ int rtx::animate_deferred(rt_ctx* c, const FlatShape* shapes) {
     for (int i = 0; i < n; ++i) {
         const int id = c->anim_ids[i];
         c->host_shapes[id] = shapes[i];
+        if (id < static_cast<int>(c->shape_moved.size())) c->shape_moved[id] = 1;
         // the growth of this frame, on the host with the device's operations
         // (reference_box: BoundingBox::growToInclude), unioned with the pending frames'
         float lo[3], hi[3];
@@ -4889,6 +5074,7 @@ int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
             c->upd_ids.push_back(id);
         }
         c->host_shapes[id] = shapes[j];
+        if (id < static_cast<int>(c->shape_moved.size())) c->shape_moved[id] = 1;
     }
     // the sub-contexts hold the same shapes in the same order (brute: under its one
     // leaf; mtc: the MT accelerator): they refit too
@@ -4981,6 +5167,8 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (c->nodes_dirty && (rc = flush_updates(c)) != RT_OK) return rc;
     const int n = static_cast<int>(c->anim_ids.size());
     for (int i = 0; i < n; ++i) c->host_shapes[c->anim_ids[i]] = shapes[i];
+    for (int i = 0; i < n; ++i)
+        if (c->anim_ids[i] < static_cast<int>(c->shape_moved.size())) c->shape_moved[c->anim_ids[i]] = 1;
     // the root's box as k_refit grows it (grow_node: glm::min / max of the listed
     // shapes' growToInclude boxes), for rtx::view_root
     for (int i = 0; i < n; ++i) {
@@ -5281,6 +5469,23 @@ extern "C" int rt_debug_refits(rt_ctx* c) { return c ? c->updates_flushed : -1; 
 // the records). Same device state either way.
 // out[7]: dirty slots, their largest and total prim range, reference nodes listing an
 // entry, refit entries, bytes of the last flush's pinned records, compactions
+// Diagnostics: the rebuild a refit asks for runs on a host thread (1, default) or in that
+// refit's flush (0). rt_debug_rebuild_state: out[0] a rebuild is running, out[1] rebuilds
+// asked for, out[2] rebuilt accelerators swapped in, out[3] the scene tree is suspended.
+extern "C" int rt_debug_async_rebuild(rt_ctx* c, int on) {
+    if (!c) return RT_ERR_INVALID;
+    c->async_rebuild = on ? 1 : 0;
+    return RT_OK;
+}
+extern "C" int rt_debug_rebuild_state(rt_ctx* c, int* out) {
+    if (!c || !out) return RT_ERR_INVALID;
+    out[0] = c->rebuild ? 1 : 0;
+    out[1] = c->anim_rebuilds;
+    out[2] = c->async_swaps;
+    out[3] = c->st_suspended ? 1 : 0;
+    return RT_OK;
+}
+
 extern "C" int rt_debug_refit_stats(rt_ctx* c, long long* out) {
     if (!c || !out) return RT_ERR_INVALID;
     out[0] = c->n_dirty;

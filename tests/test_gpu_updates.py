@@ -447,3 +447,79 @@ def test_refit_set_stays_bounded(ctx, fresh):
     assert ctx.debug_refit_stats()["compactions"] >= 1
     assert worst["entries"] <= bound, worst
     assert worst["flush_bytes"] <= bound * (rtamd.SHAPE_DTYPE.itemsize + 4), worst
+
+
+def _rebuild_state(c):
+    import ctypes as C
+    fn = c._lib.rt_debug_rebuild_state
+    fn.argtypes = [C.c_void_p, C.c_void_p]
+    out = np.zeros(4, np.int32)
+    assert fn(c._h, out.ctypes.data) == 0
+    return dict(zip(["running", "requested", "swapped", "suspended"], out.tolist()))
+
+
+def _async(c, on):
+    import ctypes as C
+    fn = c._lib.rt_debug_async_rebuild
+    fn.argtypes = [C.c_void_p, C.c_int]
+    assert fn(c._h, int(on)) == 0
+
+
+@pytest.mark.parametrize("mode,asy", [("animate", 1), ("reference", 1), ("animate", 0)])
+def test_async_rebuild_keeps_frames_exact(ctx, fresh, mode, asy):
+    """A moved shape whose kind of bound changes (a wheel triangle collapsing to a sliver,
+    then back) and node boxes that stop nesting make the refit ask for an accelerator
+    rebuild. It runs on a host thread over a snapshot of the records while the frames go
+    on; every frame, before, during and after the swap, equals a fresh upload of the same
+    records bit for bit, and the rebuilt accelerator lands (swapped, the scene tree on
+    again). The car's wheels turn every frame (rt_animate, or the reference's own uploads)."""
+    import time
+    W, H = 240, 135
+    fs = rtamd.generate(3, 0, W, H)
+    ids, wheel = bench.wheel_frames(fs, 40)
+    host = rtamd.FlatScene(fs.shapes.copy(), fs.nodes.copy(), fs.indices, fs.camera, fs.light)
+    ctx.upload(fs)
+    ctx.set_params(W, H, 3, True)
+    ctx.set_kernel(rtamd.KERNEL_AUTO)
+    fresh.set_params(W, H, 3, True)
+    _async(ctx, asy)
+    if mode == "animate":
+        ctx.set_animated(ids)
+    else:
+        ru = rtamd.ReferenceUpload(fs, ids)
+    s0 = _rebuild_state(ctx)
+    sliver = 7  # a wheel triangle (index into ids)
+    saw_running, trace = False, []
+    for k in range(40):
+        recs = wheel[k].copy()
+        if 5 <= k < 20:  # collapsed onto its first edge's midpoint: no conservative bound
+            recs["triP3"][sliver] = recs["triP1"][sliver] + (recs["triP2"][sliver] - recs["triP1"][sliver]) * 0.5
+        host.shapes[ids] = recs
+        rtamd.update_bvh(host, ids)
+        if mode == "animate":
+            ctx.animate(recs)
+        else:
+            ru.upload(ctx, recs)
+        if k == 25:  # a leaf box grown out of its parent's: the scene tree cannot hold
+            leaf = int(np.where(host.nodes["leftChild"] == -1)[0][0])
+            host.nodes["boundsMax"][leaf] += np.float32(40.0)
+            if mode == "animate":
+                ctx.update_nodes(host.nodes)
+            else:
+                ru.nodes["boundsMax"][leaf] += np.float32(40.0)
+                ctx.update_nodes(ru.nodes)
+        got = ctx.render(W, H)
+        saw_running = saw_running or bool(_rebuild_state(ctx)["running"])
+        trace.append(_rebuild_state(ctx)["requested"] - s0["requested"])
+        fresh.upload(rtamd.FlatScene(host.shapes, host.nodes, fs.indices, fs.camera, fs.light))
+        same(got, fresh.render(W, H), f"{mode} frame {k} {_rebuild_state(ctx)}")
+    # let the last rebuild land, then one more frame through it
+    t0 = time.time()
+    while _rebuild_state(ctx)["running"] and time.time() - t0 < 30:
+        time.sleep(0.01)
+        got = ctx.render(W, H)
+    same(ctx.render(W, H), fresh.render(W, H), f"{mode} after the swap")
+    st = _rebuild_state(ctx)
+    assert st["requested"] - s0["requested"] >= 2, st  # the sliver (at least) and the nesting
+    assert (st["swapped"] - s0["swapped"] >= 1 or not asy) and not st["running"] and not st["suspended"], st
+    print(f"rebuild {mode} async={asy}: {st}, a rebuild was seen running: {saw_running}, requests by frame {trace}")
