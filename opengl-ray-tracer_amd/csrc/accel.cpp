@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <climits>
 #include <cstdio>
 #include <cmath>
 #include <cstdlib>
@@ -400,6 +401,52 @@ GCone gmerge(const GCone& x, const GCone& y) {
     return GCone{{a[0], a[1], a[2]}, std::max(ang(x.a) + x.theta, ang(ya) + y.theta)};
 }
 
+namespace {
+
+// Host threads for the builds' independent halves (at most 16: the GPU box's CPU
+// share per GPU). 1 on a one-core host; RTA_BUILD_THREADS overrides it (1-64; the
+// accelerator is the same for every count, tests/test_accel_cpu.py).
+int build_threads() {
+    if (const char* e = std::getenv("RTA_BUILD_THREADS")) {
+        const int v = std::atoi(e);
+        if (v >= 1) return std::min(v, 64);
+    }
+    const unsigned h = std::thread::hardware_concurrency();
+    return static_cast<int>(std::max(1u, std::min(16u, h)));
+}
+
+// fn(i0, i1) over [0, n) in contiguous chunks on up to build_threads() threads (the
+// calling one included); chunk c is [c n / T, (c + 1) n / T).
+template <class F>
+void parallel_chunks(int n, int min_per_thread, F fn) {
+    const int T = std::max(1, std::min(build_threads(), n / std::max(1, min_per_thread)));
+    if (T <= 1) {
+        fn(0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    std::vector<std::exception_ptr> err(T);  // rethrown on the calling thread after every join
+    for (int c = 1; c < T; ++c)
+        th.emplace_back([&, c] {
+            try {
+                fn(static_cast<int>(static_cast<long long>(c) * n / T),
+                   static_cast<int>(static_cast<long long>(c + 1) * n / T), c);
+            } catch (...) {
+                err[c] = std::current_exception();
+            }
+        });
+    try {
+        fn(0, static_cast<int>(static_cast<long long>(n) / T), 0);
+    } catch (...) {
+        err[0] = std::current_exception();
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : err)
+        if (e) std::rethrow_exception(e);
+}
+
+}  // namespace
+
 void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
     const size_t M = A.lbox.size();
     A.lcone.assign(4 * M, 0.f);
@@ -501,18 +548,18 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         return agg[j];
     };
     A.lmt.assign(kMtPadF * M, 0.f);
-    for (size_t j = 0; j < M; ++j) {
-        const GCone& c = get(j);
+    auto mt_record = [&](size_t j) {
+        const GCone& c = cones[j];
         float* o = &A.lcone[4 * j];
         o[0] = static_cast<float>(c.a[0]);
         o[1] = static_cast<float>(c.a[1]);
         o[2] = static_cast<float>(c.a[2]);
         o[3] = (c.theta < 0 || c.theta >= 1.5) ? 2.f : static_cast<float>(2.0 * std::sin(0.5 * c.theta + 1e-6) + 2e-5);
-        const Agg& g = aget(j);
+        const Agg& g = agg[j];
         float* m = &A.lmt[kMtPadF * j];
         if (!(g.X > 0)) {  // no triangle below: pad 0, no slab
             m[5] = INFINITY;
-            continue;
+            return;
         }
         const double up = 1.0 + 1e-5;
         m[0] = static_cast<float>(g.cr * (1.0 - 1e-5));
@@ -526,7 +573,16 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
         // (measured in tests/native/accel_check: skipping the slab of wide cones,
         // sin > 0.3, or of nodes thicker along the axis than 1/4 of their box
         // raises the car's node steps per camera ray from 79 to 94)
+    };
+    for (size_t j = 0; j < M; ++j) {  // every node's cone and aggregate first (memoised recursion)
+        get(j);
+        aget(j);
     }
+    // then each node's record on the build threads: its slab walks its own subtree
+    // (read-only), so the nodes are independent
+    parallel_chunks(static_cast<int>(M), 1024, [&](int j0, int j1, int) {
+        for (size_t j = static_cast<size_t>(j0); j < static_cast<size_t>(j1); ++j) mt_record(j);
+    });
 }
 
 void build_cones(const FlatShape* shapes, AccelHost& A) {
@@ -537,6 +593,64 @@ void build_cones(const FlatShape* shapes, AccelHost& A) {
     const size_t M = A.lbox.size();
     A.lcone.assign(4 * M, 0.f);
     std::vector<Cone> cones(M, full_cone());
+    auto store = [&](size_t j) {
+        const Cone& c = cones[j];
+        float* o = &A.lcone[4 * j];
+        const double t = c.theta + kConeMargin;
+        if (c.full() || t >= 1.5707) {
+            o[0] = o[1] = o[2] = 0.f;
+            o[3] = -4.f;
+        } else {
+            o[0] = static_cast<float>(c.a[0]);
+            o[1] = static_cast<float>(c.a[1]);
+            o[2] = static_cast<float>(c.a[2]);
+            o[3] = static_cast<float>(-std::sin(t));
+        }
+    };
+    // The builders number every tree in preorder (a node, its left subtree, then its
+    // right one), so a node's subtree is the index range [j, j + size): subtrees of at
+    // most M / 64 nodes are independent units, each merged children first (descending
+    // index) on the build threads, then the nodes above them. Each node's cone is the
+    // same merge of its children's as in the recursion below (which forests not in
+    // preorder take).
+    std::vector<int> size(M, 1);
+    bool pre = true;
+    for (size_t j = M; j-- > 0 && pre;) {
+        if (A.la[j] < 0) continue;
+        const size_t l = static_cast<size_t>(A.la[j]), r = static_cast<size_t>(A.lb[j] & 0x3fffffff);
+        pre = l == j + 1 && r == l + static_cast<size_t>(size[l]) && r < M;
+        if (pre) size[j] = 1 + size[l] + size[r];
+    }
+    if (pre && M >= 32768) {  // (smaller: threads cost more than they save)
+        auto one = [&](size_t j) {
+            if (A.la[j] < 0) {
+                const int st = -A.la[j] - 1, n = A.lb[j];
+                Cone c = n > 0 ? shape_cone(shapes[A.prim_shape[st]]) : full_cone();
+                for (int i = 1; i < n; ++i) c = merge(c, shape_cone(shapes[A.prim_shape[st + i]]));
+                cones[j] = c;
+            } else {
+                cones[j] = merge(cones[static_cast<size_t>(A.la[j])], cones[static_cast<size_t>(A.lb[j] & 0x3fffffff)]);
+            }
+            store(j);
+        };
+        const size_t unit = std::max<size_t>(64, M / 64);
+        std::vector<std::pair<size_t, size_t>> units;  // [first, end) of each unit subtree
+        std::vector<size_t> top;                      // the nodes above them, ascending
+        for (size_t j = 0; j < M;) {
+            if (static_cast<size_t>(size[j]) <= unit) {
+                units.push_back({j, j + static_cast<size_t>(size[j])});
+                j += static_cast<size_t>(size[j]);
+            } else {
+                top.push_back(j++);
+            }
+        }
+        parallel_chunks(static_cast<int>(units.size()), 4, [&](int u0, int u1, int) {
+            for (int u = u0; u < u1; ++u)
+                for (size_t j = units[u].second; j-- > units[u].first;) one(j);
+        });
+        for (size_t q = top.size(); q-- > 0;) one(top[q]);
+        return;
+    }
     std::vector<char> done(M, 0);
     std::function<const Cone&(size_t)> get = [&](size_t j) -> const Cone& {
         if (done[j]) return cones[j];
@@ -553,18 +667,8 @@ void build_cones(const FlatShape* shapes, AccelHost& A) {
         return cones[j];
     };
     for (size_t j = 0; j < M; ++j) {
-        const Cone& c = get(j);
-        float* o = &A.lcone[4 * j];
-        const double t = c.theta + kConeMargin;
-        if (c.full() || t >= 1.5707) {
-            o[0] = o[1] = o[2] = 0.f;
-            o[3] = -4.f;
-        } else {
-            o[0] = static_cast<float>(c.a[0]);
-            o[1] = static_cast<float>(c.a[1]);
-            o[2] = static_cast<float>(c.a[2]);
-            o[3] = static_cast<float>(-std::sin(t));
-        }
+        get(j);
+        store(j);
     }
 }
 
@@ -589,27 +693,38 @@ int inner_height(const AccelHost& A, int j, std::vector<int>& memo) {
 // the wide id; `pend` = the bound reached.
 int make_wide(AccelHost& A, int j, int budget, std::vector<int>& memo, int& pend) {
     auto inner = [&](int b) { return b >= 0 && A.la[b] >= 0; };
-    std::vector<int> slots{A.la[j], A.lb[j] & 0x3fffffff};
-    auto need = [&](const std::vector<int>& sl) {
+    // at most 2 kWide children: fixed arrays, no allocation per wide node
+    struct Slots {
+        int v[2 * kWide];
+        int n = 0;
+        int size() const { return n; }
+        int& operator[](int i) { return v[i]; }
+        int operator[](int i) const { return v[i]; }
+    };
+    Slots slots;
+    slots.v[slots.n++] = A.la[j];
+    slots.v[slots.n++] = A.lb[j] & 0x3fffffff;
+    auto need = [&](const Slots& sl) {
         int m = 0;
-        for (int b : sl) m = std::max(m, inner_height(A, b, memo));
-        return static_cast<int>(sl.size()) - 1 + m;
+        for (int i = 0; i < sl.n; ++i) m = std::max(m, inner_height(A, sl.v[i], memo));
+        return sl.n - 1 + m;
     };
     const int max_kids = A.mt ? kWide : kWideKids;
+    static_assert(kWideKids <= 2 * kWide, "Slots holds the widest node");
     for (;;) {
-        if (static_cast<int>(slots.size()) >= max_kids) break;
+        if (slots.size() >= max_kids) break;
         int pick = -1;
         float best = -1.f;
-        for (int s2 = 0; s2 < static_cast<int>(slots.size()); ++s2)
+        for (int s2 = 0; s2 < slots.size(); ++s2)
             if (inner(slots[s2]) && area(A.lbox[slots[s2]]) > best) {
                 best = area(A.lbox[slots[s2]]);
                 pick = s2;
             }
         if (pick < 0) break;
-        std::vector<int> next = slots;
+        Slots next = slots;
         const int b = next[pick];
         next[pick] = A.la[b];
-        next.push_back(A.lb[b] & 0x3fffffff);
+        next.v[next.n++] = A.lb[b] & 0x3fffffff;
         if (need(next) > budget) break;  // deeper expansion would exceed the stack budget
         slots = next;
     }
@@ -648,12 +763,6 @@ struct Atom {
     float c[3];
 };
 
-int log2_ceil(int n) {
-    int h = 0;
-    while ((1 << h) < n) ++h;
-    return h;
-}
-
 // Binned SAH over atom centroids (cost = box area x shapes), into T's
 // lbox / la / lb / prim_shape / prim_seq (the layout of a local tree, so the
 // cone and wide-collapse passes apply). A leaf holds atoms of one reference
@@ -665,48 +774,6 @@ int log2_ceil(int n) {
 // Shapes of one reference leaf kept together in one scene-tree item (at most; <= 7
 // for the few-leaf item codes).
 constexpr int kItemMax = RT_ITEM_MAX;
-
-// Host threads for the builds' independent halves (at most 16: the GPU box's CPU
-// share per GPU). 1 on a one-core host; RTA_BUILD_THREADS overrides it (1-64; the
-// accelerator is the same for every count, tests/test_accel_cpu.py).
-int build_threads() {
-    if (const char* e = std::getenv("RTA_BUILD_THREADS")) {
-        const int v = std::atoi(e);
-        if (v >= 1) return std::min(v, 64);
-    }
-    const unsigned h = std::thread::hardware_concurrency();
-    return static_cast<int>(std::max(1u, std::min(16u, h)));
-}
-
-// fn(i0, i1) over [0, n) in contiguous chunks on up to build_threads() threads (the
-// calling one included); chunk c is [c n / T, (c + 1) n / T).
-template <class F>
-void parallel_chunks(int n, int min_per_thread, F fn) {
-    const int T = std::max(1, std::min(build_threads(), n / std::max(1, min_per_thread)));
-    if (T <= 1) {
-        fn(0, n, 0);
-        return;
-    }
-    std::vector<std::thread> th;
-    std::vector<std::exception_ptr> err(T);  // rethrown on the calling thread after every join
-    for (int c = 1; c < T; ++c)
-        th.emplace_back([&, c] {
-            try {
-                fn(static_cast<int>(static_cast<long long>(c) * n / T),
-                   static_cast<int>(static_cast<long long>(c + 1) * n / T), c);
-            } catch (...) {
-                err[c] = std::current_exception();
-            }
-        });
-    try {
-        fn(0, static_cast<int>(static_cast<long long>(n) / T), 0);
-    } catch (...) {
-        err[0] = std::current_exception();
-    }
-    for (auto& t : th) t.join();
-    for (auto& e : err)
-        if (e) std::rethrow_exception(e);
-}
 
 struct SceneBuilder {
     AccelHost& T;
@@ -742,7 +809,8 @@ struct SceneBuilder {
     int leaf(int b, int e) {
         const int k = static_cast<int>(T.lbox.size());
         Box3 box = empty_box();
-        std::vector<std::pair<int, int>> ps;
+        thread_local std::vector<std::pair<int, int>> ps;  // reused: one leaf per atom on config 5
+        ps.clear();
         for (int i = b; i < e; ++i) {
             grow(box, atoms[i].box);
             for (int q = atoms[i].first; q < atoms[i].first + atoms[i].n; ++q) ps.push_back(ap[q]);
@@ -794,6 +862,8 @@ struct SceneBuilder {
         for (int a = 1; a < 3; ++a)
             if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
         const int room = hmax - depth - 1;
+        // a side of x atoms fits below this level (its binary height ceil(log2 x) <= room)
+        const long long fit = room < 0 ? -1 : room >= 62 ? LLONG_MAX : 1LL << room;
         // 256 bins (measured against 32: config 3 -1.4 %, config 2 -2.5 %, config 5 equal;
         // 1024 gains nothing more)
         constexpr int kMaxBins = 256;
@@ -822,18 +892,21 @@ struct SceneBuilder {
                 // bin) is the dense sweep's (scene-tree hashes equal on configs 2, 3, 5,
                 // the 222-strip road and three soups). Config 5's whole accelerator build
                 // (93k atoms): 2.1 s -> 0.36 s on the host.
-                int used[kMaxBins], nu = 0;
+                // the occupied bins in ascending order from a bitmap (no sort)
+                unsigned long long occ[kMaxBins / 64] = {};
                 for (int i = b; i < e; ++i) {
                     const int k = bin_of(atoms[i], ax);
                     if (acnt[k] == 0) {
-                        used[nu++] = k;
+                        occ[k >> 6] |= 1ull << (k & 63);
                         bb[k] = empty_box();
                     }
                     cnt[k] += atoms[i].n;
                     ++acnt[k];
                     grow(bb[k], atoms[i].box);
                 }
-                std::sort(used, used + nu);
+                int used[kMaxBins], nu = 0;
+                for (int w = 0; w < kMaxBins / 64; ++w)
+                    for (unsigned long long m = occ[w]; m; m &= m - 1) used[nu++] = 64 * w + __builtin_ctzll(m);
                 Box3 lacc = empty_box();
                 int lcnt = 0, lat = 0;
                 float lcost[kMaxBins];
@@ -853,7 +926,7 @@ struct SceneBuilder {
                     rcnt += cnt[k];
                     rat += acnt[k];
                     const float c = lcost[j - 1] + (rcnt ? area(racc) * rcnt : 0.f);
-                    if (rat && rat < n && log2_ceil(lats[j - 1]) <= room && log2_ceil(rat) <= room && c < best) {
+                    if (rat && rat < n && c < best && lats[j - 1] <= fit && rat <= fit) {
                         best = c;
                         best_k = k;
                         best_axis = ax;
@@ -887,7 +960,7 @@ struct SceneBuilder {
                 rcnt += cnt[k];
                 rat += acnt[k];
                 const float c = lcost[k - 1] + (rcnt ? area(racc) * rcnt : 0.f);
-                if (rat && rat < n && log2_ceil(lats[k - 1]) <= room && log2_ceil(rat) <= room && c < best) {
+                if (rat && rat < n && c < best && lats[k - 1] <= fit && rat <= fit) {
                     best = c;
                     best_k = k;
                     best_axis = ax;
@@ -1005,47 +1078,69 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
             if (!(b.lo[a] <= b.hi[a])) return inf_box;  // NaN from infinite bounds: no bound at all
         return b;
     };
-    // per-leaf scratch, reused (no allocation per leaf or per atom)
-    std::vector<int> bnd;
-    std::vector<std::pair<int, int>> ub, ps;
-    for (int k = 0; k < N; ++k) {
-        const FlatNode& nd = nodes[k];
-        if (!reach[k] || nd.leftChild != -1) continue;
-        bnd.clear();
-        ub.clear();
-        for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
-            const int si = idx[nd.startShapeIdx + i];
-            if (scls[si] == NEVER) continue;
-            if (scls[si] == UNBOUNDED) ub.push_back({si, seq_base[k] + i});
-            else bnd.push_back(i);
-        }
-        // an atom of n (shape, seq) pairs starting at p
-        auto add = [&](std::vector<Atom>& dst, const std::pair<int, int>* p, int n, const Box3& box) {
-            Atom at{k, static_cast<int>(ap.size()), n, box, {0.f, 0.f, 0.f}};
-            for (int a = 0; a < 3; ++a) at.c[a] = std::isfinite(box.lo[a]) ? 0.5f * (box.lo[a] + box.hi[a]) : 0.f;
-            ap.insert(ap.end(), p, p + n);
-            dst.push_back(at);
-        };
-        if (bnd.size() <= static_cast<size_t>(kItemMax)) {
-            if (!bnd.empty()) {
-                Box3 box = empty_box();
-                ps.clear();
+    // Atoms per reference leaf, in chunks of leaves on the build threads, each into its
+    // own arrays (Atom::first relative to its own ap), then appended in leaf order: the
+    // sequential pass's atoms and ap exactly.
+    std::vector<int> rleaves;
+    for (int k = 0; k < N; ++k)
+        if (reach[k] && nodes[k].leftChild == -1) rleaves.push_back(k);
+    struct Chunk {
+        std::vector<Atom> bounded, unbounded;
+        std::vector<std::pair<int, int>> ap;
+    };
+    std::vector<Chunk> chunks(static_cast<size_t>(std::max(1, build_threads())));
+    parallel_chunks(static_cast<int>(rleaves.size()), 2048, [&](int q0, int q1, int c) {
+        Chunk& C = chunks[c];
+        // per-leaf scratch, reused (no allocation per leaf or per atom)
+        std::vector<int> bnd;
+        std::vector<std::pair<int, int>> ub, ps;
+        for (int q = q0; q < q1; ++q) {
+            const int k = rleaves[q];
+            const FlatNode& nd = nodes[k];
+            bnd.clear();
+            ub.clear();
+            for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
+                const int si = idx[nd.startShapeIdx + i];
+                if (scls[si] == NEVER) continue;
+                if (scls[si] == UNBOUNDED) ub.push_back({si, seq_base[k] + i});
+                else bnd.push_back(i);
+            }
+            // an atom of n (shape, seq) pairs starting at p
+            auto add = [&](std::vector<Atom>& dst, const std::pair<int, int>* p, int n, const Box3& box) {
+                Atom at{k, static_cast<int>(C.ap.size()), n, box, {0.f, 0.f, 0.f}};
+                for (int a = 0; a < 3; ++a) at.c[a] = std::isfinite(box.lo[a]) ? 0.5f * (box.lo[a] + box.hi[a]) : 0.f;
+                C.ap.insert(C.ap.end(), p, p + n);
+                dst.push_back(at);
+            };
+            if (bnd.size() <= static_cast<size_t>(kItemMax)) {
+                if (!bnd.empty()) {
+                    Box3 box = empty_box();
+                    ps.clear();
+                    for (int i : bnd) {
+                        const int si = idx[nd.startShapeIdx + i];
+                        grow(box, sbox[si]);
+                        ps.push_back({si, seq_base[k] + i});
+                    }
+                    add(C.bounded, ps.data(), static_cast<int>(ps.size()), box);
+                }
+            } else {
                 for (int i : bnd) {
                     const int si = idx[nd.startShapeIdx + i];
-                    grow(box, sbox[si]);
-                    ps.push_back({si, seq_base[k] + i});
+                    const std::pair<int, int> one{si, seq_base[k] + i};
+                    add(C.bounded, &one, 1, sbox[si]);
                 }
-                add(sb.atoms, ps.data(), static_cast<int>(ps.size()), box);
             }
-        } else {
-            for (int i : bnd) {
-                const int si = idx[nd.startShapeIdx + i];
-                const std::pair<int, int> one{si, seq_base[k] + i};
-                add(sb.atoms, &one, 1, sbox[si]);
-            }
+            for (size_t q2 = 0; q2 < ub.size(); q2 += 4)
+                add(C.unbounded, ub.data() + q2, static_cast<int>(std::min(ub.size(), q2 + 4) - q2), leaf_pad(nd));
         }
-        for (size_t q = 0; q < ub.size(); q += 4)
-            add(unb, ub.data() + q, static_cast<int>(std::min(ub.size(), q + 4) - q), leaf_pad(nd));
+    });
+    for (Chunk& C : chunks) {
+        const int off = static_cast<int>(ap.size());
+        for (Atom& at : C.bounded) at.first += off;
+        for (Atom& at : C.unbounded) at.first += off;
+        ap.insert(ap.end(), C.ap.begin(), C.ap.end());
+        sb.atoms.insert(sb.atoms.end(), C.bounded.begin(), C.bounded.end());
+        unb.insert(unb.end(), C.unbounded.begin(), C.unbounded.end());
     }
     const int nb = static_cast<int>(sb.atoms.size()), nu = static_cast<int>(unb.size());
     prof("  scene: atoms");
@@ -1148,12 +1243,13 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     // in any order)
     std::vector<float> mag(build_threads(), 0.f);
     parallel_chunks(S, 4096, [&](int i0, int i1, int c) {
+        float m = 0.f;  // one store per chunk: the threads' slots of `mag` share a cache line
         for (int i = i0; i < i1; ++i) {
             scls[i] = classify(shapes[i], sbox[i], 0.0, mt);
             if (scls[i] == BOUNDED)
-                for (int a = 0; a < 3; ++a)
-                    mag[c] = std::max({mag[c], std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
+                for (int a = 0; a < 3; ++a) m = std::max({m, std::fabs(sbox[i].lo[a]), std::fabs(sbox[i].hi[a])});
         }
+        mag[c] = m;
     });
     for (float m : mag) out.scene_mag = std::max(out.scene_mag, m);
     out.origin_lim = static_cast<float>((mt ? kOriginRelMt : kOriginRel) * (out.scene_mag + 1.0));
@@ -1162,6 +1258,7 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     });
     out.shape_cls = scls;
     out.shape_box = sbox;
+    prof("classify");
 
     // Reference walk order (gpu_shader.comp:384-426: pop right first): the
     // rank of each leaf's shapes, and each node's depth (pending stack bound).
@@ -1204,11 +1301,12 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
     std::vector<LeafOut> lo(leaves.size());
     std::vector<char> too_deep(build_threads(), 0);
     parallel_chunks(static_cast<int>(leaves.size()), 256, [&](int q0, int q1, int c) {
+        std::vector<Item> bounded;  // per leaf, reused (moved out only into a local build)
         for (int q = q0; q < q1; ++q) {
             const int k = leaves[q];
             const FlatNode& nd = nodes[k];
             LeafOut& L = lo[q];
-            std::vector<Item> bounded;
+            bounded.clear();
             Box3 content = empty_box();
             bool unb = false;
             for (int i = 0; i < std::max(0, nd.numShapes); ++i) {
@@ -1254,6 +1352,7 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
             }
         }
     });
+    prof("leaf builds");
     for (char t : too_deep)
         if (t) return false;
     int max_stack = 1;

@@ -4,13 +4,14 @@
 
 A shape whose kind of bound changes (an animated triangle squeezed to 1/1000 of its
 height at frame 10, back at frame 30) makes the refit ask for a rebuild. Synchronously the frame
-that asks waits for the whole host build (the car 4.5 ms, config 5 ~65 ms on the GPU
+that asks waits for the whole host build (the car 4.1 ms, config 5 ~42 ms on the GPU
 box); asynchronously the frames go on, exact (the refit enters every box above the
 changed shape), and the rebuilt accelerator lands a few frames later.
 
     python tools/rebuild_stall.py [--config 3|5] [--frames 60]
 Prints one JSON line: per mode the median and max waited frame (ms) and the frames that
-took longer than 4x the median.
+took longer than 4x the median; and the scene swap itself, rt_upload_scene of the
+config's scene into a context that holds it already (host build + device upload, ms).
 """
 import argparse
 import ctypes as C
@@ -47,6 +48,14 @@ else:  # 200 triangles drift (config 5 has no published animation)
             r[f] = (r[f] + np.float32(0.01 * k)).astype(np.float32)
         frames.append(r)
 out = {"config": a.config, "W": W, "H": H, "modes": {}}
+c = rtamd.ComputeShader(0)
+up = []
+for _ in range(5):
+    t0 = time.perf_counter()
+    c.upload(fs)
+    up.append((time.perf_counter() - t0) * 1e3)
+c.close()
+out["upload_ms"] = {"median": float(np.median(up)), "min": float(np.min(up)), "runs": len(up)}
 for asy in (0, 1):
     c = rtamd.ComputeShader(0)
     c.upload(fs)
