@@ -836,7 +836,8 @@ struct SceneBuilder {
         return k;
     }
 
-    static constexpr int kParAtoms = 8192;  // halves smaller than this stay on one thread
+    static constexpr int kParAtoms = 8192;   // halves smaller than this stay on one thread
+    static constexpr int kParAxes = 16384;   // nodes this large sweep their 3 axes on 3 threads
 
     // bounded = false: atoms with infinite boxes, split by count only.
     int build(int b, int e, int depth, bool bounded) {
@@ -881,10 +882,10 @@ struct SceneBuilder {
         // it touched, the dense one clears every bin (not 2 KB zeroed per axis and node:
         // config 5's scene tree has ~45k inner nodes)
         thread_local int cnt[kMaxBins] = {0}, acnt[kMaxBins] = {0};
-        for (int ax = 0; bounded && ax < 3; ++ax) {
+        for (int ax = 0; bounded && n < kBins && ax < 3; ++ax) {
             if (!(chi[ax] - clo[ax] > 0)) continue;
             Box3 bb[kMaxBins];
-            if (n < kBins) {
+            {
                 // Few atoms: only the bins they occupy are set up and swept. Growing by
                 // an empty bin is the identity and every boundary inside a run of empty
                 // bins makes the same partition at the same cost, so the split found
@@ -933,41 +934,81 @@ struct SceneBuilder {
                     }
                 }
                 for (int j = 0; j < nu; ++j) cnt[used[j]] = acnt[used[j]] = 0;
-                continue;
             }
-            for (auto& x : bb) x = empty_box();
-            for (int i = b; i < e; ++i) {
-                const int k = bin_of(atoms[i], ax);
-                cnt[k] += atoms[i].n;
-                ++acnt[k];
-                grow(bb[k], atoms[i].box);
+        }
+        if (bounded && n >= kBins) {
+            // Many atoms: every bin. Each axis's cheapest boundary (the first of equal
+            // costs in sweep order), then the axes in order, a later one only if strictly
+            // cheaper: the sequential sweep's choice. The axes of the largest nodes run on
+            // three threads.
+            float ab[3] = {INFINITY, INFINITY, INFINITY};
+            int ak[3] = {-1, -1, -1};
+            auto dense = [&](int ax) {
+                if (!(chi[ax] - clo[ax] > 0)) return;
+                Box3 bb[kMaxBins];
+                for (auto& x : bb) x = empty_box();
+                for (int i = b; i < e; ++i) {
+                    const int k = bin_of(atoms[i], ax);
+                    cnt[k] += atoms[i].n;
+                    ++acnt[k];
+                    grow(bb[k], atoms[i].box);
+                }
+                Box3 lacc = empty_box();
+                int lcnt = 0, lat = 0;
+                float lcost[kMaxBins];
+                int lats[kMaxBins];
+                for (int k = 0; k < kBins - 1; ++k) {
+                    grow(lacc, bb[k]);
+                    lcnt += cnt[k];
+                    lat += acnt[k];
+                    lcost[k] = lcnt ? area(lacc) * lcnt : 0.f;
+                    lats[k] = lat;
+                }
+                Box3 racc = empty_box();
+                int rcnt = 0, rat = 0;
+                for (int k = kBins - 1; k >= 1; --k) {
+                    grow(racc, bb[k]);
+                    rcnt += cnt[k];
+                    rat += acnt[k];
+                    const float c = lcost[k - 1] + (rcnt ? area(racc) * rcnt : 0.f);
+                    if (rat && rat < n && c < ab[ax] && lats[k - 1] <= fit && rat <= fit) {
+                        ab[ax] = c;
+                        ak[ax] = k;
+                    }
+                }
+                std::fill(cnt, cnt + kBins, 0);  // this thread's counters
+                std::fill(acnt, acnt + kBins, 0);
+            };
+            if (par > 0 && n >= kParAxes) {
+                std::exception_ptr err[2];
+                std::thread t1([&] {
+                    try {
+                        dense(1);
+                    } catch (...) {
+                        err[0] = std::current_exception();
+                    }
+                });
+                std::thread t2([&] {
+                    try {
+                        dense(2);
+                    } catch (...) {
+                        err[1] = std::current_exception();
+                    }
+                });
+                dense(0);
+                t1.join();
+                t2.join();
+                for (auto& x : err)
+                    if (x) std::rethrow_exception(x);
+            } else {
+                for (int ax = 0; ax < 3; ++ax) dense(ax);
             }
-            Box3 lacc = empty_box();
-            int lcnt = 0, lat = 0;
-            float lcost[kMaxBins];
-            int lats[kMaxBins];
-            for (int k = 0; k < kBins - 1; ++k) {
-                grow(lacc, bb[k]);
-                lcnt += cnt[k];
-                lat += acnt[k];
-                lcost[k] = lcnt ? area(lacc) * lcnt : 0.f;
-                lats[k] = lat;
-            }
-            Box3 racc = empty_box();
-            int rcnt = 0, rat = 0;
-            for (int k = kBins - 1; k >= 1; --k) {
-                grow(racc, bb[k]);
-                rcnt += cnt[k];
-                rat += acnt[k];
-                const float c = lcost[k - 1] + (rcnt ? area(racc) * rcnt : 0.f);
-                if (rat && rat < n && c < best && lats[k - 1] <= fit && rat <= fit) {
-                    best = c;
-                    best_k = k;
+            for (int ax = 0; ax < 3; ++ax)
+                if (ak[ax] >= 0 && ab[ax] < best) {
+                    best = ab[ax];
+                    best_k = ak[ax];
                     best_axis = ax;
                 }
-            }
-            std::fill(cnt, cnt + kBins, 0);
-            std::fill(acnt, acnt + kBins, 0);
         }
         int mid = b;
         if (best_k > 0) {
@@ -1185,23 +1226,24 @@ static void build_scene_tree(const FlatShape* shapes, const FlatNode* nodes, int
     const int P0 = static_cast<int>(out.prim_shape.size());
     out.prim_shape.insert(out.prim_shape.end(), T.prim_shape.begin(), T.prim_shape.end());
     out.prim_seq.insert(out.prim_seq.end(), T.prim_seq.begin(), T.prim_seq.end());
-    st.box = T.lbox;
-    st.a = T.la;
-    st.b = T.lb;
-    st.item_of.assign(T.lbox.size(), -1);
-    for (size_t j = 0; j < T.lbox.size(); ++j) {
-        if (T.la[j] >= 0) continue;
-        const int start = -T.la[j] - 1 + P0;
+    // T's arrays move into st (T ends here)
+    st.box = std::move(T.lbox);
+    st.a = std::move(T.la);
+    st.b = std::move(T.lb);
+    st.item_of.assign(st.box.size(), -1);
+    for (size_t j = 0; j < st.box.size(); ++j) {
+        if (st.a[j] >= 0) continue;
+        const int start = -st.a[j] - 1 + P0;
         st.a[j] = -(start + 1);
         st.item_of[j] = static_cast<int>(st.item_ref.size());
         st.item_ref.push_back(sb.leaf_ref[j]);
         st.item_start.push_back(start);
-        st.item_count.push_back(T.lb[j]);
+        st.item_count.push_back(st.b[j]);
     }
-    st.wchild = T.wchild;
-    st.wsub = T.wsub;
-    st.wpair = T.wpair;
-    out.st_cone = T.lcone;
+    st.wchild = std::move(T.wchild);
+    st.wsub = std::move(T.wsub);
+    st.wpair = std::move(T.wpair);
+    out.st_cone = std::move(T.lcone);
 }
 
 // Wide collapse of every local tree within the lane stack budget `cap`;
@@ -1222,6 +1264,10 @@ static int build_wide(AccelHost& A, const std::vector<int>& ref_depth, int cap) 
         need = std::max(need, ref_depth[k] + pend + 2);
     }
     return need;
+}
+
+void parallel_for(int n, int min_per_thread, const std::function<void(int, int)>& fn) {
+    parallel_chunks(n, min_per_thread, [&](int i0, int i1, int) { fn(i0, i1); });
 }
 
 bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, const int* idx, int I,

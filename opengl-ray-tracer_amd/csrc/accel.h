@@ -23,6 +23,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "../../include/rt_flat.h"
@@ -124,6 +125,11 @@ bool build_accel(const FlatShape* shapes, int S, const FlatNode* nodes, int N, c
 
 // Back-face cones of the local nodes (fills A.lcone; grazing cones when A.mt).
 void build_cones(const FlatShape* shapes, AccelHost& A);
+
+// fn(i0, i1) over [0, n) in contiguous chunks on the build threads (RTA_BUILD_THREADS,
+// at most 16), each of at least min_per_thread items; the calling thread takes the
+// first chunk. Exceptions reach the caller after every chunk ended.
+void parallel_for(int n, int min_per_thread, const std::function<void(int, int)>& fn);
 
 constexpr int kWide = 4;  // children per wide record (one 128-byte record of the barycentric accelerator)
 // Children per wide node of the barycentric accelerators: 8 = two consecutive records

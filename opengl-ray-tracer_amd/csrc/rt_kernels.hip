@@ -3194,47 +3194,85 @@ inline float bits_f(int v) {
 // Builds the accelerator from the host copies of the scene and uploads it;
 // expects geo_lin to be packed (k_pack_prims copies from it). On failure the
 // context keeps rendering with k_packet.
+// Diagnostics (RT_REBUILD_PROFILE set): wall time of the phases of a host step on
+// stderr, each lap since the previous one.
+struct PhaseLaps {
+    const char* step;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    explicit PhaseLaps(const char* s) : step(s) {}
+    void operator()(const char* what) {
+        static const bool on = std::getenv("RT_REBUILD_PROFILE") != nullptr;
+        if (!on) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "%s %-24s %8.3f ms\n", step, what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    }
+};
+
+// A host array left uninitialised: no serial zeroing pass, its pages are first touched
+// by the threads that fill it (config 5's 24 MB of wnodes: 5.4 ms of page faults on one
+// thread). Every element is written before the array is read.
+template <class T>
+struct RawArray {
+    std::unique_ptr<T[]> p;
+    size_t n;
+    explicit RawArray(size_t count) : p(new T[count]), n(count) {}
+    T* data() { return p.get(); }
+    size_t size() const { return n; }
+    T& operator[](size_t i) { return p[i]; }
+};
+
 int upload_built_accel(rt_ctx* c);
 int build_upload_accel(rt_ctx* c) {
+    PhaseLaps lap("build_upload_accel");
     free_accel(c);
     const int N = c->N;
     if (N == 0) return RT_OK;
+    lap("free");
     if (!rta::build_accel(c->host_shapes.data(), c->S, c->host_nodes.data(), N, c->host_idx.data(), c->I,
                           kLeafScan, kMaxStack, c->accel, c->build_mt))
         return RT_OK;
+    lap("host build");
     return upload_built_accel(c);
 }
 
 // The device half of build_upload_accel: c->accel (built) to the device, with the
 // current host node records' exact boxes and the device's current shape records.
 int upload_built_accel(rt_ctx* c) {
+    PhaseLaps lap("  upload");
     const int N = c->N;
     rta::AccelHost& A = c->accel;
     if (N >= (1 << 28)) return RT_OK;  // codes carry the node index in 28 bits
-    c->boxes_finite = 1;
-    for (int k = 0; k < N; ++k) {
-        const FlatNode& n = c->host_nodes[k];
-        for (float v : {n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, n.boundsMax.x, n.boundsMax.y, n.boundsMax.z})
-            if (std::isnan(v)) c->boxes_finite = 0;
-    }
+    // The arrays below are packed on the build threads (rta::parallel_for): each entry is
+    // written by one thread from read-only inputs.
+    constexpr int kPackChunk = 8192;
     // anodes: every reference node's exact box and content box (the root's entry test).
-    std::vector<float4> an(4 * static_cast<size_t>(N));
-    for (int k = 0; k < N; ++k) {
-        const FlatNode& n = c->host_nodes[k];
-        const rta::Box3& cb = A.content[k];
-        an[4 * k + 0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(n.leftChild));
-        an[4 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(n.rightChild));
-        an[4 * k + 2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[k]));
-        an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
-    }
+    RawArray<float4> an(4 * static_cast<size_t>(N));
+    std::atomic<int> nan_box{0};
+    rta::parallel_for(N, kPackChunk, [&](int k0, int k1) {
+        int nan = 0;
+        for (int k = k0; k < k1; ++k) {
+            const FlatNode& n = c->host_nodes[k];
+            for (float v : {n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, n.boundsMax.x, n.boundsMax.y, n.boundsMax.z})
+                nan |= std::isnan(v) ? 1 : 0;
+            const rta::Box3& cb = A.content[k];
+            an[4 * k + 0] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(n.leftChild));
+            an[4 * k + 1] = make_float4(n.boundsMax.x, n.boundsMax.y, n.boundsMax.z, bits_f(n.rightChild));
+            an[4 * k + 2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[k]));
+            an[4 * k + 3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
+        }
+        if (nan) nan_box.store(1);
+    });
+    c->boxes_finite = nan_box.load() ? 0 : 1;
+    lap("anodes");
     // lnodes: the wide local nodes (accel.h, build_wide), kWideRec float4 each with
     // quantized cones (kWideRecMt with the MT accelerator's float grazing cones; wide_kids).
     const size_t P = A.prim_shape.size();
     const int rec = A.mt ? kWideRecMt : kWideRec;
-    bool codes_ok = true;
+    std::atomic<bool> codes_ok{true};
     auto leaf_code = [&](size_t j) -> int {
         const unsigned st = static_cast<unsigned>(-A.la[j] - 1), cnt = static_cast<unsigned>(A.lb[j]);
-        if (st >= (1u << 22) || cnt > 63u) codes_ok = false;
+        if (st >= (1u << 22) || cnt > 63u) codes_ok.store(false);
         return static_cast<int>(kLocal | kLeaf | (st << 6) | cnt);
     };
     // The scene tree's wide nodes (accel.h, SceneTree) follow the local ones;
@@ -3284,9 +3322,14 @@ int upload_built_accel(rt_ctx* c) {
         }
         for (int r = 0; r < rec; ++r) ln[rec * at + r] = make_float4(v[r][0], v[r][1], v[r][2], v[r][3]);
     };
-    for (size_t w = 0; w < nw; ++w)
-        emit_wide(w, w, A.wchild, A.wsub, A.wpair, A.lbox, A.lcone,
-                  [&](int j) { return leaf_code(static_cast<size_t>(j)); }, 0);
+    {
+        const std::function<int(int)> leaf_of = [&](int j) { return leaf_code(static_cast<size_t>(j)); };
+        rta::parallel_for(static_cast<int>(nw), kPackChunk, [&](int w0, int w1) {
+            for (size_t w = static_cast<size_t>(w0); w < static_cast<size_t>(w1); ++w)
+                emit_wide(w, w, A.wchild, A.wsub, A.wpair, A.lbox, A.lcone, leaf_of, 0);
+        });
+    }
+    lap("local wide nodes");
     // Items: with <= 8 distinct reference leaves (few-leaf mode, few_mask) a
     // local-leaf code kLocal|kLeaf|kItem|start<<6|leaf<<3|count and titems =
     // the leaves' exact boxes; otherwise kTopLeaf|kItem|item and titems = per
@@ -3312,8 +3355,11 @@ int upload_built_accel(rt_ctx* c) {
     };
     std::vector<float4> ti(2 * (use_st ? std::max<size_t>(T.item_ref.size(), 1) : 1));
     if (use_st) {
-        for (size_t w = 0; w < nws; ++w)
-            emit_wide(w, nw + w, T.wchild, T.wsub, T.wpair, T.box, A.st_cone, item_code, nw);
+        const std::function<int(int)> item_of = item_code;
+        rta::parallel_for(static_cast<int>(nws), kPackChunk, [&](int w0, int w1) {
+            for (size_t w = static_cast<size_t>(w0); w < static_cast<size_t>(w1); ++w)
+                emit_wide(w, nw + w, T.wchild, T.wsub, T.wpair, T.box, A.st_cone, item_of, nw);
+        });
         auto put = [&](size_t i, int ref, int start, int count) {
             const FlatNode& n = c->host_nodes[ref];
             ti[2 * i] = make_float4(n.boundsMin.x, n.boundsMin.y, n.boundsMin.z, bits_f(start));
@@ -3329,34 +3375,40 @@ int upload_built_accel(rt_ctx* c) {
         c->n_titems = static_cast<int>(refs.size());
         c->host_titem_ref = refs;
     }
+    lap("scene tree nodes, items");
     // wnodes: per reference inner node both children's exact + content boxes;
     // tleaf: per reference leaf its plain range and local root code.
-    std::vector<float4> wn(8 * static_cast<size_t>(N));
-    std::vector<int4> tl(static_cast<size_t>(N), make_int4(0, 0, kNoChild, 0));
+    RawArray<float4> wn(8 * static_cast<size_t>(N));
+    RawArray<int4> tl(static_cast<size_t>(N));
     auto top_code_of = [&](int k) {
         return c->host_nodes[k].leftChild == -1 ? static_cast<int>(kTopLeaf | static_cast<unsigned>(k)) : k;
     };
-    for (int k = 0; k < N; ++k) {
-        const FlatNode& n = c->host_nodes[k];
-        if (n.leftChild == -1) {
-            const int r = A.local_root[k];
-            const int lr = A.wroot[k] >= 0 ? wide_code(A.wpair, A.wroot[k], 0)
-                                           : (r >= 0 ? leaf_code(static_cast<size_t>(r)) : kNoChild);
-            tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr, 0);
-            continue;
+    rta::parallel_for(N, kPackChunk, [&](int k0, int k1) {
+        for (int k = k0; k < k1; ++k) {
+            const FlatNode& n = c->host_nodes[k];
+            if (n.leftChild == -1) {
+                const int r = A.local_root[k];
+                const int lr = A.wroot[k] >= 0 ? wide_code(A.wpair, A.wroot[k], 0)
+                                               : (r >= 0 ? leaf_code(static_cast<size_t>(r)) : kNoChild);
+                tl[k] = make_int4(A.plain_start[k], A.plain_count[k], lr, 0);
+                for (int q = 0; q < 8; ++q) wn[8 * static_cast<size_t>(k) + q] = make_float4(0.f, 0.f, 0.f, 0.f);
+                continue;
+            }
+            tl[k] = make_int4(0, 0, kNoChild, 0);
+            const int ch[2] = {n.leftChild, n.rightChild};
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const FlatNode& cn = c->host_nodes[ch[s2]];
+                const rta::Box3& cb = A.content[ch[s2]];
+                float4* q = &wn[8 * static_cast<size_t>(k) + 4 * s2];
+                q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, s2 == 0 ? bits_f(top_code_of(ch[0])) : 0.f);
+                q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, s2 == 0 ? bits_f(top_code_of(ch[1])) : 0.f);
+                q[2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[ch[s2]] & 8));
+                q[3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
+            }
         }
-        const int ch[2] = {n.leftChild, n.rightChild};
-        for (int s2 = 0; s2 < 2; ++s2) {
-            const FlatNode& cn = c->host_nodes[ch[s2]];
-            const rta::Box3& cb = A.content[ch[s2]];
-            float4* q = &wn[8 * static_cast<size_t>(k) + 4 * s2];
-            q[0] = make_float4(cn.boundsMin.x, cn.boundsMin.y, cn.boundsMin.z, s2 == 0 ? bits_f(top_code_of(ch[0])) : 0.f);
-            q[1] = make_float4(cn.boundsMax.x, cn.boundsMax.y, cn.boundsMax.z, s2 == 0 ? bits_f(top_code_of(ch[1])) : 0.f);
-            q[2] = make_float4(cb.lo[0], cb.lo[1], cb.lo[2], bits_f(A.flags[ch[s2]] & 8));
-            q[3] = make_float4(cb.hi[0], cb.hi[1], cb.hi[2], 0.f);
-        }
-    }
-    if (!codes_ok) return RT_OK;
+    });
+    lap("wnodes, tleaf");
+    if (!codes_ok.load()) return RT_OK;
     for (size_t i = 0; i < P; ++i)  // PrimRec::st = seq << 2 | type
         if (A.prim_seq[i] < 0 || A.prim_seq[i] >= (1 << 29)) return RT_OK;
     std::vector<int> ps(2 * (P ? P : 1));
@@ -3364,6 +3416,7 @@ int upload_built_accel(rt_ctx* c) {
         ps[i] = A.prim_shape[i];
         ps[P + i] = A.prim_seq[i];
     }
+    lap("prim lists");
     if (hipMalloc(&c->anodes, an.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->lnodes, ln.size() * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->wnodes, wn.size() * sizeof(float4)) != hipSuccess ||
@@ -3372,6 +3425,7 @@ int upload_built_accel(rt_ctx* c) {
         hipMalloc(&c->prims, 4 * (P ? P : 1) * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->prim_idx_dev, ps.size() * sizeof(int)) != hipSuccess)
         return RT_ERR_NO_MEMORY;
+    lap("hipMalloc");
     HIP_TRY(hipMemcpyAsync(c->anodes, an.data(), an.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->lnodes, ln.data(), ln.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->wnodes, wn.data(), wn.size() * sizeof(float4), hipMemcpyHostToDevice, c->stream));
@@ -3382,7 +3436,9 @@ int upload_built_accel(rt_ctx* c) {
         hipLaunchKernelGGL(k_pack_prims, dim3((P + 255) / 256), dim3(256), 0, c->stream, c->geo_lin, c->prim_idx_dev,
                            c->prim_idx_dev + P, static_cast<int>(P), c->prims);
     HIP_TRY(hipGetLastError());
+    lap("copies issued");
     HIP_TRY(sync_stream(c));  // the host vectors die here
+    lap("copies + pack done");
     c->st_root = use_st ? wide_code(T.wpair, T.wroot, nw) : kNoChild;
     c->accel_ok = true;
     c->record_bytes = (an.size() + ln.size() + wn.size() + tl.size() + ti.size() + 4 * P + 2 * static_cast<size_t>(c->S)) *
@@ -3435,14 +3491,7 @@ int open_inf_slots(rt_ctx* c) {
 // anim_base holds, per entry, the record the accelerator's bounds and cones were
 // built from.
 int prepare_animation(rt_ctx* c) {
-    static const bool prof = std::getenv("RT_REBUILD_PROFILE") != nullptr;  // diagnostics: phase times
-    auto t0 = std::chrono::steady_clock::now();
-    auto lap = [&](const char* what) {
-        if (!prof) return;
-        const auto t = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "  prepare %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
-        t0 = t;
-    };
+    PhaseLaps lap("  prepare");
     const int n = static_cast<int>(c->refit_ids.size());
     c->anim = AnimMaps{};
     c->n_direct_slot_reads = 0;
@@ -3870,15 +3919,7 @@ int finish_rebuild(rt_ctx* c, bool* refit) {
     if (!c->rebuild || !c->rebuild->done.load(std::memory_order_acquire)) return RT_OK;
     std::unique_ptr<rt_ctx::AsyncBuild> b = std::move(c->rebuild);
     b->th.join();
-    static const bool prof = std::getenv("RT_REBUILD_PROFILE") != nullptr;  // diagnostics: phase times
-    using clk = std::chrono::steady_clock;
-    auto t0 = clk::now();
-    auto lap = [&](const char* what) {
-        if (!prof) return;
-        const auto t = clk::now();
-        std::fprintf(stderr, "finish_rebuild %-22s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
-        t0 = t;
-    };
+    PhaseLaps lap("finish_rebuild");
     int rc = sync_host_nodes(c);
     if (rc != RT_OK) return rc;
     HIP_TRY(sync_stream(c));
@@ -5013,8 +5054,10 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     int rc = check_tree(nodes, N, idx, I, S, &ms);
     if (rc != RT_OK) return rc;
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    PhaseLaps lap("rt_upload_scene");
     HIP_TRY(sync_stream(c));
     free_scene(c);
+    lap("free");
     const size_t sS = S > 0 ? S : 1, sI = I > 0 ? I : 1, sN = N > 0 ? N : 1;
     if (hipMalloc(&c->geo_lin, sS * 5 * sizeof(float4)) != hipSuccess ||
         hipMalloc(&c->geo_leaf, sI * 5 * sizeof(float4)) != hipSuccess ||
@@ -5055,7 +5098,10 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     c->upd_mark.assign(S, 0);
     c->nodes_dirty = c->nodes_rebuild = c->bounds_rebuild = false;
     c->brute_stale = c->mtc_stale = true;
-    return upload_accel(c);
+    lap("records");
+    rc = upload_accel(c);
+    lap("accelerator");
+    return rc;
 }
 
 int rt_update_shapes(rt_ctx* c, int first, int count, const FlatShape* shapes) {
