@@ -67,7 +67,7 @@ for asy in (0, 1):
     fn(c._h, asy)
     c.set_animated(ids)
     buf = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
-    ms = []
+    ms, parts = [], []  # parts: animate, dispatch, sync (ms)
     for k in range(a.frames):
         recs = frames[k].copy()
         if 10 <= k < 30:  # squeezed towards its first edge: too thin to bound, still a triangle
@@ -77,9 +77,13 @@ for asy in (0, 1):
         c.set_camera(fs.camera)
         c.set_light(fs.light)
         c.animate(recs)
+        t1 = time.perf_counter()
         c.dispatch_rows(W, H, 0, 1, 1, H, buf.data_ptr(), W * 16)
+        t2 = time.perf_counter()
         c.sync()
-        ms.append((time.perf_counter() - t0) * 1e3)
+        t3 = time.perf_counter()
+        ms.append((t3 - t0) * 1e3)
+        parts.append((round((t1 - t0) * 1e3, 3), round((t2 - t1) * 1e3, 3), round((t3 - t2) * 1e3, 3)))
     st = np.zeros(4, np.int32)
     g = c._lib.rt_debug_rebuild_state
     g.argtypes = [C.c_void_p, C.c_void_p]
@@ -88,6 +92,8 @@ for asy in (0, 1):
     out["modes"]["async" if asy else "sync"] = {
         "median_ms": med, "max_ms": float(np.max(ms)),
         "slow_frames": {int(i): round(float(v), 3) for i, v in enumerate(ms) if v > 4 * med},
+        "slow_frame_parts_animate_dispatch_sync": {int(i): parts[i] for i, v in enumerate(ms) if v > 4 * med},
+        "median_parts": [float(np.median([p[j] for p in parts])) for j in range(3)],
         "rebuilds_started": int(st[1]), "swapped": int(st[2])}
     c.close()
 print(json.dumps(out))
