@@ -472,20 +472,41 @@ void build_cones_mt(const FlatShape* shapes, AccelHost& A) {
     // Per-ray padding (accel_bound.h, MtTri; accel_math.h mt_pad): the cone's
     // s = 2 sin(theta/2) bounds |n - axis| for every normal below, so
     // |cos(d, n)| >= |d . axis| - s; the node constants take the worst triangle.
-    double zlo[3] = {INFINITY, INFINITY, INFINITY}, zhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    // per prim its MT constants, on the build threads (min/max per chunk, exact in any order)
+    const int np = static_cast<int>(A.prim_shape.size());
     std::vector<MtTri> tri(A.prim_shape.size());
     std::vector<char> has(A.prim_shape.size(), 0);
-    for (size_t p = 0; p < A.prim_shape.size(); ++p) {
-        const FlatShape& s = shapes[A.prim_shape[p]];
-        Box3 b;
-        if (s.type != RT_TRIANGLE || classify_mt_tight(s, b, 0.0, tri[p]) != BOUNDED) continue;
-        has[p] = 1;
-        if (tri[p].X > kMtBigX) continue;  // Z: the centre of the bulk, not of a large ground quad
+    const int nt = build_threads();
+    std::vector<double> zr(6 * static_cast<size_t>(nt));
+    for (int c = 0; c < nt; ++c)
         for (int a = 0; a < 3; ++a) {
-            zlo[a] = std::min(zlo[a], tri[p].p1[a]);
-            zhi[a] = std::max(zhi[a], tri[p].p1[a]);
+            zr[6 * c + a] = INFINITY;
+            zr[6 * c + 3 + a] = -INFINITY;
         }
-    }
+    parallel_chunks(np, 4096, [&](int p0, int p1, int c) {
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int p = p0; p < p1; ++p) {
+            const FlatShape& s = shapes[A.prim_shape[p]];
+            Box3 b;
+            if (s.type != RT_TRIANGLE || classify_mt_tight(s, b, 0.0, tri[p]) != BOUNDED) continue;
+            has[p] = 1;
+            if (tri[p].X > kMtBigX) continue;  // Z: the centre of the bulk, not of a large ground quad
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], tri[p].p1[a]);
+                hi[a] = std::max(hi[a], tri[p].p1[a]);
+            }
+        }
+        for (int a = 0; a < 3; ++a) {
+            zr[6 * c + a] = lo[a];
+            zr[6 * c + 3 + a] = hi[a];
+        }
+    });
+    double zlo[3] = {INFINITY, INFINITY, INFINITY}, zhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int c = 0; c < nt; ++c)
+        for (int a = 0; a < 3; ++a) {
+            zlo[a] = std::min(zlo[a], zr[6 * c + a]);
+            zhi[a] = std::max(zhi[a], zr[6 * c + 3 + a]);
+        }
     for (int a = 0; a < 3; ++a) A.mt_z[a] = std::isfinite(zlo[a]) ? static_cast<float>(0.5 * (zlo[a] + zhi[a])) : 0.f;
     struct Agg {
         double cr = INFINITY, X = 0, esum = 0, m = 0;

@@ -3044,6 +3044,11 @@ struct rt_ctx {
         std::vector<FlatNode> nodes;
     };
     std::unique_ptr<AsyncBuild> rebuild;
+    // The last swapped-in build's object, kept for the next rebuild: its snapshot buffers
+    // are refilled in place, and its A (the replaced accelerator's host arrays) is
+    // released by the next build on its thread -- freeing ~30-100 MB at the swap took
+    // 5-11 ms of the frame on config 5 (munmap).
+    std::unique_ptr<AsyncBuild> spare;
     int async_rebuild = 1;
     bool st_suspended = false;          // the scene tree is off until the rebuild lands
     int async_swaps = 0;                // rebuilt accelerators swapped in (diagnostics)
@@ -3202,7 +3207,7 @@ struct PhaseLaps {
     explicit PhaseLaps(const char* s) : step(s) {}
     void operator()(const char* what) {
         static const bool on = std::getenv("RT_REBUILD_PROFILE") != nullptr;
-        if (!on) return;
+        if (!on || !step) return;  // (a null step: this instance reports nothing)
         const auto t = std::chrono::steady_clock::now();
         std::fprintf(stderr, "%s %-24s %8.3f ms\n", step, what, std::chrono::duration<double, std::milli>(t - t0).count());
         t0 = t;
@@ -3895,9 +3900,11 @@ int start_rebuild(rt_ctx* c) {
     if (rc != RT_OK) return rc;
     if (c->nodes_rebuild) c->st_suspended = true;  // exact meanwhile: the reference tree only
     c->nodes_rebuild = false;
-    auto b = std::make_unique<rt_ctx::AsyncBuild>();
-    b->shapes = c->host_shapes;
-    b->nodes = c->host_nodes;
+    std::unique_ptr<rt_ctx::AsyncBuild> b = c->spare ? std::move(c->spare) : std::make_unique<rt_ctx::AsyncBuild>();
+    b->done.store(false);
+    b->ok = false;
+    b->shapes.assign(c->host_shapes.begin(), c->host_shapes.end());  // into the spare's capacity
+    b->nodes.assign(c->host_nodes.begin(), c->host_nodes.end());
     rt_ctx::AsyncBuild* raw = b.get();
     const std::vector<int>* idx = &c->host_idx;  // fixed while the build runs: an upload joins it first
     const int S = c->S, N = c->N, I = c->I;
@@ -3917,9 +3924,10 @@ int start_rebuild(rt_ctx* c) {
 // next refit brings the new accelerator to the current records (the caller's flush).
 int finish_rebuild(rt_ctx* c, bool* refit) {
     if (!c->rebuild || !c->rebuild->done.load(std::memory_order_acquire)) return RT_OK;
+    PhaseLaps lap("finish_rebuild");
     std::unique_ptr<rt_ctx::AsyncBuild> b = std::move(c->rebuild);
     b->th.join();
-    PhaseLaps lap("finish_rebuild");
+    lap("join");
     int rc = sync_host_nodes(c);
     if (rc != RT_OK) return rc;
     HIP_TRY(sync_stream(c));
@@ -3928,13 +3936,15 @@ int finish_rebuild(rt_ctx* c, bool* refit) {
     c->st_suspended = false;
     for (bool& pend : c->report_pending) pend = false;  // reports about the accelerator replaced
     ++c->async_swaps;
+    // the replaced accelerator's host arrays go to b->A, freed by the next build's thread
+    std::swap(c->accel, b->A);
     if (!b->ok) {  // as a failed synchronous build: no accelerator (k_packet)
         c->accel = rta::AccelHost();
         c->refit_ids.clear();
         c->anim_base.clear();
+        c->spare = std::move(b);
         return prepare_animation(c);
     }
-    c->accel = std::move(b->A);
     lap("free");
     if ((rc = upload_built_accel(c)) != RT_OK) return rc;
     lap("upload");
@@ -3966,6 +3976,7 @@ int finish_rebuild(rt_ctx* c, bool* refit) {
     lap("refit set");
     rc = prepare_animation(c);
     lap("prepare_animation");
+    c->spare = std::move(b);  // reused by the next rebuild (not freed here)
     return rc;
 }
 
@@ -4103,8 +4114,10 @@ int flush_updates(rt_ctx* c, bool grow = false) {
     bool swapped = false;  // a rebuilt accelerator landed: its refit set is refit now
     int rc = finish_rebuild(c, &swapped);
     if (rc != RT_OK) return rc;
+    PhaseLaps lap(swapped ? "flush after swap" : nullptr);
     rc = check_reports(c);
     if (rc != RT_OK) return rc;
+    lap("check_reports");
     const bool gbox = c->grow_pending && !c->anim_ids.empty();
     const bool work = !c->upd_ids.empty() || c->nodes_dirty || grow || gbox || swapped;
     if (!work && !c->bounds_rebuild) return RT_OK;
@@ -4120,6 +4133,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             }
         if (added) compact_refit_set(c);
         if (added && (rc = prepare_animation(c)) != RT_OK) return rc;
+        lap("refit set joined");
         const int n = static_cast<int>(c->refit_ids.size());
         const bool nodes = c->nodes_dirty && c->N > 0;
         const size_t rec_bytes = static_cast<size_t>(n) * (sizeof(FlatShape) + sizeof(int));
@@ -4132,6 +4146,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             const char* pin_dev = nullptr;
             const int slot = pinned_slot(c, bytes, &pin, &pin_dev);
             if (slot < 0) return slot;
+            lap("pinned slot");
             for (int i = 0; i < n; ++i)
                 std::memcpy(pin + i * sizeof(FlatShape), &c->host_shapes[c->refit_ids[i]], sizeof(FlatShape));
             int* flags = reinterpret_cast<int*>(pin + n * sizeof(FlatShape));
@@ -4224,6 +4239,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             } else if ((rc = go(r, waves)) != RT_OK) {
                 return rc;
             }
+            lap("records staged, k_refit launched");
             // the slot may be refilled once its event (recorded behind the next dispatch) is done
             if ((rc = record_mark(c)) != RT_OK) return rc;
             c->mark_slot = slot;
@@ -4244,6 +4260,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
         for (int id : c->upd_ids) c->upd_mark[id] = 0;
         c->upd_ids.clear();
         c->upd_base.clear();
+        lap("flush end");
     }
     if (!c->nodes_rebuild && !c->bounds_rebuild) {
         ++c->updates_flushed;
@@ -5203,6 +5220,7 @@ int rt_set_animated(rt_ctx* c, const int* ids, int count) {
 
 int rt_animate(rt_ctx* c, const FlatShape* shapes) {
     if (!c || !c->have_scene || c->anim_ids.empty() || !shapes) return RT_ERR_INVALID;
+    PhaseLaps lap(c->rebuild && c->rebuild->done.load() ? "rt_animate (swap)" : nullptr);
     if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
     int rc = RT_OK;
     if (c->grow_pending) {  // deferred frames pending (rtx::animate_deferred): this one joins them
@@ -5232,9 +5250,12 @@ int rt_animate(rt_ctx* c, const FlatShape* shapes) {
             if (rt_update_shapes(c->brute, c->anim_ids[i], 1, &shapes[i]) != RT_OK) c->brute_stale = true;
     // the MT context: the same frame, its nodes grown the same way (its set follows c's)
     if (c->mtc && !c->mtc_stale && rt_animate(c->mtc, shapes) != RT_OK) c->mtc_stale = true;
+    lap("host records");
     // the records and the growth on the device (one k_refit launch); a host rebuild
     // only after a bound changed kind
-    return flush_updates(c, true);
+    rc = flush_updates(c, true);
+    lap("flush");
+    return rc;
 }
 
 int rt_build_lbvh(rt_ctx* c, float* device_ms) {

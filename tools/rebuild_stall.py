@@ -32,6 +32,7 @@ import rtamd  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", type=int, default=3)
 ap.add_argument("--frames", type=int, default=60)
+ap.add_argument("--kernel-times", action="store_true", help="also each frame's render-kernel device ms (HIP events)")
 a = ap.parse_args()
 cfg, W, H, mb, _, _ = bench.WORKLOADS[a.config]
 fs = rtamd.generate(cfg, 0, W, H)
@@ -60,7 +61,7 @@ for asy in (0, 1):
     c = rtamd.ComputeShader(0)
     c.upload(fs)
     c.set_params(W, H, mb, True)
-    c.set_kernel_timing(False)
+    c.set_kernel_timing(a.kernel_times)
     c.set_latency_mode(1)
     fn = c._lib.rt_debug_async_rebuild
     fn.argtypes = [C.c_void_p, C.c_int]
@@ -83,7 +84,8 @@ for asy in (0, 1):
         c.sync()
         t3 = time.perf_counter()
         ms.append((t3 - t0) * 1e3)
-        parts.append((round((t1 - t0) * 1e3, 3), round((t2 - t1) * 1e3, 3), round((t3 - t2) * 1e3, 3)))
+        parts.append((round((t1 - t0) * 1e3, 3), round((t2 - t1) * 1e3, 3), round((t3 - t2) * 1e3, 3))
+                     + ((round(float(c.last_kernel_ms()), 3),) if a.kernel_times else ()))
     st = np.zeros(4, np.int32)
     g = c._lib.rt_debug_rebuild_state
     g.argtypes = [C.c_void_p, C.c_void_p]
@@ -92,8 +94,9 @@ for asy in (0, 1):
     out["modes"]["async" if asy else "sync"] = {
         "median_ms": med, "max_ms": float(np.max(ms)),
         "slow_frames": {int(i): round(float(v), 3) for i, v in enumerate(ms) if v > 4 * med},
-        "slow_frame_parts_animate_dispatch_sync": {int(i): parts[i] for i, v in enumerate(ms) if v > 4 * med},
-        "median_parts": [float(np.median([p[j] for p in parts])) for j in range(3)],
+        "slow_frame_parts_animate_dispatch_sync_kernel": {int(i): parts[i] for i, v in enumerate(ms) if v > 4 * med},
+        "median_parts": [float(np.median([p[j] for p in parts])) for j in range(len(parts[0]))],
+        "frames_parts": parts if a.kernel_times else None,
         "rebuilds_started": int(st[1]), "swapped": int(st[2])}
     c.close()
 print(json.dumps(out))
