@@ -45,17 +45,18 @@ def _p(a):
 
 @pytest.mark.parametrize("cfg", [2, 3, 5])
 def test_threaded_build_is_the_sequential_one(check_lib, cfg, monkeypatch):
-    """The host build runs the scene tree's SAH halves, the shape classification and the
-    per-leaf local builds on several threads, each into its own arrays appended in the
-    sequential order: every field of the accelerator (FNV hash) is the same with 1, 3 and
-    8 threads, for the barycentric and the Moller-Trumbore builds."""
+    """The host build runs the scene tree's SAH halves (and the axis sweeps of its largest
+    nodes), the shape classification, the per-leaf local builds, the scene tree's atoms and
+    cones and the MT constants on several threads, each into its own arrays appended in the
+    sequential order: every field of the accelerator (FNV hash) is the same with 1, 3, 8
+    and 16 threads, for the barycentric and the Moller-Trumbore builds."""
     fs = rtamd.generate(cfg, 0, 320, 180)
     fs = rtamd.FlatScene(fs.shapes, fs.nodes, fs.indices, fs.camera, fs.light)
     check_lib.accel_hash.restype = C.c_ulonglong
     check_lib.accel_hash.argtypes = [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int]
     for mt in (0, 1):
         hashes = []
-        for t in ("1", "3", "8"):
+        for t in ("1", "3", "8", "16"):
             monkeypatch.setenv("RTA_BUILD_THREADS", t)
             hashes.append(check_lib.accel_hash(_p(fs.shapes), len(fs.shapes), _p(fs.nodes), len(fs.nodes),
                                                _p(fs.indices), len(fs.indices), mt))
