@@ -3913,8 +3913,13 @@ int start_rebuild(rt_ctx* c) {
     const int S = c->S, N = c->N, I = c->I;
     const bool mt = c->build_mt;
     raw->th = std::thread([raw, idx, S, N, I, mt] {
-        raw->ok = rta::build_accel(raw->shapes.data(), S, raw->nodes.data(), N, idx->data(), I, kLeafScan, kMaxStack,
-                                   raw->A, mt);
+        try {  // (bad_alloc: swapped in as a failed build, no accelerator; never past the thread)
+            raw->ok = rta::build_accel(raw->shapes.data(), S, raw->nodes.data(), N, idx->data(), I, kLeafScan,
+                                       kMaxStack, raw->A, mt);
+        } catch (...) {
+            raw->A = rta::AccelHost();
+            raw->ok = false;
+        }
         raw->done.store(true, std::memory_order_release);
     });
     c->rebuild = std::move(b);
@@ -5093,8 +5098,13 @@ int rt_upload_scene(rt_ctx* c, const FlatShape* shapes, int S, const FlatNode* n
     std::thread builder;
     if (overlap)
         builder = std::thread([c, S, N, I, &built] {
-            built = rta::build_accel(c->host_shapes.data(), S, c->host_nodes.data(), N, c->host_idx.data(), I, kLeafScan,
-                                     kMaxStack, c->accel, c->build_mt);
+            try {  // (bad_alloc: no accelerator, as a failed build; never past the thread)
+                built = rta::build_accel(c->host_shapes.data(), S, c->host_nodes.data(), N, c->host_idx.data(), I,
+                                         kLeafScan, kMaxStack, c->accel, c->build_mt);
+            } catch (...) {
+                c->accel = rta::AccelHost();
+                built = false;
+            }
         });
     const auto records = [&]() -> int {
         const size_t sS = S > 0 ? S : 1, sI = I > 0 ? I : 1, sN = N > 0 ? N : 1;
