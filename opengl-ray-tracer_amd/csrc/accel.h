@@ -111,9 +111,10 @@ struct AccelHost {
     // centre Z the origin distance |o - Z| is measured from.
     std::vector<float> lmt;
     float mt_z[3] = {0.f, 0.f, 0.f};
-    // Per shape, its class and conservative box (classify with origin_lim) as built: the
-    // refit's fixed slot boxes reuse them for shapes not moved since (rt_kernels.hip
-    // prepare_animation; classifying 100k shapes again took ~40 ms of a config-5 refit setup).
+    // Per shape, its class and conservative box (classify with origin_lim) as built, then
+    // as prepare_animation last classified it (shapes written since the build): the refit's
+    // fixed slot boxes reuse them (rt_kernels.hip prepare_animation; classifying 100k
+    // shapes again took ~40 ms of a config-5 refit setup).
     std::vector<int> shape_cls;
     std::vector<Box3> shape_box;
 };

@@ -3064,8 +3064,9 @@ struct rt_ctx {
     // (lo xyz, hi xyz), applied by the next flush as that shape's growth (AF_BOX)
     std::vector<float> grow_box;
     bool grow_pending = false;
-    // per shape: its host record may differ from the one the accelerator was built from
-    // (prepare_animation then classifies it again instead of reusing AccelHost::shape_box)
+    // per shape: its host record may differ from the one AccelHost::shape_cls / shape_box
+    // were classified from (the build's, or prepare_animation's since): prepare_animation
+    // then classifies it again and caches the result there
     std::vector<char> shape_moved;
     // The brute-force branch (useBVH = 0, gpu_shader.comp:523-620) tests every shape in
     // index order, keeps the strict-< first minimum and stops shadows at the first
@@ -3667,6 +3668,9 @@ int prepare_animation(rt_ctx* c) {
         }
     lap("scene tree maps");
         std::vector<float4> pb(2 * (P ? P : 1), make_float4(INFINITY, INFINITY, INFINITY, 0.f));
+        // per shape its class and box as last classified (the build's, or here for shapes
+        // written since: a host rewriting a different 1 % of config 5 every frame had
+        // every shape it ever wrote classified again at each change of the set, 11 ms)
         const bool cached = A.shape_cls.size() == static_cast<size_t>(c->S) && c->shape_moved.size() == A.shape_cls.size();
         for (size_t p = 0; p < P; ++p) {
             rta::Box3 b;
@@ -3677,6 +3681,11 @@ int prepare_animation(rt_ctx* c) {
                 b = A.shape_box[sh];
             } else {
                 cls = rta::classify(c->host_shapes[sh], b, A.origin_lim, A.mt);
+                if (cached) {
+                    c->accel.shape_cls[sh] = cls;
+                    c->accel.shape_box[sh] = b;
+                    c->shape_moved[sh] = 0;
+                }
             }
             if (cls != rta::BOUNDED) {
                 pb[2 * p + 1] = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.f);
