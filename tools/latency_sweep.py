@@ -82,6 +82,11 @@ SETTINGS = {
     "h81x32": {"heavy": (81, 32)},
     "h324x8": {"heavy": (324, 8)},
     "h324x16": {"heavy": (324, 16)},
+    # Sweep 11 (r06): config 5's waited frame with ray compaction (rt_set_tail) off or from
+    # another bounce (auto: on from bounce 2 for scenes of >= 8,192 scene-tree items)
+    "tail_off": {"tail": 0},
+    "tail1": {"tail": 1},
+    "tail3": {"tail": 3},
 }
 
 
@@ -109,6 +114,7 @@ def main():
         c.debug_lane_k(*s.get("lane_k", (-1, 2)))
         c.debug_cost_time(s.get("cost_time", -1))
         c.set_latency_mode(s.get("latency", 1))
+        c.set_tail(s.get("tail", -1))
 
     def frame():
         c.set_camera(fs.camera)
