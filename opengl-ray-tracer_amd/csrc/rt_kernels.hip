@@ -2854,6 +2854,15 @@ struct rt_ctx {
     bool own_stream = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;      // used once the ring is full
     hipEvent_t sync_ev = nullptr;                  // rt_sync's poll target
+    // The cost order's kernels (k_cost_dilate, k_tile_order) on a second stream behind the
+    // render's end event (rt_debug_order_stream; 0: on this stream, 1: latency-mode
+    // dispatches, 2: all), so that a waited frame ends with its render; the next accelerated
+    // dispatch waits for order_done (join_order), anything that frees or reads the order's
+    // buffers on the host synchronizes order_stream first (sync_order).
+    hipStream_t order_stream = nullptr;
+    hipEvent_t order_ready = nullptr, order_done = nullptr;
+    bool order_pending = false;  // order_done not yet waited for on `stream`
+    int order_mode = 0;
     hipEvent_t last0 = nullptr, last1 = nullptr;  // events of the latest dispatch
     bool timed = false;
     // per-dispatch event pairs since the last rt_kernel_times call
@@ -4009,11 +4018,32 @@ void stream_drained(rt_ctx* c) {
 // hipStreamSynchronize of the context's stream, which also retires its refit slots
 // (and its sub-contexts', which run on the same stream).
 hipError_t sync_stream(rt_ctx* c) {
-    const hipError_t e = hipStreamSynchronize(c->stream);
+    hipError_t e = hipStreamSynchronize(c->stream);
+    for (rt_ctx* x : {c, c->brute, c->mtc})
+        if (e == hipSuccess && x && x->order_stream) {
+            e = hipStreamSynchronize(x->order_stream);
+            if (e == hipSuccess) x->order_pending = false;
+        }
     if (e == hipSuccess)
         for (rt_ctx* x : {c, c->brute, c->mtc})
             if (x) stream_drained(x);
     return e;
+}
+
+// The host is about to free or reuse the cost order's buffers: the order stream's kernels end first.
+hipError_t sync_order(rt_ctx* c) {
+    if (!c->order_stream) return hipSuccess;
+    const hipError_t e = hipStreamSynchronize(c->order_stream);
+    if (e == hipSuccess) c->order_pending = false;
+    return e;
+}
+
+// The next accelerated dispatch reads the order the order stream wrote: the context's
+// stream waits for it (a device-side wait, the host does not block).
+hipError_t join_order(rt_ctx* c) {
+    if (!c->order_pending) return hipSuccess;
+    c->order_pending = false;
+    return hipStreamWaitEvent(c->stream, c->order_done, 0);
 }
 
 // Records the anim_copied event of the last k_refit's slot if it is still pending.
@@ -4391,6 +4421,7 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->moving_period = c->moving_period;
     b->moving_dilate = c->moving_dilate;
     b->moving_split = c->moving_split;
+    b->order_mode = c->order_mode;
     b->refit_mode = c->refit_mode;
     b->tail_from = c->tail_from;
     b->tail_max_lanes = c->tail_max_lanes;
@@ -4543,6 +4574,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
         hipLaunchKernelGGL(k_lane<false>, grid, dim3(kBlock), lds, c->stream, c->geo_leaf, c->geo_lin, c->mat,
                            c->nodes, kp);
     } else if (kind == RT_KERNEL_ACCEL) {
+        HIP_TRY(join_order(c));  // the previous cost frame's order, if it ran on the order stream
         KParams k2 = kp;
         k2.tiles_x = (kp.width + 7) / 8;
         k2.tiles = k2.tiles_x * ((kp.out_rows + 7) / 8);
@@ -4585,6 +4617,7 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             k2.tile_order = c->tile_order;
         } else if (c->schedule != RT_SCHED_ROWS) {
             if (c->sched_cap < k2.tiles) {
+                HIP_TRY(sync_order(c));
                 hipFree(c->sched_cost);
                 hipFree(c->sched_order);
                 hipFree(c->sched_sets);
@@ -4842,24 +4875,43 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             unsigned* next = c->sched_sets + (1 - c->sched_parity) * sched_set_words(c->sched_cap);
             const int groups = (k2.tiles + kOrderThreads - 1) / kOrderThreads;
             const unsigned* cost = c->sched_cost;
+            // the order stream (rt_debug_order_stream): behind the render's end, off the frame's end
+            const bool side = c->order_mode == 2 || (c->order_mode == 1 && latency);
+            hipStream_t os = c->stream;
+            if (side) {
+                if (!c->order_stream) {
+                    if (rtx::make_stream(&c->order_stream, false) != hipSuccess ||
+                        hipEventCreateWithFlags(&c->order_ready, hipEventDisableTiming) != hipSuccess ||
+                        hipEventCreateWithFlags(&c->order_done, hipEventDisableTiming) != hipSuccess)
+                        return RT_ERR_DEVICE;
+                }
+                HIP_TRY(hipEventRecord(c->order_ready, c->stream));
+                HIP_TRY(hipStreamWaitEvent(c->order_stream, c->order_ready, 0));
+                os = c->order_stream;
+            }
             if (dilate > 0) {
                 const size_t need = static_cast<size_t>(k2.tiles) + static_cast<size_t>(groups) * kOrderBuckets;
                 if (c->dil_cap < need) {
+                    HIP_TRY(sync_order(c));
                     hipFree(c->dil_cost);
                     c->dil_cost = nullptr;
                     c->dil_cap = 0;
                     if (hipMalloc(&c->dil_cost, need * sizeof(unsigned)) != hipSuccess) return RT_ERR_NO_MEMORY;
                     c->dil_cap = need;
                 }
-                hipLaunchKernelGGL(k_cost_dilate, dim3(groups), dim3(kOrderThreads), 0, c->stream, c->sched_cost,
+                hipLaunchKernelGGL(k_cost_dilate, dim3(groups), dim3(kOrderThreads), 0, os, c->sched_cost,
                                    k2.tiles, k2.tiles_x, dilate, c->dil_cost, c->dil_cost + k2.tiles);
                 cost = c->dil_cost;
                 set = c->dil_cost + k2.tiles;
             }
             hipLaunchKernelGGL(k_tile_order, dim3(groups), dim3(kOrderThreads),
-                               0, c->stream, cost, k2.tiles, set, next,
+                               0, os, cost, k2.tiles, set, next,
                                static_cast<int>(sched_set_words(c->sched_cap)), c->sched_order,
                                c->schedule == RT_SCHED_COST_XCD ? 1 : 0);
+            if (side) {
+                HIP_TRY(hipEventRecord(c->order_done, os));
+                c->order_pending = true;
+            }
             c->sched_parity = 1 - c->sched_parity;
             c->sched_valid = k2.tiles;
         }
@@ -5053,6 +5105,9 @@ int rt_destroy(rt_ctx* c) {
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
     if (c->sync_ev) hipEventDestroy(c->sync_ev);
+    if (c->order_ready) hipEventDestroy(c->order_ready);
+    if (c->order_done) hipEventDestroy(c->order_done);
+    if (c->order_stream) hipStreamDestroy(c->order_stream);
     if (c->ev0) hipEventDestroy(c->ev0);
     if (c->ev1) hipEventDestroy(c->ev1);
     if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
@@ -5672,6 +5727,14 @@ extern "C" int rt_debug_moving(rt_ctx* c, int period, int dilate, int split) {
     c->moving_period = period;
     c->moving_dilate = dilate;
     c->moving_split = split ? 1 : 0;
+    return RT_OK;
+}
+
+// Diagnostics / policy: where the cost order's kernels run (0: the context's stream after
+// the render; 1: an order stream in latency-mode dispatches; 2: the order stream always).
+extern "C" int rt_debug_order_stream(rt_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 2) return RT_ERR_INVALID;
+    c->order_mode = mode;
     return RT_OK;
 }
 

@@ -820,6 +820,13 @@ class ComputeShader:
         fn.argtypes = [_P, _I, _I, _I]
         self._chk(fn(self._h, int(period), int(dilate), int(split)), "rt_debug_moving")
 
+    def debug_order_stream(self, mode):
+        """Where the cost order's kernels run: 0 the context's stream after the render,
+        1 an order stream in latency-mode dispatches, 2 the order stream always."""
+        fn = self._lib.rt_debug_order_stream
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(mode)), "rt_debug_order_stream")
+
     def debug_cost_dilate(self, r):
         """Cost order over each tile's largest cost within r tiles (0: off)."""
         fn = self._lib.rt_debug_cost_dilate

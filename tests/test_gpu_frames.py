@@ -719,11 +719,15 @@ def test_group_refuses_members_changed_behind_its_back(ctx):
         g.close()
 
 
-def test_moving_camera_cost_order_exact(ctx):
+@pytest.mark.parametrize("order_stream", [0, 1, 2])
+def test_moving_camera_cost_order_exact(ctx, order_stream):
     """Latency mode with a camera that moves every frame: each dispatch re-derives the
     cost order from its tiles' whole wall times dilated by one tile (k_cost_dilate, then
     k_tile_order) for the next. Every frame equals the row-major frame of its own camera,
-    and a still camera after the moves (the still policy again) too."""
+    and a still camera after the moves (the still policy again) too. With the order's
+    kernels on the order stream (rt_debug_order_stream 1, 2) the next dispatch waits for
+    them on the device; mode 2 also with 12 frames in flight between waits (a torn order
+    would leave NaN tiles of the poisoned surfaces, or draw a tile twice)."""
     import bench
     W, H = 320, 180
     cfg, _, _, mb, _, target = bench.WORKLOADS[3]
@@ -741,7 +745,20 @@ def test_moving_camera_cost_order_exact(ctx):
             refs.append(ctx.render(W, H))
         ctx.set_schedule(rtamd.SCHED_COST)
         ctx.set_latency_mode(1)
+        ctx.debug_order_stream(order_stream)
         full = torch.empty((H, W, 4), dtype=torch.float32, device="cuda")
+        if order_stream == 2:
+            ctx.debug_sched_period(1)  # every dispatch a cost frame: its order on the order stream
+            outs = torch.full((12, H, W, 4), float("nan"), dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
+            for k in range(12):
+                ctx.set_camera(cams[k % len(cams)])
+                ctx.dispatch_rows(W, H, 0, 1, 1, H, outs[k].data_ptr(), W * 16)
+            ctx.sync()
+            got = outs.cpu().numpy()
+            for k in range(12):
+                assert np.array_equal(got[k], refs[k % len(cams)]), f"in flight frame {k}"
+            ctx.debug_sched_period(16)
         for rnd in range(3):
             for i, cam in enumerate(cams):
                 ctx.set_camera(cam)
@@ -756,6 +773,7 @@ def test_moving_camera_cost_order_exact(ctx):
             ctx.sync()
             assert np.array_equal(full.cpu().numpy(), refs[-1])
     finally:
+        ctx.debug_order_stream(0)
         ctx.set_latency_mode(0)
         ctx.set_schedule(rtamd.SCHED_COST)
         ctx.set_kernel(rtamd.KERNEL_AUTO)
