@@ -198,6 +198,14 @@ int rt_dispatch_rows_ex(struct rt_ctx* ctx, int width, int height, int y0, int s
 /* glMemoryBarrier + wait: blocks until the context's stream is drained. */
 int rt_sync(struct rt_ctx* ctx);
 
+/* The wait of the reference's render loop (src/main.cpp:290-462: dispatch, barrier, draw,
+ * swap): blocks until the last dispatch's frame is complete -- its image and every upload
+ * issued before it. Scheduling work the renderer queued behind the frame for the next one
+ * (a latency-mode cost frame's tile order) may still be running; the next dispatch on the
+ * same stream runs after it. Work the host enqueued after that dispatch is not waited for
+ * (use rt_sync); when there is no such frame marker it is rt_sync. */
+int rt_sync_frame(struct rt_ctx* ctx);
+
 /* Read the context surface back to host memory: `height` rows of `pitch` bytes.
  * width/height state the destination's size and must equal the surface's (the
  * last rt_dispatch's W x H), so a short buffer is refused, never overrun. */

@@ -11,7 +11,7 @@
  * frame into dst (a device surface, pitch bytes per row), camera cams[i %
  * ncams] for frame i.
  *
- * wait_each != 0: every frame is waited for (rt_sync) before the next starts,
+ * wait_each != 0: every frame is waited for (rt_sync_frame) before the next starts,
  * and frame_ms[i] is frame i's host wall time from its camera upload to the
  * host seeing its end. wait_each == 0: the frames are issued back to back on
  * the context's stream and frame_ms[0] is the wall time of all of them up to

@@ -97,7 +97,7 @@ int render_loop(rt_ctx* ctx, const FlatCamera* cams, int ncams, const FlatLight*
             rc = rows ? rt_dispatch_rows_ex(ctx, width, height, rows->y0, rows->stripe, rows->period, rows->out_rows,
                                             dst, pitch, rows->format)
                       : rt_dispatch_rows(ctx, width, height, 0, 1, 1, height, dst, pitch);
-        if (rc == RT_OK && wait_each) rc = rt_sync(ctx);                                       // the frame's end
+        if (rc == RT_OK && wait_each) rc = rt_sync_frame(ctx);                                 // the frame's end
         if (rc != RT_OK) return rc;
         if (wait_each) frame_ms[i] = std::chrono::duration<double, std::milli>(clk::now() - t0).count();
     }

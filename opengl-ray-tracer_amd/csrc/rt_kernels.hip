@@ -2863,6 +2863,14 @@ struct rt_ctx {
     hipEvent_t order_ready = nullptr, order_done = nullptr;
     bool order_pending = false;  // order_done not yet waited for on `stream`
     int order_mode = 0;
+    // rt_sync_frame: a latency-mode cost frame records frame_ev between its render and the
+    // order's kernels (same stream), and the waited frame ends there (rt_debug_frame_event)
+    int frame_event = 1;
+    hipEvent_t frame_ev = nullptr;
+    bool frame_ev_set = false;         // this context's last launch recorded frame_ev
+    rt_ctx* frame_from = nullptr;      // the context whose launch rendered the last dispatch
+    unsigned long long refit_launches = 0;  // k_refit launches so far
+    unsigned long long frame_refits = 0;    // those of this context + sub-contexts at that dispatch
     hipEvent_t last0 = nullptr, last1 = nullptr;  // events of the latest dispatch
     bool timed = false;
     // per-dispatch event pairs since the last rt_kernel_times call
@@ -4291,6 +4299,7 @@ int flush_updates(rt_ctx* c, bool grow = false) {
             if ((rc = record_mark(c)) != RT_OK) return rc;
             c->mark_slot = slot;
             c->slot_busy[slot] = true;
+            ++c->refit_launches;  // rt_sync_frame: a slot taken since the frame's dispatch
             c->report_pending[slot] = n > 0 && acc;
             if (nodes && (rc = open_inf_slots(c)) != RT_OK) return rc;
         }
@@ -4422,6 +4431,7 @@ void inherit(rt_ctx* b, const rt_ctx* c) {
     b->moving_dilate = c->moving_dilate;
     b->moving_split = c->moving_split;
     b->order_mode = c->order_mode;
+    b->frame_event = c->frame_event;
     b->refit_mode = c->refit_mode;
     b->tail_from = c->tail_from;
     b->tail_max_lanes = c->tail_max_lanes;
@@ -4503,7 +4513,26 @@ rt_ctx* mt_ctx(rt_ctx* c, const KParams& kp) {
 // rt_dispatch_rows' render: through `brute` (useBVH = 0) and / or `mtc`
 // (Moller-Trumbore) when they apply and their accelerator can take the frame,
 // timed by this context's events (rt_kernel_times) like any other dispatch.
+unsigned long long refit_launches(const rt_ctx* c, int depth = 0) {
+    if (!c) return 0;
+    unsigned long long n = c->refit_launches;
+    if (depth < 2) n += refit_launches(c->brute, depth + 1) + refit_launches(c->mtc, depth + 1);
+    return n;
+}
+
+int render_frame(rt_ctx* c, const KParams& kp, rt_ctx** from);
+
+// rt_dispatch_rows' render (render_frame), remembering for rt_sync_frame which context's
+// launch drew it and the refit launches so far
 int render(rt_ctx* c, const KParams& kp) {
+    rt_ctx* from = nullptr;
+    const int rc = render_frame(c, kp, &from);
+    c->frame_from = rc == RT_OK ? from : nullptr;
+    c->frame_refits = refit_launches(c);
+    return rc;
+}
+
+int render_frame(rt_ctx* c, const KParams& kp, rt_ctx** from) {
     // this context's own pending writes first, also when a sub-context renders the frame
     if (const int rc = flush_updates(c)) return rc;
     rt_ctx* t = c;
@@ -4523,7 +4552,11 @@ int render(rt_ctx* c, const KParams& kp) {
         t = nxt;
         kt = kn;
     }
-    if (t == c || !accel_usable(t, kt)) return launch(c, kp, false);
+    if (t == c || !accel_usable(t, kt)) {
+        *from = c;
+        return launch(c, kp, false);
+    }
+    *from = t;
     t->timing = false;  // the sub-context's own events would not be read: this context's time it
     if (!c->timing) {
         const int rc = launch(t, kt, false);
@@ -4550,6 +4583,7 @@ int render(rt_ctx* c, const KParams& kp) {
 }
 
 int launch(rt_ctx* c, const KParams& kp, bool stats) {
+    c->frame_ev_set = false;
     if (const int rc = flush_updates(c)) return rc;  // rt_update_shapes / rt_update_nodes since the last dispatch
     if (kp.out_rows == 0) return RT_OK;
     dim3 grid((kp.width + kTileW - 1) / kTileW, (kp.out_rows + kTileH - 1) / kTileH);
@@ -4878,6 +4912,14 @@ int launch(rt_ctx* c, const KParams& kp, bool stats) {
             // the order stream (rt_debug_order_stream): behind the render's end, off the frame's end
             const bool side = c->order_mode == 2 || (c->order_mode == 1 && latency);
             hipStream_t os = c->stream;
+            if (!side && latency && c->frame_event) {
+                // a waited frame ends here (rt_sync_frame); the order runs behind it on the same
+                // stream, within the host's turnaround to the next dispatch
+                if (!c->frame_ev && hipEventCreateWithFlags(&c->frame_ev, hipEventDisableTiming) != hipSuccess)
+                    return RT_ERR_DEVICE;
+                HIP_TRY(hipEventRecord(c->frame_ev, c->stream));
+                c->frame_ev_set = true;
+            }
             if (side) {
                 if (!c->order_stream) {
                     if (rtx::make_stream(&c->order_stream, false) != hipSuccess ||
@@ -5105,6 +5147,7 @@ int rt_destroy(rt_ctx* c) {
     for (hipEvent_t e : c->ring0) if (e) hipEventDestroy(e);
     for (hipEvent_t e : c->ring1) if (e) hipEventDestroy(e);
     if (c->sync_ev) hipEventDestroy(c->sync_ev);
+    if (c->frame_ev) hipEventDestroy(c->frame_ev);
     if (c->order_ready) hipEventDestroy(c->order_ready);
     if (c->order_done) hipEventDestroy(c->order_done);
     if (c->order_stream) hipStreamDestroy(c->order_stream);
@@ -5516,6 +5559,30 @@ int rt_sync(rt_ctx* c) {
     return RT_OK;
 }
 
+int rt_sync_frame(rt_ctx* c) {
+    if (!c) return RT_ERR_INVALID;
+    // The last dispatch's frame ended at frame_ev if its launch recorded one (a latency-mode
+    // cost frame, before the cost order's kernels) and no refit slot was taken since;
+    // otherwise (and for work enqueued after the dispatch) the whole stream, as rt_sync.
+    rt_ctx* t = c->frame_from;
+    const bool known = t && (t == c || t == c->brute || t == c->mtc || (c->brute && t == c->brute->mtc) ||
+                             (c->mtc && t == c->mtc->brute));
+    if (!known || !t->frame_ev_set || !t->frame_ev || refit_launches(c) != c->frame_refits) return rt_sync(c);
+    if (set_dev(c) != RT_OK) return RT_ERR_DEVICE;
+    const hipEvent_t ev = t->frame_ev;
+    const rtg::WaitResult w = rtg::wait_bounded(
+        [ev] {
+            const hipError_t e = hipEventQuery(ev);
+            return e == hipSuccess ? 0 : (e == hipErrorNotReady ? 1 : -1);
+        },
+        [] { return false; }, 0.0);
+    if (w != rtg::kWaitDone) return RT_ERR_DEVICE;
+    // every refit slot in use was taken before the frame's render (none since): free
+    for (rt_ctx* x : {c, c->brute, c->mtc})
+        if (x) stream_drained(x);
+    return RT_OK;
+}
+
 int rt_read_image(rt_ctx* c, float* dst, size_t pitch, int width, int height) {
     if (!c || !dst || !c->img || width != c->img_w || height != c->img_h ||
         pitch < static_cast<size_t>(c->img_w) * 16)
@@ -5735,6 +5802,13 @@ extern "C" int rt_debug_moving(rt_ctx* c, int period, int dilate, int split) {
 extern "C" int rt_debug_order_stream(rt_ctx* c, int mode) {
     if (!c || mode < 0 || mode > 2) return RT_ERR_INVALID;
     c->order_mode = mode;
+    return RT_OK;
+}
+
+// Diagnostics / policy: latency-mode cost frames record the event rt_sync_frame waits for (1, default) or not (0).
+extern "C" int rt_debug_frame_event(rt_ctx* c, int on) {
+    if (!c || on < 0 || on > 1) return RT_ERR_INVALID;
+    c->frame_event = on;
     return RT_OK;
 }
 

@@ -203,7 +203,7 @@ RT_SYMBOLS = {
     "rt_dispatch_rows": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t]),
     "rt_dispatch_rows_fmt": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I]),
     "rt_dispatch_rows_ex": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, C.c_size_t, _I]),
-    "rt_sync": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
+    "rt_sync": (_I, [_P]), "rt_sync_frame": (_I, [_P]), "rt_read_image": (_I, [_P, _P, C.c_size_t, _I, _I]),
     "rt_device_image": (_I, [_P, _P, _P]),
     "rt_collect_stats": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
     "rt_collect_stats_ex": (_I, [_P, _I, _I, _I, _I, _I, _I, _P]),
@@ -646,6 +646,10 @@ class ComputeShader:
     def sync(self):
         self._chk(self._lib.rt_sync(self._h), "rt_sync")
 
+    def sync_frame(self):
+        """Waits for the last dispatch's frame (rt_sync_frame), not the renderer's order work behind it."""
+        self._chk(self._lib.rt_sync_frame(self._h), "rt_sync_frame")
+
     def read_image(self, width, height):
         out = np.empty((height, width, 4), np.float32)
         self._chk(self._lib.rt_read_image(self._h, _ptr(out), width * 16, width, height), "rt_read_image")
@@ -826,6 +830,12 @@ class ComputeShader:
         fn = self._lib.rt_debug_order_stream
         fn.argtypes = [_P, _I]
         self._chk(fn(self._h, int(mode)), "rt_debug_order_stream")
+
+    def debug_frame_event(self, on):
+        """Latency-mode cost frames record the event rt_sync_frame waits for (1) or not (0)."""
+        fn = self._lib.rt_debug_frame_event
+        fn.argtypes = [_P, _I]
+        self._chk(fn(self._h, int(on)), "rt_debug_frame_event")
 
     def debug_cost_dilate(self, r):
         """Cost order over each tile's largest cost within r tiles (0: off)."""

@@ -727,7 +727,8 @@ def test_moving_camera_cost_order_exact(ctx, order_stream):
     and a still camera after the moves (the still policy again) too. With the order's
     kernels on the order stream (rt_debug_order_stream 1, 2) the next dispatch waits for
     them on the device; mode 2 also with 12 frames in flight between waits (a torn order
-    would leave NaN tiles of the poisoned surfaces, or draw a tile twice)."""
+    would leave NaN tiles of the poisoned surfaces, or draw a tile twice). Each moving
+    frame is waited for by rt_sync_frame (its frame event, before the order's kernels)."""
     import bench
     W, H = 320, 180
     cfg, _, _, mb, _, target = bench.WORKLOADS[3]
@@ -765,7 +766,7 @@ def test_moving_camera_cost_order_exact(ctx, order_stream):
                 full.fill_(float("nan"))
                 torch.cuda.synchronize()  # the renderer's stream does not wait on torch's
                 ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
-                ctx.sync()
+                ctx.sync_frame()  # the frame's end: the cost order may still run behind it
                 img = full.cpu().numpy()
                 assert np.array_equal(img, refs[i]), f"round {rnd} camera {i}: {int((img != refs[i]).any(axis=-1).sum())} px"
         for _ in range(20):  # held still: the still policy's split frames

@@ -4,7 +4,7 @@ item 4): is a moving camera slower because its views cost more, or because the
 cost-ordered dispatch ranks tiles by an older view?
 
     python tools/camera_probe.py [--path orbit|dolly] [--samples 8] [--variants 16:0:-1,4:0:-1,1:0:-1]
-                                 [--order-stream 0|1|2]
+                                 [--order-stream 0|1|2] [--frame-event 0|1]
 
 From the C++ host loop (librthost.so rth_render_loop, latency mode on, as bench.py's
 serial frames):
@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--latency", type=int, default=1)
     ap.add_argument("--order-stream", type=int, default=None,
                     help="rt_debug_order_stream mode for every context (default: the library's)")
+    ap.add_argument("--frame-event", type=int, default=None,
+                    help="rt_debug_frame_event for every context (default: the library's)")
     a = ap.parse_args()
     import torch
     import bench
@@ -62,11 +64,13 @@ def main():
             ctx.debug_moving(*moving)
         if a.order_stream is not None:
             ctx.debug_order_stream(a.order_stream)
+        if a.frame_event is not None:
+            ctx.debug_frame_event(a.frame_event)
         return ctx
 
     idx = [int(round(k * n / a.samples)) % n for k in range(a.samples)]
     out = {"config": a.config, "path": a.path, "frames": n, "latency_mode": a.latency, "samples": idx,
-           "order_stream": a.order_stream}
+           "order_stream": a.order_stream, "frame_event": a.frame_event}
     ctx = fresh()
     still = []
     for i in idx:
