@@ -712,9 +712,10 @@ def main():
     # SURVEY §8(d)'s frame: upload + dispatch + completion, one at a time, FPS = 1 / median.
     # Each frame waits for its completion (the reference's loop, src/main.cpp:290-462), with
     # rt_set_latency_mode on: the setting for a host that waits for every frame.
-    # The host sees a frame's end through the renderer's own wait (rt_sync / the group's
-    # bounded rt_group_sync), which polls the stream instead of sleeping on the runtime's
-    # completion interrupt. Over rt_group every rank starts each frame after a barrier,
+    # The host sees a frame's end through the renderer's own wait (rt_sync_frame / the group's
+    # bounded rt_group_sync), which polls an event instead of sleeping on the runtime's
+    # completion interrupt; rt_sync_frame ends a latency-mode cost frame before the next
+    # frame's tile-order kernels, which run behind it on the same stream. Over rt_group every rank starts each frame after a barrier,
     # so rank 0's frame includes the slowest peer's stripes crossing its link.
     serial_frames = []
     # at least three cost-order periods (rt_set_schedule: every 16th frame) before the waited
@@ -730,7 +731,7 @@ def main():
             if grp is not None:
                 group_sync()
             else:
-                ctx.sync()
+                ctx.sync_frame()
 
         for i in range(wait_warmup):
             frame(i, 1)
