@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r06q
 export TMPDIR=/tmp
-tools/gpu_tests.sh > gpurun_out/r06q/tests.out 2>&1 || { tail -20 gpurun_out/r06q/tests.out; exit 1; }
+bash tools/gpu_tests.sh > gpurun_out/r06q/tests.out 2>&1 || { tail -20 gpurun_out/r06q/tests.out; exit 1; }
 cp gpurun_out/pytest_gpu.log gpurun_out/smoke.log gpurun_out/r06q/
 timeout -k 10 300 python bench.py > gpurun_out/r06q/bench_default.json 2> gpurun_out/r06q/bench_default.err || exit 1
 for cp in orbit dolly; do
