@@ -769,6 +769,10 @@ def test_moving_camera_cost_order_exact(ctx, order_stream):
                 ctx.sync_frame()  # the frame's end: the cost order may still run behind it
                 img = full.cpu().numpy()
                 assert np.array_equal(img, refs[i]), f"round {rnd} camera {i}: {int((img != refs[i]).any(axis=-1).sum())} px"
+        # the order the last moving frame queued behind its frame event: whole once the
+        # stream drains (rt_debug_sched_order synchronizes it)
+        tiles = ((W + 7) // 8) * ((H + 7) // 8)
+        assert np.array_equal(np.sort(ctx.debug_sched_order(tiles)), np.arange(tiles))
         for _ in range(20):  # held still: the still policy's split frames
             ctx.dispatch_rows(W, H, 0, 1, 1, H, full.data_ptr(), W * 16)
             ctx.sync()
